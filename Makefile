@@ -1,0 +1,36 @@
+# Build of libpgrt.so (gfx950 HIP kernels + C ABI) and the oracle (test infrastructure).
+# Usage: make -j8            (driven by __graft_entry__.build())
+HIPCC   ?= /opt/rocm/bin/hipcc
+ARCH    ?= gfx950
+BUILD   := build
+LIBDIR  := pgi_raytracing_amd/lib
+SRC     := pgi_raytracing_amd/csrc
+# -ffp-contract=off: no implicit FMA, so every float op rounds exactly like the CPU restatement
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off \
+            -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -I$(SRC) -Wall -Wno-unused-result
+OBJS := $(BUILD)/trace.o $(BUILD)/render.o $(BUILD)/bvh.o $(BUILD)/context.o $(BUILD)/objloader.o
+
+all: $(LIBDIR)/libpgrt.so oracle
+
+$(BUILD) $(LIBDIR):
+	mkdir -p $@
+
+HDRS := include/pgrt.h include/pgrt_detmath.h $(SRC)/common.hpp $(SRC)/trace.hpp $(SRC)/shade_ops.hpp
+
+$(BUILD)/%.o: $(SRC)/%.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/%.o: $(SRC)/%.cpp $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/libpgrt.so: $(OBJS) | $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf $(BUILD) $(LIBDIR)/libpgrt.so
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean

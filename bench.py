@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""Benchmark of the Whitted trace hot path (BASELINE.json metric: Mrays/s + ms/frame, avenger
+1920x1080 Whitted d=5, 1/2/4/8 GPU).
+
+One step = one frame of BASELINE config C2 (avenger-proxy, 1920x1080, 1 spp pinhole, Whitted
+depth 5, spherical env map) rendered into an HBM-resident framebuffer.  N > 1: one process
+per GPU (torch.distributed launcher env), 64x64 image tiles dealt round-robin to ranks, one
+ncclGather (RCCL over xGMI) to rank 0 and an unpack kernel there -- the total frame is fixed
+(strong scaling).  Rays = every closest-hit query (primary + shadow + reflect + refract).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+METRIC = "Mrays/sec + ms/frame, avenger 1920x1080 Whitted d=5, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# algorithmic bytes: ray in 32 B + hit out 16 B per ray, 64 B per BVH node
+# visited, 48 B per triangle tested (our triangle record: v0|id, e1, e2)
+RAY_BYTES, NODE_BYTES, TRI_BYTES = 48, 64, 48
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--max-level", type=int, default=5)
+    ap.add_argument("--spp-side", type=int, default=1)
+    ap.add_argument("--dof", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # control plane only; the frame gather is RCCL in libpgrt
+
+        dist.init_process_group("gloo", init_method="env://")
+    import scenes
+    from pgi_raytracing_amd import abi
+    from pgi_raytracing_amd.raytracer import Context, load_obj
+
+    if rank == 0 and not os.path.exists(scenes.AVENGER_OBJ):
+        scenes.write_avenger_proxy()
+    if dist:
+        dist.barrier()
+    scene = load_obj(scenes.AVENGER_OBJ)
+    scene.set_environment(os.path.join(ROOT, "assets", "spherical_map_windows.jpg"))
+    cam = abi.default_camera(args.width, args.height)
+    params = abi.make_params(spp_side=args.spp_side, max_level=args.max_level, dof=args.dof,
+                             jitter=abi.PGRT_JITTER_HASH if (args.spp_side > 1 or args.dof) else abi.PGRT_JITTER_NONE)
+    ctx = Context(local_rank)
+    ctx.set_scene(scene)
+    ctx.set_camera(cam)
+    bvh = ctx.bvh_info()
+    fb = ctx.alloc(args.width * args.height * 16) if rank == 0 or world == 1 else None
+    if world > 1:
+        uid = [Context.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ctx.comm_init(world, rank, uid[0])
+
+    def frame(p):
+        if world > 1:
+            return ctx.render_distributed_device(p, fb)
+        return ctx.render_device(p, fb)
+
+    for _ in range(args.warmup):
+        frame(params)
+    ctx.synchronize()
+    if dist:
+        dist.barrier()
+    rays = 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st = frame(params)
+        rays += st.rays()
+    ctx.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    total_rays = rays
+    if dist:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        r = torch.tensor([rays], dtype=torch.float64)
+        dist.all_reduce(r, op=dist.ReduceOp.SUM)
+        total_rays = int(r.item())
+
+    roof = None
+    if not args.no_roofline:
+        # live per-kernel timing: HIP events on libpgrt's own stream around every closest-hit
+        # launch (profile=1), and the instrumented traversal counts (profile=2, separate frame)
+        p1 = abi.RenderParams.from_buffer_copy(params)
+        p1.profile = 1
+        reps = 5
+        ms_trace = 0.0
+        launches = 0
+        for _ in range(reps):
+            s1 = frame(p1)
+            ms_trace += s1.ms_trace
+            launches += s1.trace_launches
+        p1.profile = 2
+        s2 = frame(p1)
+        frame_rays = s2.rays()
+        alg_bytes = RAY_BYTES * frame_rays + NODE_BYTES * s2.node_visits + TRI_BYTES * s2.tri_tests
+        avg_launch_ms = ms_trace / max(1, launches)
+        per_launch_bytes = alg_bytes / max(1, launches / reps)
+        achieved = per_launch_bytes / (avg_launch_ms * 1e-3) / 1e9
+        roof = {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "kernel": "k_trace<false> (closest hit)",
+            "avg_launch_ms": round(avg_launch_ms, 4),
+            "launches_per_frame": launches // reps,
+            "trace_ms_per_frame": round(ms_trace / reps, 4),
+            "node_visits_per_ray": round(s2.node_visits / max(1, frame_rays), 2),
+            "tri_tests_per_ray": round(s2.tri_tests / max(1, frame_rays), 2),
+            "bytes_per_ray": round(alg_bytes / max(1, frame_rays), 1),
+        }
+        tf = os.path.join(ROOT, "profiles", "traffic_c2.json")
+        if os.path.exists(tf):
+            try:
+                roof["traffic"] = json.load(open(tf)).get("bytes_per_launch")
+            except Exception:  # noqa: BLE001
+                pass
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle  # cpu_baseline leg only: the CPU restatement timed on the host cores
+
+        osc = pyoracle.OracleScene(scene)
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        step = 4  # every 4th row of the same frame: ~1/4 of the C2 work
+        t1 = time.perf_counter()
+        _, sc = osc.render(cam, params, row_step=step, threads=threads)
+        dt = time.perf_counter() - t1
+        cpu = {"value": round(sc.rays() / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+               "sample": f"every {step}th row of the C2 frame ({sc.rays()} rays, {dt:.2f} s), "
+                         f"oracle/ CPU restatement with its own SAH BVH, OpenMP"}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(total_rays / elapsed / 1e6, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: avenger-proxy OBJ (reference OBJ absent) + spherical_map_windows.jpg",
+            "config": {
+                "workload": f"C2 avenger-proxy {args.width}x{args.height} Whitted d={args.max_level} + env map, "
+                            f"{args.spp_side ** 2} spp {'DoF' if args.dof else 'pinhole'}",
+                "triangles": bvh.num_triangles,
+                "rays_per_frame": int(total_rays / args.steps),
+                "parallelism": f"image tiles 64x64 over {world} GPU(s), ncclGather to rank 0" if world > 1
+                else "1 GPU",
+            },
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,217 @@
+/* pgrt.h -- C ABI of the MI355X-native Whitted trace path (libpgrt.so).
+ *
+ * This is the drop-in boundary for the reference renderer src/pg/pg1_embree.  It replaces
+ * two reference interfaces (see INTEGRATION.md for the binding a maintainer adds):
+ *
+ *  (1) virtual Color4f SimpleGuiDX11::get_pixel(int x, int y, float t)
+ *        simpleguidx11.h:27, overridden at raytracer.h:32, implemented raytracer.cpp:396-437,
+ *        called per pixel by SimpleGuiDX11::Producer (simpleguidx11.cpp:105-118).
+ *      -> pgrt_render(): one call renders the whole frame (or a tile rect) into an RGBA float
+ *         framebuffer with the Producer's layout (row-major, top-down, 4 floats per pixel,
+ *         simpleguidx11.cpp:109-115).  The reference's get_pixel(x,y) is then a load from it.
+ *
+ *  (2) the Embree 3.11 scene / query API used by Raytracer::LoadScene and get_ray_hit
+ *        rtcNewScene/rtcNewGeometry/rtcSetNewGeometryBuffer/rtcCommitScene (raytracer.cpp:71-127)
+ *        rtcIntersect1 (raytracer.cpp:146; src/libs/embree/include/embree3/rtcore_scene.h:96)
+ *      -> pgrt_set_scene(): host arrays in, LBVH built on the device (Embree disappears);
+ *         pgrt_intersect_closest(): batched closest-hit query with rtcIntersect1 semantics.
+ *
+ * Conventions: every entry point returns PGRT_OK (0) or a negative PGRT_ERR_* code; no C++
+ * exception crosses the ABI; pgrt_last_error(ctx) describes the last failure on that context.
+ * One host thread per context; calls on one context are not reentrant.  Pointers are plain
+ * host pointers unless the name says _device.  Sizes are element counts.
+ */
+#ifndef PGRT_H_
+#define PGRT_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PGRT_ABI_VERSION 1
+
+#define PGRT_OK 0
+#define PGRT_ERR_INVALID_ARGUMENT (-1)
+#define PGRT_ERR_HIP (-2)
+#define PGRT_ERR_OUT_OF_MEMORY (-3)
+#define PGRT_ERR_NO_SCENE (-4)
+#define PGRT_ERR_NO_CAMERA (-5)
+#define PGRT_ERR_RCCL (-6)
+#define PGRT_ERR_IO (-7)
+#define PGRT_ERR_NO_DEVICE (-8)
+
+/* Material kinds (MTL "shader" key, objloader.cpp:135-138; only 4 is special-cased,
+ * raytracer.cpp:293-294).  Any other value shades with the Phong branch. */
+#define PGRT_MATERIAL_DIELECTRIC 4
+
+/* Index of refraction of air; rays start in air (material.h:15, raytracer.cpp:416). */
+#define PGRT_IOR_AIR 1.000293f
+
+/* Jitter modes for the stratified sample offsets r1,r2 (raytracer.cpp:407-410) and the lens
+ * offsets (PinHoleCamera.cpp:77-81).  The reference seeds std::mt19937 from the wall clock,
+ * which is not reproducible; these modes are counter-based and deterministic. */
+#define PGRT_JITTER_NONE 0            /* r1 = r2 = 0, lens offset 0 */
+#define PGRT_JITTER_HASH 1            /* independent hashed uniforms per (pixel, sample) */
+#define PGRT_JITTER_HASH_CORRELATED 2 /* lens uniforms == jitter uniforms, as when both
+                                         reference generators get the same microsecond seed */
+
+typedef struct pgrt_ctx pgrt_ctx;
+
+/* Material (material.h:34-125); fields the trace path reads. */
+typedef struct pgrt_material {
+    float diffuse[3];  /* Kd (RGB) */
+    float specular[3]; /* Ks (RGB) */
+    float shininess;   /* Ns */
+    float ior;         /* Ni */
+    int type;          /* "shader" */
+    int diffuse_tex;   /* index into pgrt_scene_desc.textures, -1 = none (map_Kd) */
+} pgrt_material;
+
+/* Decoded texture: raw BGR(A) bytes, top-down rows, `pitch` bytes per row, `bpp` bytes per
+ * pixel -- the layout Texture::Texture produces with FreeImage_ConvertToRawBits
+ * (texture.cpp:43-47). */
+typedef struct pgrt_texture {
+    int width, height, pitch, bpp;
+    const unsigned char* data;
+} pgrt_texture;
+
+/* Point light (LightSource.h; the ambient term is unused by the trace path). */
+typedef struct pgrt_light {
+    float position[3];
+    float diffuse[3];
+    float specular[3];
+} pgrt_light;
+
+/* Scene: de-indexed triangles (3 vertices per triangle, raytracer.cpp:96-120), the global
+ * triangle index is (surface offset + Embree primID) in surface attach order.  The library
+ * copies everything to HBM; the caller keeps ownership of the arrays. */
+typedef struct pgrt_scene_desc {
+    int num_triangles;
+    const float* positions;   /* 9*N: v0.xyz v1.xyz v2.xyz          (vertex buffer)      */
+    const float* normals;     /* 9*N: per-vertex normals           (attribute slot 0)   */
+    const float* uvs;         /* 6*N: per-vertex (u,v)             (attribute slot 1)   */
+    const int* material_ids;  /* N:   index into materials          (geometry user data) */
+    int num_materials;
+    const pgrt_material* materials;
+    int num_textures;
+    const pgrt_texture* textures;
+    int env_texture;          /* SphericalMap texture (index into textures), -1 = black */
+    int num_lights;
+    const pgrt_light* lights;
+} pgrt_scene_desc;
+
+/* PinHoleCamera(width, height, fov_y, view_from, view_at) (PinHoleCamera.cpp:5-29). */
+typedef struct pgrt_camera {
+    int width, height;
+    float fov_y; /* radians */
+    float from[3], at[3], up[3];
+} pgrt_camera;
+
+/* Per-frame parameters.  Reference values: spp_side 3, max_level 7, dof 1, focal 200,
+ * aperture 5, gamma 0.5 (raytracer.cpp:398-400,282; UI default :450,464-465). */
+typedef struct pgrt_render_params {
+    int spp_side;         /* S: S*S stratified samples per pixel */
+    int max_level;        /* d: rays at level >= d are intersected but shaded black (:282) */
+    int dof;              /* 0: pinhole generate_ray(x,y), 1: thin-lens generate_ray(...,f,a) */
+    float focal_distance; /* DoF focal distance */
+    float aperture;       /* DoF square aperture side */
+    float gamma_level;    /* Raytracer::gamma exponent (applied twice) */
+    int jitter;           /* PGRT_JITTER_* */
+    uint32_t seed;
+    uint32_t frame;
+    int rect_x, rect_y, rect_w, rect_h; /* sub-rectangle; rect_w==0 -> full frame */
+    int profile;          /* 0 off, 1 per-stage HIP-event timing, 2 + traversal counters */
+} pgrt_render_params;
+
+typedef struct pgrt_stats {
+    uint64_t rays_primary, rays_shadow, rays_reflect, rays_refract;
+    uint64_t node_visits, tri_tests; /* only with profile == 2 */
+    double ms_total;                 /* host wall time of the call */
+    double ms_raygen, ms_trace, ms_shade, ms_shadow, ms_combine, ms_resolve, ms_gather;
+    int trace_launches;              /* launches of the closest-hit kernel in ms_trace */
+    int levels;                      /* trace levels executed */
+    int overflow_retries;            /* queue re-sizings this call */
+} pgrt_stats;
+
+typedef struct pgrt_bvh_info {
+    int num_triangles, num_nodes, max_depth;
+    double build_ms;
+    float scene_lo[3], scene_hi[3];
+    size_t device_bytes;
+} pgrt_bvh_info;
+
+/* ---- context ---- */
+const char* pgrt_version(void);
+int pgrt_device_count(int* count);
+int pgrt_create(int hip_device, pgrt_ctx** out);
+void pgrt_destroy(pgrt_ctx* ctx);
+const char* pgrt_last_error(const pgrt_ctx* ctx);
+
+/* ---- scene / camera (replaces Raytracer::LoadScene's Embree upload, raytracer.cpp:71-127,
+ *      and the PinHoleCamera ctor, PinHoleCamera.cpp:5-29) ---- */
+int pgrt_set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* scene);
+int pgrt_bvh_get_info(const pgrt_ctx* ctx, pgrt_bvh_info* info);
+int pgrt_set_camera(pgrt_ctx* ctx, const pgrt_camera* cam);
+
+/* ---- frame (replaces get_pixel for every pixel of the Producer loop) ---- */
+int pgrt_render(pgrt_ctx* ctx, const pgrt_render_params* p, float* rgba_host, pgrt_stats* st);
+/* Same, output left in device memory (rgba_device: W*H*4 floats, or rect_w*rect_h*4). */
+int pgrt_render_device(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device,
+                       pgrt_stats* st);
+/* Device buffer helpers for callers without their own allocator (bench, tests). */
+int pgrt_device_alloc(pgrt_ctx* ctx, size_t bytes, void** out);
+int pgrt_device_free(pgrt_ctx* ctx, void* ptr);
+int pgrt_copy_to_host(pgrt_ctx* ctx, void* dst_host, const void* src_device, size_t bytes);
+int pgrt_synchronize(pgrt_ctx* ctx);
+
+/* ---- batched closest-hit query with rtcIntersect1 semantics ----
+ * rays: n x 8 floats {org.xyz, tnear, dir.xyz, tfar}; hits: n x 4 {t, u, v, prim} where prim
+ * is the global triangle index stored as int32 bits, -1 on a miss (t = tfar, u = v = 0). */
+int pgrt_intersect_closest(pgrt_ctx* ctx, const float* rays, int n, float* hits);
+
+/* ---- multi-GPU image tiles (one process per GPU, RCCL over xGMI) ----
+ * Tiles are tile_size x tile_size, numbered row-major; tile t belongs to rank t % world. */
+int pgrt_tile_count(int width, int height, int tile_size, int rank, int world);
+int pgrt_tile_rect(int width, int height, int tile_size, int tile_index, int rect[4]);
+/* Unpack a rank-major gathered tile buffer (every rank's tiles, each tile tile_size^2 * 4
+ * floats, padded) into a W x H RGBA framebuffer.  Host reference of the device unpack. */
+int pgrt_unpack_tiles_host(int width, int height, int tile_size, int world,
+                           const float* gathered, float* rgba);
+int pgrt_comm_unique_id(char id[128]);
+int pgrt_comm_init(pgrt_ctx* ctx, int world, int rank, const char id[128]);
+/* Render this rank's tiles, gather them on rank 0 with one ncclGather, unpack on device.
+ * rgba_host (rank 0 only, may be NULL elsewhere): W*H*4 floats. */
+int pgrt_render_distributed(pgrt_ctx* ctx, const pgrt_render_params* p, float* rgba_host,
+                            pgrt_stats* st);
+/* Same, framebuffer left on rank 0's device (W*H*4 floats). */
+int pgrt_render_distributed_device(pgrt_ctx* ctx, const pgrt_render_params* p,
+                                   void* rgba_device, pgrt_stats* st);
+
+/* ---- scene ingest (LoadOBJ / LoadMTL, objloader.cpp:53-507; host only) ----
+ * Texture files named by map_Kd are NOT decoded here: their paths are reported so the caller
+ * decodes them (FreeImage is not available) and fills pgrt_texture entries. */
+typedef struct pgrt_obj pgrt_obj;
+int pgrt_obj_load(const char* obj_path, int flip_yz, pgrt_obj** out);
+void pgrt_obj_free(pgrt_obj* obj);
+const char* pgrt_obj_error(void);
+/* Fills desc with pointers owned by obj (textures/env/lights left empty for the caller). */
+int pgrt_obj_scene(const pgrt_obj* obj, pgrt_scene_desc* desc);
+int pgrt_obj_counts(const pgrt_obj* obj, int* num_surfaces, int* num_materials,
+                    int* num_textures);
+const char* pgrt_obj_texture_path(const pgrt_obj* obj, int i);
+const char* pgrt_obj_material_name(const pgrt_obj* obj, int i);
+int pgrt_obj_surface_range(const pgrt_obj* obj, int i, int* first_triangle, int* count);
+
+/* ---- test hook: evaluates the shared math of pgrt_detmath.h on the device.  in: n (a,b)
+ *      pairs; out: n x 8 {sqrtf(a), a/b, powf(a,b), expf(a), atan2f(a,b), asinf(a),
+ *      1/sqrtf(a), (float)pow((double)a,(double)b)} ---- */
+int pgrt_selftest_math(pgrt_ctx* ctx, const float* in_pairs, int n, float* out8);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PGRT_H_ */

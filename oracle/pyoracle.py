@@ -1,0 +1,170 @@
+"""ctypes wrapper of liboracle.so (the CPU restatement) -- TEST INFRASTRUCTURE ONLY.
+
+Imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, never by the
+product package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+from pgi_raytracing_amd import abi  # noqa: E402  (struct layouts only)
+
+_LIBS = {}
+
+
+def lib(libm: bool = False):
+    name = "liboracle_libm.so" if libm else "liboracle.so"
+    if name not in _LIBS:
+        path = os.path.join(HERE, "_build", name)
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run `make -C oracle` (or __graft_entry__.build())")
+        L = C.CDLL(path)
+        L.orc_scene_create.restype = C.c_void_p
+        L.orc_scene_create.argtypes = [C.POINTER(abi.SceneDesc), C.c_int]
+        L.orc_scene_destroy.argtypes = [C.c_void_p]
+        L.orc_render.argtypes = [C.c_void_p, C.POINTER(abi.Camera), C.POINTER(abi.RenderParams), C.c_int,
+                                 C.c_int, C.POINTER(C.c_float), C.POINTER(abi.Stats)]
+        L.orc_intersect.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_float)]
+        L.orc_camera_basis.argtypes = [C.POINTER(abi.Camera), C.POINTER(C.c_float)]
+        L.orc_generate_ray.argtypes = [C.POINTER(abi.Camera), C.c_float, C.c_float, C.c_int, C.c_float,
+                                       C.c_float, C.c_float, C.c_float, C.POINTER(C.c_float)]
+        L.orc_get_texel.argtypes = [C.POINTER(abi.Texture), C.c_float, C.c_float, C.POINTER(C.c_float)]
+        L.orc_env_texel.argtypes = [C.POINTER(abi.Texture), C.c_float, C.c_float, C.c_float,
+                                    C.POINTER(C.c_float)]
+        L.orc_mix_srgb.argtypes = [C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_float, C.POINTER(C.c_float)]
+        L.orc_gamma.argtypes = [C.POINTER(C.c_float), C.c_float, C.POINTER(C.c_float)]
+        L.orc_compress.restype = C.c_float
+        L.orc_compress.argtypes = [C.c_float]
+        L.orc_expand.restype = C.c_float
+        L.orc_expand.argtypes = [C.c_float]
+        L.orc_jitter.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_float)]
+        L.orc_uses_libm.restype = C.c_int
+        _LIBS[name] = L
+    return _LIBS[name]
+
+
+class OracleScene:
+    def __init__(self, scene, accel: int = 1, libm: bool = False):
+        self.L = lib(libm)
+        self.desc = scene.desc()
+        self._scene = scene
+        self.h = self.L.orc_scene_create(C.byref(self.desc), accel)
+        if not self.h:
+            raise RuntimeError("orc_scene_create failed")
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            self.L.orc_scene_destroy(h)
+            self.h = None
+
+    def render(self, cam, params, row_step: int = 1, threads: int = 0):
+        w = params.rect_w if params.rect_w > 0 else cam.width
+        h = params.rect_h if params.rect_h > 0 else cam.height
+        out = np.zeros((h, w, 4), np.float32)
+        st = abi.Stats()
+        rc = self.L.orc_render(self.h, C.byref(cam), C.byref(params), row_step, threads,
+                               out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(st))
+        if rc != 0:
+            raise RuntimeError(f"orc_render -> {rc}")
+        return out, st
+
+    def intersect(self, rays: np.ndarray) -> np.ndarray:
+        rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+        hits = np.zeros((rays.shape[0], 4), np.float32)
+        rc = self.L.orc_intersect(self.h, abi.fptr(rays), rays.shape[0], abi.fptr(hits))
+        if rc != 0:
+            raise RuntimeError(f"orc_intersect -> {rc}")
+        return hits
+
+
+def fvec(*xs):
+    return (C.c_float * len(xs))(*xs)
+
+
+def camera_basis(cam):
+    out = (C.c_float * 10)()
+    lib().orc_camera_basis(C.byref(cam), out)
+    return np.array(out[:], np.float32)
+
+
+def generate_ray(cam, x, y, dof=0, focal=200.0, aperture=5.0, r1=0.0, r2=0.0):
+    out = (C.c_float * 9)()
+    lib().orc_generate_ray(C.byref(cam), x, y, dof, focal, aperture, r1, r2, out)
+    return np.array(out[:], np.float32)
+
+
+def get_texel(tex, u, v, libm=False):
+    out = (C.c_float * 3)()
+    t = tex.to_c()
+    lib(libm).orc_get_texel(C.byref(t), u, v, out)
+    return np.array(out[:], np.float32)
+
+
+def env_texel(tex, x, y, z, libm=False):
+    out = (C.c_float * 4)()
+    t = tex.to_c()
+    lib(libm).orc_env_texel(C.byref(t), x, y, z, out)
+    return np.array(out[:], np.float32)
+
+
+def mix_srgb(c0, c1, a, libm=False):
+    out = (C.c_float * 4)()
+    lib(libm).orc_mix_srgb(fvec(*c0), fvec(*c1), a, out)
+    return np.array(out[:], np.float32)
+
+
+def gamma(c, g, libm=False):
+    out = (C.c_float * 4)()
+    lib(libm).orc_gamma(fvec(*c), g, out)
+    return np.array(out[:], np.float32)
+
+
+def scene_from_obj_ref(obj_path: str, env_path: str | None = None, flip_yz: bool = False):
+    """Build a Scene with the Python restatement of LoadOBJ (tests cross-check the product
+    loader against this)."""
+    from pgi_raytracing_amd.scene import LightData, MaterialData, Scene, TextureData
+
+    from objloader_ref import load_obj  # type: ignore
+
+    surfaces, mats = load_obj(obj_path, flip_yz)
+    textures, tex_index = [], {}
+    mds = []
+    for m in mats:
+        ti = -1
+        if m["map_kd"]:
+            if m["map_kd"] not in tex_index:
+                tex_index[m["map_kd"]] = len(textures)
+                textures.append(TextureData.from_file(m["map_kd"]))
+            ti = tex_index[m["map_kd"]]
+        mds.append(MaterialData(m["name"], tuple(m["diffuse"]), tuple(m["specular"]), m["shininess"],
+                                m["ior"], m["type"], ti))
+    default_mat = len(mds)
+    mds.append(MaterialData())
+    pos, nrm, uv, mid, surf = [], [], [], [], []
+    first = 0
+    for s in surfaces:
+        T = s["positions"].shape[0]
+        pos.append(s["positions"].reshape(-1))
+        nrm.append(s["normals"].reshape(-1))
+        uv.append(s["uvs"].reshape(-1))
+        mid.append(np.full(T, s["material"] if s["material"] >= 0 else default_mat, np.int32))
+        surf.append((s["name"], first, T))
+        first += T
+    sc = Scene(np.concatenate(pos), np.concatenate(nrm), np.concatenate(uv), np.concatenate(mid), mds, textures,
+               -1, [LightData()], surf)
+    if env_path:
+        sc.set_environment(env_path)
+    return sc
+
+
+sys.path.insert(0, HERE)

@@ -1,0 +1,124 @@
+// common.hpp -- shared host/device definitions for libpgrt (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+
+#include "pgrt.h"
+#include "pgrt_detmath.h"
+
+namespace pgrt {
+
+// Error carried from deep inside the library to the C ABI (never crosses it).
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define PGRT_HIP(call)                                                                        \
+    do {                                                                                      \
+        hipError_t e_ = (call);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            throw ::pgrt::Error(PGRT_ERR_HIP, std::string(#call " failed: ") +                \
+                                                  hipGetErrorString(e_) + " at " __FILE__ ":" + \
+                                                  std::to_string(__LINE__));                  \
+    } while (0)
+
+#define PGRT_REQUIRE(cond, code, msg)                     \
+    do {                                                  \
+        if (!(cond)) throw ::pgrt::Error((code), (msg)); \
+    } while (0)
+
+// Device buffer owned by the context (RAII, no exceptions in the destructor).
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    void alloc(size_t count) {
+        if (count <= n && p) return;
+        release();
+        if (count == 0) count = 1;
+        hipError_t e = hipMalloc(&p, count * sizeof(T));
+        if (e != hipSuccess) {
+            p = nullptr;
+            throw Error(PGRT_ERR_OUT_OF_MEMORY, "hipMalloc of " + std::to_string(count * sizeof(T)) +
+                                                    " bytes failed: " + hipGetErrorString(e));
+        }
+        n = count;
+    }
+    size_t bytes() const { return n * sizeof(T); }
+};
+
+// ---- device-side scene layout (HBM) -------------------------------------------------------
+
+struct DevMaterial {  // 48 B, read through the scalar/vector cache
+    float kd[3];
+    float ks[3];
+    float ns, ior;
+    int type, tex;
+    int pad[2];
+};
+
+struct DevTexture {
+    int width, height, pitch, bpp;
+    long long offset;  // into the texel pool
+    long long size;    // pitch * height
+};
+
+struct DevLight {
+    float pos[3], kd[3], ks[3];
+};
+
+// BVH2 node, 64 B: both child boxes live in the parent (Aila-Laine layout).
+//   a = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)   b = (c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y)
+//   c = (c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z)   d = (child0, child1, -, -)
+// child >= 0: internal node index; child < 0: leaf = 0x80000000 | (count-1) << 27 | first.
+struct BvhNode {
+    float4 a, b, c;
+    int4 d;
+};
+
+constexpr int kLeafMaxTris = 4;
+__host__ __device__ inline int leaf_encode(int first, int count) {
+    return (int)(0x80000000u | ((unsigned)(count - 1) << 27) | (unsigned)first);
+}
+__host__ __device__ inline int leaf_first(int c) { return (int)((unsigned)c & 0x07ffffffu); }
+__host__ __device__ inline int leaf_count(int c) { return (int)(((unsigned)c >> 27) & 0xfu) + 1; }
+
+struct SceneView {  // kernel-argument view of the device scene
+    const float4* tri;     // 3 x float4 per sorted triangle: (v0, orig id bits) (e1) (e2)
+    const BvhNode* nodes;
+    int root;              // node index, or a leaf code for tiny scenes
+    int ntri;
+    const float* attr;     // 16 floats per ORIGINAL triangle: n0 n1 n2 uv0 uv1 uv2, mat (bits)
+    const DevMaterial* mats;
+    const DevTexture* tex;
+    const unsigned char* texels;
+    int env;
+    int nlight;
+    const DevLight* lights;
+};
+
+struct CameraView {
+    int width, height;
+    float fy;
+    float from[3];
+    float m[9];  // row-major; columns x_c, y_c, z_c
+};
+
+inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace pgrt

@@ -1,0 +1,825 @@
+// context.cpp -- frame driver and C ABI (include/pgrt.h) of libpgrt.
+//
+// Replaces SimpleGuiDX11::Producer's serial y/x loop over Raytracer::get_pixel
+// (APP/simpleguidx11.cpp:95-125, APP/raytracer.cpp:396-437) with one wavefront pass per
+// sample batch on one HIP stream, and Embree's scene API (APP/raytracer.cpp:71-127) with an
+// on-device LBVH.  No exception crosses the ABI: every entry point returns a PGRT_* code and
+// records a message readable with pgrt_last_error().
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "trace.hpp"
+
+using namespace pgrt;
+
+namespace {
+
+constexpr long long kMaxBatchRays = 16ll << 20;  // level-0 rays per sample batch
+constexpr int kTraceGridThreads = 2048 * 256;    // persistent trace grid (global overflow stacks)
+
+struct StageTimer {
+    struct Rec {
+        hipEvent_t a, b;
+        int cat;
+    };
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> pool;
+    bool on = false;
+    hipEvent_t get() {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e;
+        PGRT_HIP(hipEventCreate(&e));
+        return e;
+    }
+    int begin(hipStream_t s, int cat) {
+        if (!on) return -1;
+        Rec r{get(), get(), cat};
+        PGRT_HIP(hipEventRecord(r.a, s));
+        recs.push_back(r);
+        return (int)recs.size() - 1;
+    }
+    void end(hipStream_t s, int id) {
+        if (id >= 0) PGRT_HIP(hipEventRecord(recs[id].b, s));
+    }
+    void collect(double* ms) {  // after stream sync
+        for (auto& r : recs) {
+            float t = 0;
+            PGRT_HIP(hipEventElapsedTime(&t, r.a, r.b));
+            ms[r.cat] += t;
+            pool.push_back(r.a);
+            pool.push_back(r.b);
+        }
+        recs.clear();
+    }
+    ~StageTimer() {
+        for (auto& r : recs) {
+            (void)hipEventDestroy(r.a);
+            (void)hipEventDestroy(r.b);
+        }
+        for (auto e : pool) (void)hipEventDestroy(e);
+    }
+};
+
+enum { CAT_RAYGEN, CAT_TRACE, CAT_SHADE, CAT_SHADOW, CAT_COMBINE, CAT_RESOLVE, CAT_GATHER, CAT_N };
+
+}  // namespace
+
+struct pgrt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // scene
+    DevBuf<float4> tri;
+    DevBuf<BvhNode> nodes;
+    DevBuf<float> attr;
+    DevBuf<DevMaterial> mats;
+    DevBuf<DevTexture> texd;
+    DevBuf<unsigned char> texels;
+    DevBuf<DevLight> lights;
+    SceneView view{};
+    bool has_scene = false;
+    pgrt_bvh_info info{};
+
+    CameraView cam{};
+    bool has_cam = false;
+
+    // frame state
+    DevBuf<int4> tiles;
+    DevBuf<float4> q_ro[2], q_rd[2], q_hit[2];
+    DevBuf<float> q_time[2];
+    int q_cap = 0;
+    std::vector<std::unique_ptr<DevBuf<float4>>> n_color, n_att;
+    std::vector<std::unique_ptr<DevBuf<int4>>> n_link;
+    std::vector<int> level_cap;
+    DevBuf<float4> s_ro, s_rd, s_hit, s_contrib;
+    int s_cap = 0;
+    DevBuf<FrameCounters> fc;
+    DevBuf<float4> accum;
+    DevBuf<int> gstack;
+    DevBuf<float> out_tmp;
+    StageTimer timer;
+
+    // multi-GPU
+    ncclComm_t comm = nullptr;
+    int world = 1, rank = 0;
+    DevBuf<float> tilebuf, gathered, fb_dev;
+
+    ~pgrt_ctx() {
+        if (comm) (void)ncclCommDestroy(comm);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace {
+
+template <class F>
+int guarded(pgrt_ctx* ctx, F&& f) {
+    try {
+        if (ctx) {
+            PGRT_HIP(hipSetDevice(ctx->device));
+        }
+        f();
+        return PGRT_OK;
+    } catch (const Error& e) {
+        if (ctx) ctx->err = e.what();
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        if (ctx) ctx->err = "host out of memory";
+        return PGRT_ERR_OUT_OF_MEMORY;
+    } catch (const std::exception& e) {
+        if (ctx) ctx->err = e.what();
+        return PGRT_ERR_INVALID_ARGUMENT;
+    }
+}
+
+// PinHoleCamera::PinHoleCamera (APP/PinHoleCamera.cpp:5-29), evaluated on the host in float.
+CameraView make_camera(const pgrt_camera& c) {
+    auto norm = [](float v[3]) {
+        const float n = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+        if (n != 0) {
+            const float rn = 1 / std::sqrt(n);
+            v[0] *= rn;
+            v[1] *= rn;
+            v[2] *= rn;
+        }
+    };
+    auto cross = [](const float a[3], const float b[3], float o[3]) {
+        o[0] = a[1] * b[2] - a[2] * b[1];
+        o[1] = a[2] * b[0] - a[0] * b[2];
+        o[2] = a[0] * b[1] - a[1] * b[0];
+    };
+    CameraView k{};
+    k.width = c.width;
+    k.height = c.height;
+    k.fy = (float)c.height / (2 * tanf(c.fov_y / 2));
+    for (int i = 0; i < 3; ++i) k.from[i] = c.from[i];
+    float z[3] = {c.from[0] - c.at[0], c.from[1] - c.at[1], c.from[2] - c.at[2]};
+    float x[3], y[3];
+    cross(c.up, z, x);
+    cross(z, x, y);
+    norm(z);
+    norm(x);
+    norm(y);
+    k.m[0] = x[0]; k.m[1] = y[0]; k.m[2] = z[0];
+    k.m[3] = x[1]; k.m[4] = y[1]; k.m[5] = z[1];
+    k.m[6] = x[2]; k.m[7] = y[2]; k.m[8] = z[2];
+    return k;
+}
+
+void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
+    PGRT_REQUIRE(d != nullptr, PGRT_ERR_INVALID_ARGUMENT, "scene descriptor is NULL");
+    const int n = d->num_triangles;
+    PGRT_REQUIRE(n > 0 && n < (1 << 27), PGRT_ERR_INVALID_ARGUMENT, "num_triangles must be in [1, 2^27)");
+    PGRT_REQUIRE(d->positions && d->normals && d->uvs && d->material_ids, PGRT_ERR_INVALID_ARGUMENT,
+                 "triangle arrays must be non-NULL");
+    PGRT_REQUIRE(d->num_materials > 0 && d->materials, PGRT_ERR_INVALID_ARGUMENT, "at least one material required");
+    PGRT_REQUIRE(d->num_lights >= 0 && d->num_lights <= 64 && (d->num_lights == 0 || d->lights),
+                 PGRT_ERR_INVALID_ARGUMENT, "num_lights must be in [0, 64]");
+    PGRT_REQUIRE(d->num_textures >= 0 && (d->num_textures == 0 || d->textures), PGRT_ERR_INVALID_ARGUMENT,
+                 "bad texture table");
+    PGRT_REQUIRE(d->env_texture < d->num_textures, PGRT_ERR_INVALID_ARGUMENT, "env_texture out of range");
+    auto t0 = std::chrono::steady_clock::now();
+    hipStream_t st = ctx->stream;
+    ctx->has_scene = false;
+
+    // materials / textures / lights (host-side packing, small)
+    std::vector<DevMaterial> mats(d->num_materials);
+    for (int i = 0; i < d->num_materials; ++i) {
+        const pgrt_material& m = d->materials[i];
+        DevMaterial& o = mats[i];
+        for (int k = 0; k < 3; ++k) {
+            o.kd[k] = m.diffuse[k];
+            o.ks[k] = m.specular[k];
+        }
+        o.ns = m.shininess;
+        o.ior = m.ior;
+        o.type = m.type;
+        o.tex = m.diffuse_tex;
+        PGRT_REQUIRE(m.diffuse_tex < d->num_textures, PGRT_ERR_INVALID_ARGUMENT, "diffuse_tex out of range");
+    }
+    std::vector<DevTexture> texs(std::max(1, d->num_textures));
+    long long pool = 0;
+    for (int i = 0; i < d->num_textures; ++i) {
+        const pgrt_texture& t = d->textures[i];
+        PGRT_REQUIRE(t.width > 0 && t.height > 0 && t.bpp >= 3 && t.pitch >= t.width * t.bpp && t.data,
+                     PGRT_ERR_INVALID_ARGUMENT, "bad texture " + std::to_string(i));
+        texs[i] = DevTexture{t.width, t.height, t.pitch, t.bpp, pool, (long long)t.pitch * t.height};
+        pool += ((long long)t.pitch * t.height + 255) / 256 * 256;
+    }
+    std::vector<DevLight> lights(std::max(1, d->num_lights));
+    for (int i = 0; i < d->num_lights; ++i)
+        for (int k = 0; k < 3; ++k) {
+            lights[i].pos[k] = d->lights[i].position[k];
+            lights[i].kd[k] = d->lights[i].diffuse[k];
+            lights[i].ks[k] = d->lights[i].specular[k];
+        }
+    // per-triangle shading attributes in original order: n0 n1 n2 uv0 uv1 uv2 material
+    std::vector<float> attr((size_t)n * 16);
+    float lo[3] = {3.4e38f, 3.4e38f, 3.4e38f}, hi[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+    for (int i = 0; i < n; ++i) {
+        float* a = &attr[(size_t)i * 16];
+        std::memcpy(a, d->normals + (size_t)i * 9, 9 * sizeof(float));
+        std::memcpy(a + 9, d->uvs + (size_t)i * 6, 6 * sizeof(float));
+        int mid = d->material_ids[i];
+        if (mid < 0 || mid >= d->num_materials) mid = 0;  // see DESIGN.md: NULL surface material
+        std::memcpy(a + 15, &mid, sizeof(int));
+        for (int v = 0; v < 9; ++v) {
+            const float p = d->positions[(size_t)i * 9 + v];
+            lo[v % 3] = std::min(lo[v % 3], p);
+            hi[v % 3] = std::max(hi[v % 3], p);
+        }
+    }
+    float ext = 0;
+    for (int k = 0; k < 3; ++k) ext = std::max(ext, hi[k] - lo[k]);
+    PGRT_REQUIRE(std::isfinite(ext), PGRT_ERR_INVALID_ARGUMENT, "non-finite vertex positions");
+    const float pad = 1e-5f * ext + 1e-30f;
+
+    ctx->attr.alloc(attr.size());
+    PGRT_HIP(hipMemcpyAsync(ctx->attr.p, attr.data(), attr.size() * sizeof(float), hipMemcpyHostToDevice, st));
+    ctx->mats.alloc(mats.size());
+    PGRT_HIP(hipMemcpyAsync(ctx->mats.p, mats.data(), mats.size() * sizeof(DevMaterial), hipMemcpyHostToDevice, st));
+    ctx->texd.alloc(texs.size());
+    PGRT_HIP(hipMemcpyAsync(ctx->texd.p, texs.data(), texs.size() * sizeof(DevTexture), hipMemcpyHostToDevice, st));
+    ctx->texels.alloc((size_t)std::max(1ll, pool));
+    for (int i = 0; i < d->num_textures; ++i)
+        PGRT_HIP(hipMemcpyAsync(ctx->texels.p + texs[i].offset, d->textures[i].data, (size_t)texs[i].size,
+                                hipMemcpyHostToDevice, st));
+    ctx->lights.alloc(lights.size());
+    PGRT_HIP(hipMemcpyAsync(ctx->lights.p, lights.data(), lights.size() * sizeof(DevLight), hipMemcpyHostToDevice, st));
+
+    // positions -> device, LBVH build on device
+    DevBuf<float> pos;
+    pos.alloc((size_t)n * 9);
+    PGRT_HIP(hipMemcpyAsync(pos.p, d->positions, (size_t)n * 9 * sizeof(float), hipMemcpyHostToDevice, st));
+    ctx->tri.alloc((size_t)n * 3);
+    ctx->nodes.alloc((size_t)std::max(1, n - 1));
+    DevBuf<int> scratch;
+    scratch.alloc(lbvh_scratch_ints(n));
+    const size_t tmp_bytes = lbvh_sort_temp_bytes(n);
+    DevBuf<unsigned char> sort_tmp;
+    sort_tmp.alloc(tmp_bytes);
+    BuildOut bo{};
+    auto tb = std::chrono::steady_clock::now();
+    build_lbvh(pos.p, n, ctx->tri.p, ctx->nodes.p, scratch.p, sort_tmp.p, tmp_bytes, pad, &bo, st);
+    auto te = std::chrono::steady_clock::now();
+    PGRT_REQUIRE(bo.max_depth <= 32 + kGlobalStack - 2, PGRT_ERR_INVALID_ARGUMENT,
+                 "BVH depth " + std::to_string(bo.max_depth) + " exceeds the traversal stack");
+
+    SceneView& v = ctx->view;
+    v.tri = ctx->tri.p;
+    v.nodes = ctx->nodes.p;
+    v.root = bo.root;
+    v.ntri = n;
+    v.attr = ctx->attr.p;
+    v.mats = ctx->mats.p;
+    v.tex = ctx->texd.p;
+    v.texels = ctx->texels.p;
+    v.env = d->env_texture;
+    v.nlight = d->num_lights;
+    v.lights = ctx->lights.p;
+    ctx->has_scene = true;
+    pgrt_bvh_info& bi = ctx->info;
+    bi.num_triangles = n;
+    bi.num_nodes = bo.num_nodes;
+    bi.max_depth = bo.max_depth;
+    bi.build_ms = std::chrono::duration<double, std::milli>(te - tb).count();
+    for (int k = 0; k < 3; ++k) {
+        bi.scene_lo[k] = lo[k];
+        bi.scene_hi[k] = hi[k];
+    }
+    bi.device_bytes = ctx->tri.bytes() + ctx->nodes.bytes() + ctx->attr.bytes() + ctx->texels.bytes();
+    (void)t0;
+}
+
+void ensure_frame_buffers(pgrt_ctx* ctx, int n0, int levels) {
+    if (ctx->q_cap < n0) {
+        for (int b = 0; b < 2; ++b) {
+            ctx->q_ro[b].alloc(n0);
+            ctx->q_rd[b].alloc(n0);
+            ctx->q_hit[b].alloc(n0);
+            ctx->q_time[b].alloc(n0);
+        }
+        ctx->q_cap = n0;
+    }
+    if ((int)ctx->level_cap.size() < levels) ctx->level_cap.resize(levels, 0);
+    while ((int)ctx->n_color.size() < levels) {
+        ctx->n_color.emplace_back(new DevBuf<float4>());
+        ctx->n_att.emplace_back(new DevBuf<float4>());
+        ctx->n_link.emplace_back(new DevBuf<int4>());
+    }
+    for (int L = 0; L < levels; ++L) {
+        const int cap = std::max(L == 0 ? n0 : std::min(ctx->q_cap, std::max(ctx->level_cap[L], n0)), 1);
+        if (ctx->level_cap[L] < cap || (int)ctx->n_color[L]->n < cap) {
+            ctx->n_color[L]->alloc(cap);
+            ctx->n_att[L]->alloc(cap);
+            ctx->n_link[L]->alloc(cap);
+            ctx->level_cap[L] = cap;
+        }
+    }
+    const int nl = std::max(1, ctx->view.nlight);
+    if (ctx->s_cap < n0 * nl) {
+        const int sc = n0 * nl;
+        ctx->s_ro.alloc(sc);
+        ctx->s_rd.alloc(sc);
+        ctx->s_hit.alloc(sc);
+        ctx->s_contrib.alloc(sc);
+        ctx->s_cap = sc;
+    }
+    ctx->fc.alloc(1);
+    if (ctx->gstack.n == 0) ctx->gstack.alloc((size_t)kTraceGridThreads * kGlobalStack);
+}
+
+// Render the pixels of `tiles` (each <= kTile x kTile); out_mode 0 writes a framebuffer
+// (origin ox,oy, pitch in pixels), 1 writes tile-compact buffers.  Device pointer output.
+void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<int4>& tiles, float* out,
+                  int out_mode, int ox, int oy, int pitch, pgrt_stats* st) {
+    PGRT_REQUIRE(ctx->has_scene, PGRT_ERR_NO_SCENE, "pgrt_set_scene has not been called");
+    PGRT_REQUIRE(ctx->has_cam, PGRT_ERR_NO_CAMERA, "pgrt_set_camera has not been called");
+    PGRT_REQUIRE(p->spp_side >= 1 && p->spp_side <= 64, PGRT_ERR_INVALID_ARGUMENT, "spp_side must be in [1, 64]");
+    PGRT_REQUIRE(p->max_level >= 0 && p->max_level <= kMaxLevels - 2, PGRT_ERR_INVALID_ARGUMENT,
+                 "max_level must be in [0, 14]");
+    hipStream_t s = ctx->stream;
+    const int ntiles = (int)tiles.size();
+    const long long npix = (long long)ntiles * kTile * kTile;
+    const int spp = p->spp_side * p->spp_side;
+    if (ntiles == 0) return;
+    PGRT_REQUIRE(npix <= kMaxBatchRays * 8, PGRT_ERR_INVALID_ARGUMENT, "frame too large");
+    int nsb = (int)std::max(1ll, std::min<long long>(spp, kMaxBatchRays / npix));
+    const int levels = p->max_level + 1;
+    ctx->tiles.alloc(ntiles);
+    PGRT_HIP(hipMemcpyAsync(ctx->tiles.p, tiles.data(), sizeof(int4) * ntiles, hipMemcpyHostToDevice, s));
+    ctx->accum.alloc((size_t)npix);
+    ctx->timer.on = p->profile > 0;
+    double ms[CAT_N] = {0};
+    uint64_t rays_shadow = 0, rays_reflect = 0, rays_refract = 0, trav_nodes = 0, trav_tests = 0;
+    int retries = 0, trace_launches = 0;
+    FrameParams fp{};
+    fp.spp_side = p->spp_side;
+    fp.max_level = p->max_level;
+    fp.dof = p->dof;
+    fp.focal = p->focal_distance;
+    fp.aperture = p->aperture;
+    fp.gamma = p->gamma_level;
+    fp.jitter = p->jitter;
+    fp.seed = p->seed;
+    fp.frame = p->frame;
+    fp.ntiles = ntiles;
+    for (;;) {  // whole-frame retry if any queue overflowed
+        const int n0max = (int)(npix * nsb);
+        ensure_frame_buffers(ctx, n0max, levels);
+        std::vector<FrameCounters> host_fc;
+        for (int s0 = 0; s0 < spp; s0 += nsb) {
+            fp.s0 = s0;
+            fp.nsb = std::min(nsb, spp - s0);
+            const int n0 = (int)(npix * fp.nsb);
+            FrameCounters* fcd = ctx->fc.p;
+            PGRT_HIP(hipMemsetAsync(fcd, 0, sizeof(FrameCounters), s));
+            Queue q[2];
+            for (int b = 0; b < 2; ++b)
+                q[b] = Queue{ctx->q_ro[b].p, ctx->q_rd[b].p, ctx->q_time[b].p, ctx->q_hit[b].p, ctx->q_cap};
+            ShadowQueue sq{ctx->s_ro.p, ctx->s_rd.p, ctx->s_hit.p, ctx->s_contrib.p, ctx->s_cap};
+            int id = ctx->timer.begin(s, CAT_RAYGEN);
+            launch_raygen(ctx->cam, fp, ctx->tiles.p, q[0], n0, fcd, s);
+            ctx->timer.end(s, id);
+            for (int L = 0; L < levels; ++L) {
+                Queue qc = q[L & 1], qn = q[(L + 1) & 1];
+                const int maxc = L == 0 ? n0 : std::min(ctx->q_cap, ctx->level_cap[L]);
+                qc.cap = maxc;
+                qn.cap = std::min(ctx->q_cap, L + 1 < levels ? ctx->level_cap[L + 1] : ctx->q_cap);
+                LevelNodes ln{ctx->n_color[L]->p, ctx->n_link[L]->p, ctx->n_att[L]->p};
+                id = ctx->timer.begin(s, CAT_TRACE);
+                launch_trace(ctx->view, qc.ro, qc.rd, qc.hit, &fcd->count[L], 0, maxc, ctx->gstack.p,
+                             kTraceGridThreads, fcd->trav, p->profile >= 2, s);
+                ctx->timer.end(s, id);
+                ++trace_launches;
+                id = ctx->timer.begin(s, CAT_SHADE);
+                launch_shade(ctx->view, fp, L, qc, qn, ln, sq, fcd, maxc, s);
+                ctx->timer.end(s, id);
+                if (ctx->view.nlight > 0 && L < p->max_level) {
+                    const int smax = std::min((long long)ctx->s_cap, (long long)maxc * ctx->view.nlight);
+                    id = ctx->timer.begin(s, CAT_TRACE);
+                    launch_trace(ctx->view, sq.ro, sq.rd, sq.hit, &fcd->shadow_count[L], 0, (int)smax,
+                                 ctx->gstack.p, kTraceGridThreads, fcd->trav, p->profile >= 2, s);
+                    ctx->timer.end(s, id);
+                    ++trace_launches;
+                    id = ctx->timer.begin(s, CAT_SHADOW);
+                    launch_shadow_resolve(ctx->view, L, ln, sq, fcd, maxc, s);
+                    ctx->timer.end(s, id);
+                }
+            }
+            id = ctx->timer.begin(s, CAT_COMBINE);
+            for (int L = levels - 2; L >= 0; --L) {
+                LevelNodes ln{ctx->n_color[L]->p, ctx->n_link[L]->p, ctx->n_att[L]->p};
+                LevelNodes lc{ctx->n_color[L + 1]->p, ctx->n_link[L + 1]->p, ctx->n_att[L + 1]->p};
+                launch_combine(L, ln, lc, fcd, L == 0 ? n0 : std::min(ctx->q_cap, ctx->level_cap[L]), s);
+            }
+            LevelNodes l0{ctx->n_color[0]->p, ctx->n_link[0]->p, ctx->n_att[0]->p};
+            launch_accumulate(fp, ctx->tiles.p, l0, ctx->accum.p, (int)npix, s0 == 0, s);
+            ctx->timer.end(s, id);
+            FrameCounters hfc;
+            PGRT_HIP(hipMemcpyAsync(&hfc, fcd, sizeof(FrameCounters), hipMemcpyDeviceToHost, s));
+            PGRT_HIP(hipStreamSynchronize(s));
+            host_fc.push_back(hfc);
+            if (hfc.overflow) break;
+        }
+        PGRT_HIP(hipGetLastError());
+        bool overflow = false;
+        for (auto& h : host_fc) overflow |= h.overflow != 0;
+        if (overflow) {
+            // grow every level queue to what was requested (2x margin) and redo the frame
+            for (auto& h : host_fc)
+                for (int L = 1; L < levels; ++L) {
+                    const int need = h.count[L] * 2;
+                    if (need > ctx->level_cap[L]) ctx->level_cap[L] = need;
+                    if (need > ctx->q_cap) {
+                        for (int b = 0; b < 2; ++b) {
+                            ctx->q_ro[b].alloc(need);
+                            ctx->q_rd[b].alloc(need);
+                            ctx->q_hit[b].alloc(need);
+                            ctx->q_time[b].alloc(need);
+                        }
+                        ctx->q_cap = need;
+                    }
+                    for (int L2 = 1; L2 < levels; ++L2)
+                        if ((int)ctx->n_color[L2]->n < ctx->level_cap[L2]) {
+                            ctx->n_color[L2]->alloc(ctx->level_cap[L2]);
+                            ctx->n_att[L2]->alloc(ctx->level_cap[L2]);
+                            ctx->n_link[L2]->alloc(ctx->level_cap[L2]);
+                        }
+                    int sh = 0;
+                    for (int L2 = 0; L2 < levels; ++L2) sh = std::max(sh, h.shadow_count[L2] * 2);
+                    if (sh > ctx->s_cap) {
+                        ctx->s_ro.alloc(sh);
+                        ctx->s_rd.alloc(sh);
+                        ctx->s_hit.alloc(sh);
+                        ctx->s_contrib.alloc(sh);
+                        ctx->s_cap = sh;
+                    }
+                }
+            ctx->timer.collect(ms);
+            std::fill(ms, ms + CAT_N, 0.0);
+            ++retries;
+            PGRT_REQUIRE(retries < 8, PGRT_ERR_OUT_OF_MEMORY, "ray queues kept overflowing");
+            trace_launches = 0;
+            continue;
+        }
+        for (auto& h : host_fc) {
+            for (int L = 0; L < levels; ++L) {
+                rays_shadow += (uint64_t)h.shadow_count[L];
+                if (L >= 1) {
+                    rays_refract += (uint64_t)h.refract[L];
+                    rays_reflect += (uint64_t)(h.count[L] - h.refract[L]);
+                }
+            }
+            trav_nodes += h.trav[0];
+            trav_tests += h.trav[1];
+        }
+        break;
+    }
+    int id = ctx->timer.begin(s, CAT_RESOLVE);
+    launch_resolve(fp, ctx->tiles.p, ctx->accum.p, out, out_mode, ox, oy, pitch, (int)npix, s);
+    ctx->timer.end(s, id);
+    PGRT_HIP(hipGetLastError());
+    if (st) {
+        PGRT_HIP(hipStreamSynchronize(s));
+        ctx->timer.collect(ms);
+        long long real_pix = 0;
+        for (auto& t : tiles) real_pix += (long long)t.z * t.w;
+        st->rays_primary = (uint64_t)(real_pix * spp);
+        st->rays_shadow = rays_shadow;
+        st->rays_reflect = rays_reflect;
+        st->rays_refract = rays_refract;
+        st->node_visits = trav_nodes;
+        st->tri_tests = trav_tests;
+        st->ms_raygen = ms[CAT_RAYGEN];
+        st->ms_trace = ms[CAT_TRACE];
+        st->ms_shade = ms[CAT_SHADE];
+        st->ms_shadow = ms[CAT_SHADOW];
+        st->ms_combine = ms[CAT_COMBINE];
+        st->ms_resolve = ms[CAT_RESOLVE];
+        st->trace_launches = trace_launches;
+        st->levels = levels;
+        st->overflow_retries = retries;
+    } else {
+        ctx->timer.collect(ms);
+    }
+}
+
+std::vector<int4> rect_tiles(int x0, int y0, int w, int h) {
+    std::vector<int4> t;
+    for (int ty = 0; ty < h; ty += kTile)
+        for (int tx = 0; tx < w; tx += kTile)
+            t.push_back(make_int4(x0 + tx, y0 + ty, std::min(kTile, w - tx), std::min(kTile, h - ty)));
+    return t;
+}
+
+void frame_rect(const pgrt_ctx* ctx, const pgrt_render_params* p, int& x, int& y, int& w, int& h) {
+    x = p->rect_x;
+    y = p->rect_y;
+    w = p->rect_w;
+    h = p->rect_h;
+    if (w <= 0 || h <= 0) {
+        x = 0;
+        y = 0;
+        w = ctx->cam.width;
+        h = ctx->cam.height;
+    }
+    PGRT_REQUIRE(x >= 0 && y >= 0 && x + w <= ctx->cam.width && y + h <= ctx->cam.height, PGRT_ERR_INVALID_ARGUMENT,
+                 "render rect outside the camera image");
+}
+
+std::vector<int4> rank_tiles(int W, int H, int rank, int world) {
+    std::vector<int4> all = rect_tiles(0, 0, W, H), mine;
+    for (size_t t = 0; t < all.size(); ++t)
+        if ((int)(t % world) == rank) mine.push_back(all[t]);
+    return mine;
+}
+
+}  // namespace
+
+// =========================================================================== C ABI
+
+extern "C" {
+
+const char* pgrt_version(void) { return "pgrt 0.1.0 (gfx950, abi 1)"; }
+
+int pgrt_device_count(int* count) {
+    if (!count) return PGRT_ERR_INVALID_ARGUMENT;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return PGRT_OK;
+}
+
+int pgrt_create(int hip_device, pgrt_ctx** out) {
+    if (!out) return PGRT_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return PGRT_ERR_NO_DEVICE;
+    if (hip_device < 0 || hip_device >= n) return PGRT_ERR_INVALID_ARGUMENT;
+    pgrt_ctx* ctx = new (std::nothrow) pgrt_ctx();
+    if (!ctx) return PGRT_ERR_OUT_OF_MEMORY;
+    ctx->device = hip_device;
+    int rc = guarded(ctx, [&] { PGRT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)); });
+    if (rc != PGRT_OK) {
+        delete ctx;
+        return rc;
+    }
+    *out = ctx;
+    return PGRT_OK;
+}
+
+void pgrt_destroy(pgrt_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    delete ctx;
+}
+
+const char* pgrt_last_error(const pgrt_ctx* ctx) { return ctx ? ctx->err.c_str() : "NULL context"; }
+
+int pgrt_set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* scene) {
+    if (!ctx) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] { set_scene(ctx, scene); });
+}
+
+int pgrt_bvh_get_info(const pgrt_ctx* ctx, pgrt_bvh_info* info) {
+    if (!ctx || !info) return PGRT_ERR_INVALID_ARGUMENT;
+    if (!ctx->has_scene) return PGRT_ERR_NO_SCENE;
+    *info = ctx->info;
+    return PGRT_OK;
+}
+
+int pgrt_set_camera(pgrt_ctx* ctx, const pgrt_camera* cam) {
+    if (!ctx) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        PGRT_REQUIRE(cam && cam->width > 0 && cam->height > 0 && cam->width <= 65536 && cam->height <= 65536,
+                     PGRT_ERR_INVALID_ARGUMENT, "camera resolution must be in [1, 65536]");
+        ctx->cam = make_camera(*cam);
+        ctx->has_cam = true;
+    });
+}
+
+int pgrt_render_device(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device, pgrt_stats* st) {
+    if (!ctx || !p || !rgba_device) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        PGRT_REQUIRE(ctx->has_cam, PGRT_ERR_NO_CAMERA, "pgrt_set_camera has not been called");
+        auto t0 = std::chrono::steady_clock::now();
+        int x, y, w, h;
+        frame_rect(ctx, p, x, y, w, h);
+        render_tiles(ctx, p, rect_tiles(x, y, w, h), static_cast<float*>(rgba_device), 0, x, y, w, st);
+        if (st) st->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    });
+}
+
+int pgrt_render(pgrt_ctx* ctx, const pgrt_render_params* p, float* rgba_host, pgrt_stats* st) {
+    if (!ctx || !p || !rgba_host) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        PGRT_REQUIRE(ctx->has_cam, PGRT_ERR_NO_CAMERA, "pgrt_set_camera has not been called");
+        auto t0 = std::chrono::steady_clock::now();
+        int x, y, w, h;
+        frame_rect(ctx, p, x, y, w, h);
+        ctx->out_tmp.alloc((size_t)w * h * 4);
+        render_tiles(ctx, p, rect_tiles(x, y, w, h), ctx->out_tmp.p, 0, x, y, w, st);
+        PGRT_HIP(hipMemcpyAsync(rgba_host, ctx->out_tmp.p, (size_t)w * h * 4 * sizeof(float), hipMemcpyDeviceToHost,
+                                ctx->stream));
+        PGRT_HIP(hipStreamSynchronize(ctx->stream));
+        if (st) st->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    });
+}
+
+int pgrt_device_alloc(pgrt_ctx* ctx, size_t bytes, void** out) {
+    if (!ctx || !out) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        hipError_t e = hipMalloc(out, bytes ? bytes : 1);
+        if (e != hipSuccess) throw Error(PGRT_ERR_OUT_OF_MEMORY, hipGetErrorString(e));
+    });
+}
+
+int pgrt_device_free(pgrt_ctx* ctx, void* ptr) {
+    if (!ctx) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] { PGRT_HIP(hipFree(ptr)); });
+}
+
+int pgrt_copy_to_host(pgrt_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (!ctx || (!dst && bytes) || (!src && bytes)) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        PGRT_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        PGRT_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int pgrt_synchronize(pgrt_ctx* ctx) {
+    if (!ctx) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] { PGRT_HIP(hipStreamSynchronize(ctx->stream)); });
+}
+
+int pgrt_intersect_closest(pgrt_ctx* ctx, const float* rays, int n, float* hits) {
+    if (!ctx || n < 0 || (n > 0 && (!rays || !hits))) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        PGRT_REQUIRE(ctx->has_scene, PGRT_ERR_NO_SCENE, "pgrt_set_scene has not been called");
+        if (n == 0) return;
+        DevBuf<float4> ro, rd, h;
+        ro.alloc(n);
+        rd.alloc(n);
+        h.alloc(n);
+        std::vector<float4> a(n), b(n);
+        for (int i = 0; i < n; ++i) {
+            const float* r = rays + 8 * (size_t)i;
+            a[i] = make_float4(r[0], r[1], r[2], r[3]);
+            b[i] = make_float4(r[4], r[5], r[6], r[7]);
+        }
+        PGRT_HIP(hipMemcpyAsync(ro.p, a.data(), sizeof(float4) * n, hipMemcpyHostToDevice, ctx->stream));
+        PGRT_HIP(hipMemcpyAsync(rd.p, b.data(), sizeof(float4) * n, hipMemcpyHostToDevice, ctx->stream));
+        if (ctx->gstack.n == 0) ctx->gstack.alloc((size_t)kTraceGridThreads * kGlobalStack);
+        launch_trace(ctx->view, ro.p, rd.p, h.p, nullptr, n, n, ctx->gstack.p, kTraceGridThreads, nullptr, false,
+                     ctx->stream);
+        PGRT_HIP(hipGetLastError());
+        PGRT_HIP(hipMemcpyAsync(hits, h.p, sizeof(float4) * n, hipMemcpyDeviceToHost, ctx->stream));
+        PGRT_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+// ---- tiles / multi-GPU -------------------------------------------------------------------
+
+int pgrt_tile_count(int width, int height, int tile_size, int rank, int world) {
+    if (width <= 0 || height <= 0 || tile_size <= 0 || world <= 0 || rank < 0 || rank >= world)
+        return PGRT_ERR_INVALID_ARGUMENT;
+    const long long total = (long long)((width + tile_size - 1) / tile_size) * ((height + tile_size - 1) / tile_size);
+    return (int)(total / world + (rank < total % world ? 1 : 0));
+}
+
+int pgrt_tile_rect(int width, int height, int tile_size, int t, int rect[4]) {
+    if (width <= 0 || height <= 0 || tile_size <= 0 || !rect) return PGRT_ERR_INVALID_ARGUMENT;
+    const int tx = (width + tile_size - 1) / tile_size, ty = (height + tile_size - 1) / tile_size;
+    if (t < 0 || t >= tx * ty) return PGRT_ERR_INVALID_ARGUMENT;
+    rect[0] = (t % tx) * tile_size;
+    rect[1] = (t / tx) * tile_size;
+    rect[2] = std::min(tile_size, width - rect[0]);
+    rect[3] = std::min(tile_size, height - rect[1]);
+    return PGRT_OK;
+}
+
+int pgrt_unpack_tiles_host(int width, int height, int tile_size, int world, const float* g, float* rgba) {
+    if (width <= 0 || height <= 0 || tile_size <= 0 || world <= 0 || !g || !rgba) return PGRT_ERR_INVALID_ARGUMENT;
+    const int tx = (width + tile_size - 1) / tile_size, ty = (height + tile_size - 1) / tile_size;
+    const int total = tx * ty;
+    const int per_rank = (total + world - 1) / world;
+    const size_t tile_floats = (size_t)tile_size * tile_size * 4;
+    for (int r = 0; r < world; ++r)
+        for (int j = 0; j < per_rank; ++j) {
+            const int t = j * world + r;
+            if (t >= total) continue;
+            const float* src = g + ((size_t)r * per_rank + j) * tile_floats;
+            const int x0 = (t % tx) * tile_size, y0 = (t / tx) * tile_size;
+            for (int y = 0; y < tile_size && y0 + y < height; ++y)
+                for (int x = 0; x < tile_size && x0 + x < width; ++x)
+                    std::memcpy(rgba + ((size_t)(y0 + y) * width + (x0 + x)) * 4,
+                                src + ((size_t)y * tile_size + x) * 4, 4 * sizeof(float));
+        }
+    return PGRT_OK;
+}
+
+int pgrt_comm_unique_id(char id[128]) {
+    if (!id) return PGRT_ERR_INVALID_ARGUMENT;
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return PGRT_ERR_RCCL;
+    std::memcpy(id, u.internal, 128);
+    return PGRT_OK;
+}
+
+int pgrt_comm_init(pgrt_ctx* ctx, int world, int rank, const char id[128]) {
+    if (!ctx || !id || world <= 0 || rank < 0 || rank >= world) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        if (ctx->comm) {
+            (void)ncclCommDestroy(ctx->comm);
+            ctx->comm = nullptr;
+        }
+        ctx->world = world;
+        ctx->rank = rank;
+        if (world == 1) return;
+        ncclUniqueId u;
+        std::memcpy(u.internal, id, 128);
+        ncclResult_t r = ncclCommInitRank(&ctx->comm, world, u, rank);
+        if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    });
+}
+
+int pgrt_render_distributed_device(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device, pgrt_stats* st) {
+    if (!ctx || !p) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        PGRT_REQUIRE(ctx->has_cam, PGRT_ERR_NO_CAMERA, "pgrt_set_camera has not been called");
+        PGRT_REQUIRE(ctx->rank != 0 || rgba_device, PGRT_ERR_INVALID_ARGUMENT, "rank 0 needs an output buffer");
+        auto t0 = std::chrono::steady_clock::now();
+        const int W = ctx->cam.width, H = ctx->cam.height;
+        const int total = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
+        const int per_rank = (total + ctx->world - 1) / ctx->world;
+        const size_t tile_floats = (size_t)kTile * kTile * 4;
+        std::vector<int4> mine = rank_tiles(W, H, ctx->rank, ctx->world);
+        ctx->tilebuf.alloc((size_t)per_rank * tile_floats);
+        if ((int)mine.size() < per_rank)
+            PGRT_HIP(hipMemsetAsync(ctx->tilebuf.p, 0, ctx->tilebuf.bytes(), ctx->stream));
+        render_tiles(ctx, p, mine, ctx->tilebuf.p, 1, 0, 0, 0, st);
+        auto tg = std::chrono::steady_clock::now();
+        if (ctx->world == 1) {
+            launch_unpack_tiles(ctx->tilebuf.p, static_cast<float*>(rgba_device), W, H, 1, per_rank, ctx->stream);
+        } else {
+            PGRT_REQUIRE(ctx->comm, PGRT_ERR_RCCL, "pgrt_comm_init has not been called");
+            if (ctx->rank == 0) ctx->gathered.alloc((size_t)per_rank * tile_floats * ctx->world);
+            ncclResult_t r = ncclGather(ctx->tilebuf.p, ctx->rank == 0 ? ctx->gathered.p : nullptr,
+                                        (size_t)per_rank * tile_floats, ncclFloat, 0, ctx->comm, ctx->stream);
+            if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string("ncclGather: ") + ncclGetErrorString(r));
+            if (ctx->rank == 0)
+                launch_unpack_tiles(ctx->gathered.p, static_cast<float*>(rgba_device), W, H, ctx->world, per_rank,
+                                    ctx->stream);
+        }
+        PGRT_HIP(hipGetLastError());
+        PGRT_HIP(hipStreamSynchronize(ctx->stream));
+        if (st) {
+            st->ms_gather = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tg).count();
+            st->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        }
+    });
+}
+
+int pgrt_render_distributed(pgrt_ctx* ctx, const pgrt_render_params* p, float* rgba_host, pgrt_stats* st) {
+    if (!ctx || !p) return PGRT_ERR_INVALID_ARGUMENT;
+    const int W = ctx->cam.width, H = ctx->cam.height;
+    int rc = guarded(ctx, [&] {
+        PGRT_REQUIRE(ctx->has_cam, PGRT_ERR_NO_CAMERA, "pgrt_set_camera has not been called");
+        if (ctx->rank == 0) ctx->fb_dev.alloc((size_t)W * H * 4);
+    });
+    if (rc != PGRT_OK) return rc;
+    rc = pgrt_render_distributed_device(ctx, p, ctx->rank == 0 ? ctx->fb_dev.p : nullptr, st);
+    if (rc != PGRT_OK || ctx->rank != 0 || !rgba_host) return rc;
+    return pgrt_copy_to_host(ctx, rgba_host, ctx->fb_dev.p, (size_t)W * H * 4 * sizeof(float));
+}
+
+// test hook: device evaluation of the shared math (sqrt, div, powf, expf, atan2f, asinf, rsqrt, pow)
+int pgrt_selftest_math(pgrt_ctx* ctx, const float* in_pairs, int n, float* out8) {
+    if (!ctx || n < 0 || (n > 0 && (!in_pairs || !out8))) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        if (n == 0) return;
+        DevBuf<float> a, b;
+        a.alloc((size_t)2 * n);
+        b.alloc((size_t)8 * n);
+        PGRT_HIP(hipMemcpyAsync(a.p, in_pairs, sizeof(float) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
+        launch_selftest_math(a.p, n, b.p, ctx->stream);
+        PGRT_HIP(hipGetLastError());
+        PGRT_HIP(hipMemcpyAsync(out8, b.p, sizeof(float) * 8 * n, hipMemcpyDeviceToHost, ctx->stream));
+        PGRT_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,461 @@
+// render.hip -- wavefront Whitted pipeline kernels (ray generation, shading, shadow resolve,
+// bottom-up combine of the non-linear mix_srgb tree, sample accumulation, resolve + gamma).
+//
+// Reference: Raytracer::get_pixel / trace (APP/raytracer.cpp:237-437), PinHoleCamera
+// (APP/PinHoleCamera.cpp:31-105), LightSource::GenerateRay (APP/LightSource.cpp:11-32).
+// The recursion of trace() becomes one ray queue per level: level L+1 holds the reflection /
+// refraction children of the dielectric hits of level L, appended with one atomic per wave
+// (__ballot-free prefix by __shfl_up, the wave's total claimed by its last lane).  Shadow rays
+// of each level live in one queue traced by the same closest-hit kernel.  Because mix_srgb is
+// non-linear (it clamps and sRGB-encodes before the attenuation multiply, :318-321), colours
+// are combined bottom-up per level once every level is traced.
+#include "shade_ops.hpp"
+#include "trace.hpp"
+
+namespace pgrt {
+
+constexpr int kBlock = 256;
+
+// wave-level exclusive prefix allocation: every lane of the wave must call it (k = 0 allowed)
+__device__ __forceinline__ int wave_alloc(int* counter, int k) {
+    const int lane = __lane_id();
+    int x = k;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    const int total = __shfl(x, 63, 64);
+    int base = 0;
+    if (lane == 63 && total > 0) base = atomicAdd(counter, total);
+    base = __shfl(base, 63, 64);
+    return base + x - k;
+}
+
+// ------------------------------------------------------------------ ray generation
+
+__device__ __forceinline__ void tile_pixel(int slot_pix, const int4* tiles, int& px, int& py, bool& valid) {
+    const int tile = slot_pix / (kTile * kTile);
+    const int p = slot_pix - tile * kTile * kTile;
+    const int blk = p >> 6, w = p & 63;
+    const int lx = ((blk & 7) << 3) + (w & 7);
+    const int ly = ((blk >> 3) << 3) + (w >> 3);
+    const int4 tr = tiles[tile];
+    valid = lx < tr.z && ly < tr.w;
+    px = tr.x + lx;
+    py = tr.y + ly;
+}
+
+__global__ __launch_bounds__(kBlock) void k_raygen(CameraView cam, FrameParams fp, const int4* __restrict__ tiles,
+                                                   Queue q, int n0, FrameCounters* fc) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i == 0) fc->count[0] = n0;
+    if (i >= n0) return;
+    const int slot_pix = i / fp.nsb;
+    const int s = fp.s0 + (i - slot_pix * fp.nsb);
+    int px, py;
+    bool valid;
+    tile_pixel(slot_pix, tiles, px, py, valid);
+    if (!valid) {
+        q.ro[i] = make_float4(0, 0, 0, 0);
+        q.rd[i] = make_float4(0, 0, 0, -1.0f);  // padding slot: tfar < 0, never hits
+        q.time[i] = 0.0f;
+        return;
+    }
+    const int S = fp.spp_side;
+    const int sx = s / S, sy = s - (s / S) * S;
+    const uint32_t pixel = (uint32_t)py * (uint32_t)cam.width + (uint32_t)px;
+    float j0 = 0.0f, j1 = 0.0f, j2 = 0.0f, j3 = 0.0f;
+    if (fp.jitter != PGRT_JITTER_NONE) {
+        const float Sf = (float)S;
+        const float ja = -0.5f / Sf, jb = 0.5f / Sf;
+        const float la = -fp.aperture / 2.0f, lb = fp.aperture / 2.0f;
+        const float u0 = pg_jitter_u01(fp.seed, fp.frame, pixel, (uint32_t)s, 0);
+        const float u1 = pg_jitter_u01(fp.seed, fp.frame, pixel, (uint32_t)s, 1);
+        const bool corr = fp.jitter == PGRT_JITTER_HASH_CORRELATED;
+        const float u2 = corr ? u0 : pg_jitter_u01(fp.seed, fp.frame, pixel, (uint32_t)s, 2);
+        const float u3 = corr ? u1 : pg_jitter_u01(fp.seed, fp.frame, pixel, (uint32_t)s, 3);
+        j0 = u0 * (jb - ja) + ja;
+        j1 = u1 * (jb - ja) + ja;
+        j2 = u2 * (lb - la) + la;
+        j3 = u3 * (lb - la) + la;
+    }
+    // get_pixel sample position (raytracer.cpp:412-413)
+    const float nx = (float)px + ((float)sx * (1.0f / (float)S)) + j0;
+    const float ny = (float)py + ((float)sy * (1.0f / (float)S)) + j1;
+    // camera-space direction with integer W/2, H/2 (PinHoleCamera.cpp:41-42, :67)
+    V3 crd = v3(nx - (float)(cam.width / 2), (float)(cam.height / 2) - ny, -cam.fy);
+    crd = normalize(crd);
+    V3 org, dir;
+    float tnear;
+    if (!fp.dof) {  // generate_ray(x, y) (PinHoleCamera.cpp:31-63)
+        org = v3(cam.from[0], cam.from[1], cam.from[2]);
+        dir = mat_mul(cam.m, crd);
+        tnear = 0.001f;
+    } else {  // generate_ray(x, y, focal, aperture) (PinHoleCamera.cpp:65-105)
+        V3 dws = normalize(mat_mul(cam.m, crd));
+        const V3 fpnt = v3(cam.from[0] + dws.x * fp.focal, cam.from[1] + dws.y * fp.focal,
+                           cam.from[2] + dws.z * fp.focal);
+        const V3 shift = mat_mul(cam.m, v3(j2, j3, 0));
+        org = v3(cam.from[0] + shift.x, cam.from[1] + shift.y, cam.from[2] + shift.z);
+        dir = normalize(v3(fpnt.x - org.x, fpnt.y - org.y, fpnt.z - org.z));
+        tnear = 0.01f;
+    }
+    q.ro[i] = make_float4(org.x, org.y, org.z, tnear);
+    q.rd[i] = make_float4(dir.x, dir.y, dir.z, 3.402823466e+38f);
+    q.time[i] = PGRT_IOR_AIR;  // raytracer.cpp:416
+}
+
+void launch_raygen(const CameraView& cam, const FrameParams& fp, const int4* tiles, Queue q, int n0,
+                   FrameCounters* fc, hipStream_t stream) {
+    if (n0 <= 0) return;
+    hipLaunchKernelGGL(k_raygen, dim3(ceil_div(n0, kBlock)), dim3(kBlock), 0, stream, cam, fp, tiles, q, n0, fc);
+}
+
+// ------------------------------------------------------------------ shading (trace body)
+
+__global__ __launch_bounds__(kBlock) void k_shade(SceneView s, FrameParams fp, int level, Queue q, Queue next,
+                                                  LevelNodes nodes, ShadowQueue sq, FrameCounters* fc) {
+    const int n = min(fc->count[level], q.cap);
+    const int tid = threadIdx.x;
+    for (int base_i = blockIdx.x * kBlock; base_i < n; base_i += gridDim.x * kBlock) {
+        const int i = base_i + tid;
+        const bool active = i < n;
+        int kind = 0;  // 0 final colour, 1 dielectric, 2 opaque (shadow rays pending)
+        float4 color = make_float4(0, 0, 0, 1);
+        int nshadow = 0, nchild = 0;
+        V3 org = v3(0, 0, 0), dirraw = v3(0, 0, 0), d = v3(0, 0, 0), nrm = v3(0, 0, 0), hitp = v3(0, 0, 0);
+        V3 refl_dir = v3(0, 0, 0), refr_dir = v3(0, 0, 0);
+        float n1 = 0, n2 = 0, t = 0;
+        float4 att = make_float4(0, 0, 0, 0);
+        float m_d_r = 0, m_d_g = 0, m_d_b = 0;
+        int mid = 0;
+        if (active) {
+            const float4 o4 = q.ro[i];
+            const float4 d4 = q.rd[i];
+            const float rtime = q.time[i];
+            const float4 h = q.hit[i];
+            org = v3(o4.x, o4.y, o4.z);
+            dirraw = v3(d4.x, d4.y, d4.z);
+            if (d4.w < 0.0f) {
+                color = make_float4(0, 0, 0, 0);  // padding slot
+            } else {
+                d = normalize(dirraw);
+                const int prim = __float_as_int(h.w);
+                if (prim < 0) {
+                    color = env_texel(s, d);  // miss (raytracer.cpp:390-393)
+                } else {
+                    t = h.x;
+                    const float* a = s.attr + 16 * (size_t)prim;
+                    const float u = h.y, v = h.z;
+                    V3 nn = v3(interp1(a[0], a[3], a[6], u, v), interp1(a[1], a[4], a[7], u, v),
+                               interp1(a[2], a[5], a[8], u, v));
+                    mid = __float_as_int(a[15]);
+                    const DevMaterial& m = s.mats[mid];
+                    nn = normalize(nn);
+                    hitp = org + scale(t, dirraw);
+                    if (rtime == PGRT_IOR_AIR) {
+                        n1 = PGRT_IOR_AIR;
+                        n2 = m.ior;
+                    } else {
+                        n1 = m.ior;
+                        n2 = PGRT_IOR_AIR;
+                    }
+                    if (dot(nn, d) > 0) nn = -nn;
+                    nrm = nn;
+                    if (level >= fp.max_level) {
+                        color = make_float4(0, 0, 0, 1);  // raytracer.cpp:282-283
+                    } else if (m.type == PGRT_MATERIAL_DIELECTRIC) {
+                        kind = 1;
+                        {  // get_reflection_ray (raytracer.cpp:209-235)
+                            const V3 dd = normalize(d), rn = normalize(nn);
+                            refl_dir = dd - scale(2, scale(dot(dd, rn), rn));
+                        }
+                        att.x = pg_expf(-(1 - m.kd[0]) * t);  // raytracer.cpp:303-305
+                        att.y = pg_expf(-(1 - m.kd[1]) * t);
+                        att.z = pg_expf(-(1 - m.kd[2]) * t);
+                        {  // get_refraction_ray (raytracer.cpp:178-207)
+                            const V3 dd = normalize(d), rn = normalize(nn);
+                            const float n1_n2 = n1 / n2;
+                            const float d_n = dot(dd, rn);
+                            const V3 sd = v3(dd.x * n1_n2, dd.y * n1_n2, dd.z * n1_n2);
+                            const float kk = n1_n2 * d_n + sqrtf(1 - ((n1_n2 * n1_n2) * (1 - (d_n * d_n))));
+                            refr_dir = sd - scale(kk, rn);
+                        }
+                        nchild = 1;
+                        if (refr_dir.x == refr_dir.x) {  // no total internal reflection
+                            nchild = 2;
+                            const float cos1 = fabsf(dot(nn, -d));
+                            const float alpha = (n1 - n2) / (n1 + n2);
+                            att.w = (float)((double)(alpha * alpha + (1 - (alpha * alpha))) *
+                                            pg_pow_d((double)(1 - cos1), 5.0));
+                        }
+                    } else {
+                        kind = 2;
+                        if (m.tex < 0) {
+                            m_d_r = m.kd[2];
+                            m_d_g = m.kd[1];
+                            m_d_b = m.kd[0];
+                        } else {
+                            const float tu = interp1(a[9], a[11], a[13], u, v);
+                            const float tv = interp1(a[10], a[12], a[14], u, v);
+                            const V3 tx = tex_texel(s.tex[m.tex], s.texels, tu, 1.0f - tv);
+                            m_d_r = tx.x;
+                            m_d_g = tx.y;
+                            m_d_b = tx.z;
+                        }
+                        for (int li = 0; li < s.nlight; ++li) {
+                            const DevLight& L = s.lights[li];
+                            if (!(dot(nn, v3(L.pos[0], L.pos[1], L.pos[2])) < 0)) ++nshadow;
+                        }
+                        color = make_float4(0, 0, 0, 1);
+                    }
+                }
+            }
+        }
+        // ---- queue allocation (wave-uniform control flow) ----
+        const int cbase = wave_alloc(&fc->count[level + 1 < kMaxLevels ? level + 1 : level], nchild);
+        const int sbase = wave_alloc(&fc->shadow_count[level], nshadow);
+        const int nref = wave_alloc(&fc->refract[level + 1 < kMaxLevels ? level + 1 : level], nchild == 2 ? 1 : 0);
+        (void)nref;
+        if (!active) continue;
+        int4 link = make_int4(-1, -1, -1, 0);
+        if (kind == 1) {
+            if (cbase + nchild > next.cap || level + 1 >= kMaxLevels) {
+                atomicOr(&fc->overflow, 1);
+            } else {
+                next.ro[cbase] = make_float4(hitp.x, hitp.y, hitp.z, 0.01f);
+                next.rd[cbase] = make_float4(refl_dir.x, refl_dir.y, refl_dir.z, 3.402823466e+38f);
+                next.time[cbase] = n1;
+                link.x = cbase;
+                if (nchild == 2) {
+                    next.ro[cbase + 1] = make_float4(hitp.x, hitp.y, hitp.z, 0.01f);
+                    next.rd[cbase + 1] = make_float4(refr_dir.x, refr_dir.y, refr_dir.z, 3.402823466e+38f);
+                    next.time[cbase + 1] = n2;
+                    link.y = cbase + 1;
+                }
+            }
+            nodes.att[i] = att;
+        } else if (kind == 2 && nshadow > 0) {
+            if (sbase + nshadow > sq.cap) {
+                atomicOr(&fc->overflow, 1);
+            } else {
+                const DevMaterial& m = s.mats[mid];
+                int k = sbase;
+                for (int li = 0; li < s.nlight; ++li) {
+                    const DevLight& L = s.lights[li];
+                    const V3 lp = v3(L.pos[0], L.pos[1], L.pos[2]);
+                    if (dot(nrm, lp) < 0) continue;  // is_illuminated's N.L test (raytracer.cpp:155)
+                    // LightSource::GenerateRay(hit): org = light, dir = hit position vector
+                    sq.ro[k] = make_float4(lp.x, lp.y, lp.z, 0.01f);
+                    sq.rd[k] = make_float4(hitp.x, hitp.y, hitp.z,
+                                           length(v3(lp.x - hitp.x, lp.y - hitp.y, lp.z - hitp.z)));
+                    // Phong term for this light (raytracer.cpp:355-382)
+                    const V3 lv = normalize(v3(lp.x - hitp.x, lp.y - hitp.y, lp.z - hitp.z));
+                    const V3 cv = normalize(v3(org.x - dirraw.x, org.y - dirraw.y, org.z - dirraw.z));
+                    const float gam = m.ns;
+                    const float i_d_r = L.kd[2], i_d_g = L.kd[1], i_d_b = L.kd[0];
+                    const float i_s_r = L.ks[2], i_s_g = L.ks[1], i_s_b = L.ks[0];
+                    const float m_s_r = m.ks[2], m_s_g = m.ks[1], m_s_b = m.ks[0];
+                    const float nl = dot(nrm, lv);
+                    V3 l_r = scale(2 * nl, nrm) - lv;
+                    l_r = normalize(l_r);
+                    const float spec = pg_powf(dot(cv, l_r), gam);
+                    const float tb = i_d_b * m_d_b * dot(nrm, lv) + i_s_b * m_s_b * spec;
+                    const float tg = i_d_g * m_d_g * dot(nrm, lv) + i_s_g * m_s_g * spec;
+                    const float tr = i_d_r * m_d_r * dot(nrm, lv) + i_s_r * m_s_r * spec;
+                    sq.contrib[k] = make_float4(tb, tg, tr, 0.0f);
+                    ++k;
+                }
+                link.z = sbase;
+                link.w = nshadow;
+            }
+        }
+        nodes.link[i] = link;
+        nodes.color[i] = color;
+    }
+}
+
+void launch_shade(const SceneView& s, const FrameParams& fp, int level, Queue q, Queue next, LevelNodes nodes,
+                  ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream) {
+    if (max_count <= 0) return;
+    int grid = ceil_div(max_count, kBlock);
+    if (grid > 4096) grid = 4096;
+    hipLaunchKernelGGL(k_shade, dim3(grid), dim3(kBlock), 0, stream, s, fp, level, q, next, nodes, sq, fc);
+}
+
+// ------------------------------------------------------------------ shadow resolve
+
+__global__ __launch_bounds__(kBlock) void k_shadow_resolve(SceneView s, int level, LevelNodes nodes, ShadowQueue sq,
+                                                           const FrameCounters* fc, int cap) {
+    const int n = min(fc->count[level], cap);
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const int4 link = nodes.link[i];
+        if (link.z < 0) continue;
+        float blue = 0, green = 0, red = 0;
+        for (int j = 0; j < link.w; ++j) {
+            const int k = link.z + j;
+            const int prim = __float_as_int(sq.hit[k].w);
+            bool lit = true;  // is_illuminated (raytracer.cpp:163-173): closest hit decides
+            if (prim >= 0) {
+                const int mid = __float_as_int(s.attr[16 * (size_t)prim + 15]);
+                lit = s.mats[mid].type == PGRT_MATERIAL_DIELECTRIC;
+            }
+            if (lit) {
+                const float4 c = sq.contrib[k];
+                blue += c.x;
+                green += c.y;
+                red += c.z;
+            }
+        }
+        nodes.color[i] = make_float4(blue, green, red, 1.0f);
+    }
+}
+
+void launch_shadow_resolve(const SceneView& s, int level, LevelNodes nodes, ShadowQueue sq, const FrameCounters* fc,
+                           int max_count, hipStream_t stream) {
+    if (max_count <= 0) return;
+    int grid = ceil_div(max_count, kBlock);
+    if (grid > 4096) grid = 4096;
+    hipLaunchKernelGGL(k_shadow_resolve, dim3(grid), dim3(kBlock), 0, stream, s, level, nodes, sq, fc, max_count);
+}
+
+// ------------------------------------------------------------------ combine (dielectric nodes)
+
+__global__ __launch_bounds__(kBlock) void k_combine(int level, LevelNodes nodes, LevelNodes child,
+                                                    const FrameCounters* fc, int cap) {
+    const int n = min(fc->count[level], cap);
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const int4 link = nodes.link[i];
+        if (link.x < 0) continue;
+        const float4 att = nodes.att[i];
+        const float4 refl = child.color[link.x];
+        float4 out;
+        if (link.y >= 0) {  // raytracer.cpp:318-319
+            const float4 refr = child.color[link.y];
+            const float4 c = mix_srgb(refl, refr, att.w);
+            out = make_float4(c.x * att.x, c.y * att.y, c.z * att.z, 1);
+        } else {  // total internal reflection (raytracer.cpp:321)
+            out = make_float4(refl.x * att.x, refl.y * att.y, refl.z * att.z, 1);
+        }
+        nodes.color[i] = out;
+    }
+}
+
+void launch_combine(int level, LevelNodes nodes, LevelNodes child, const FrameCounters* fc, int max_count,
+                    hipStream_t stream) {
+    if (max_count <= 0) return;
+    int grid = ceil_div(max_count, kBlock);
+    if (grid > 4096) grid = 4096;
+    hipLaunchKernelGGL(k_combine, dim3(grid), dim3(kBlock), 0, stream, level, nodes, child, fc, max_count);
+}
+
+// ------------------------------------------------------------------ accumulate + resolve
+
+__global__ __launch_bounds__(kBlock) void k_accumulate(FrameParams fp, LevelNodes l0, float4* __restrict__ accum,
+                                                       int npix, int first) {
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= npix) return;
+    float4 acc = first ? make_float4(0.0f, 0.0f, 0.0f, 1.0f) : accum[p];
+    const float4* c = l0.color + (size_t)p * fp.nsb;
+    for (int k = 0; k < fp.nsb; ++k) {  // final_color += result_colors[x][y] (raytracer.cpp:422-429)
+        const float4 v = c[k];
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+    }
+    accum[p] = acc;
+}
+
+void launch_accumulate(const FrameParams& fp, const int4* tiles, LevelNodes l0, float4* accum, int npix, bool first,
+                       hipStream_t stream) {
+    (void)tiles;
+    if (npix <= 0) return;
+    hipLaunchKernelGGL(k_accumulate, dim3(ceil_div(npix, kBlock)), dim3(kBlock), 0, stream, fp, l0, accum, npix,
+                       first ? 1 : 0);
+}
+
+__global__ __launch_bounds__(kBlock) void k_resolve(FrameParams fp, const int4* __restrict__ tiles,
+                                                    const float4* __restrict__ accum, float* __restrict__ out,
+                                                    int out_mode, int ox, int oy, int pitch, int npix) {
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= npix) return;
+    int px, py;
+    bool valid;
+    tile_pixel(p, tiles, px, py, valid);
+    if (!valid) return;
+    const float4 acc = accum[p];
+    const int area = fp.spp_side * fp.spp_side;
+    // gamma(Color4f{final.b/area, final.g/area, final.r/area}) (raytracer.cpp:431-435)
+    const float4 o = gamma_rgba(acc.z / (float)area, acc.y / (float)area, acc.x / (float)area, fp.gamma);
+    float* dst;
+    if (out_mode == 0) {
+        dst = out + ((size_t)(py - oy) * (size_t)pitch + (size_t)(px - ox)) * 4;
+    } else {
+        const int tile = p / (kTile * kTile);
+        const int4 tr = tiles[tile];
+        dst = out + ((size_t)tile * kTile * kTile + (size_t)(py - tr.y) * kTile + (size_t)(px - tr.x)) * 4;
+    }
+    *reinterpret_cast<float4*>(dst) = o;
+}
+
+void launch_resolve(const FrameParams& fp, const int4* tiles, const float4* accum, float* out, int out_mode, int ox,
+                    int oy, int pitch, int npix, hipStream_t stream) {
+    if (npix <= 0) return;
+    hipLaunchKernelGGL(k_resolve, dim3(ceil_div(npix, kBlock)), dim3(kBlock), 0, stream, fp, tiles, accum, out,
+                       out_mode, ox, oy, pitch, npix);
+}
+
+// ------------------------------------------------------------------ multi-GPU unpack
+
+__global__ __launch_bounds__(kBlock) void k_unpack(const float4* __restrict__ g, float4* __restrict__ rgba, int width,
+                                                   int height, int world, int tiles_per_rank) {
+    const long long idx = (long long)blockIdx.x * kBlock + threadIdx.x;
+    const long long per_rank = (long long)tiles_per_rank * kTile * kTile;
+    if (idx >= per_rank * world) return;
+    const int rank = (int)(idx / per_rank);
+    const long long r = idx - rank * per_rank;
+    const int j = (int)(r / (kTile * kTile));
+    const int p = (int)(r - (long long)j * kTile * kTile);
+    const int tiles_x = (width + kTile - 1) / kTile;
+    const int tiles_y = (height + kTile - 1) / kTile;
+    const int t = j * world + rank;
+    if (t >= tiles_x * tiles_y) return;
+    const int x = (t % tiles_x) * kTile + (p % kTile);
+    const int y = (t / tiles_x) * kTile + (p / kTile);
+    if (x >= width || y >= height) return;
+    rgba[(size_t)y * width + x] = g[idx];
+}
+
+void launch_unpack_tiles(const float* gathered, float* rgba, int width, int height, int world, int tiles_per_rank,
+                         hipStream_t stream) {
+    const long long total = (long long)world * tiles_per_rank * kTile * kTile;
+    if (total <= 0) return;
+    hipLaunchKernelGGL(k_unpack, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
+                       reinterpret_cast<const float4*>(gathered), reinterpret_cast<float4*>(rgba), width, height,
+                       world, tiles_per_rank);
+}
+
+// ------------------------------------------------------------------ math self-test
+
+__global__ void k_selftest(const float* in, int n, float* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float a = in[2 * i], b = in[2 * i + 1];
+    float* o = out + 8 * (size_t)i;
+    o[0] = sqrtf(a);
+    o[1] = a / b;
+    o[2] = pg_powf(a, b);
+    o[3] = pg_expf(a);
+    o[4] = pg_atan2f(a, b);
+    o[5] = pg_asinf(a);
+    o[6] = 1 / sqrtf(a);
+    o[7] = (float)pg_pow_d((double)a, (double)b);
+}
+
+void launch_selftest_math(const float* in, int n, float* out, hipStream_t stream) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_selftest, dim3(ceil_div(n, 256)), dim3(256), 0, stream, in, n, out);
+}
+
+}  // namespace pgrt

@@ -1,0 +1,130 @@
+// shade_ops.hpp -- device restatement of the reference's per-hit arithmetic.
+//
+// Every function keeps the reference's float operation order (the library is compiled with
+// -ffp-contract=off) so results are bit-identical to the CPU restatement in oracle/oracle.c.
+// Reference anchors are given per function; src/pg/pg1_embree is abbreviated APP.
+#pragma once
+
+#include "common.hpp"
+
+namespace pgrt {
+
+struct V3 {
+    float x, y, z;
+};
+__device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
+// Vector3 operator*(float, Vector3) == operator*(Vector3, float) == a * v.c (APP/vector3.cpp:245-253)
+__device__ __forceinline__ V3 scale(float a, V3 v) { return v3(a * v.x, a * v.y, a * v.z); }
+// DotProduct (APP/vector3.cpp:187-190)
+__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+// CrossProduct (APP/vector3.cpp:169-175)
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+    return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+// Normalize (APP/vector3.cpp:155-167)
+__device__ __forceinline__ V3 normalize(V3 v) {
+    const float norm = v.x * v.x + v.y * v.y + v.z * v.z;
+    if (norm != 0) {
+        const float rn = 1 / sqrtf(norm);
+        v.x *= rn;
+        v.y *= rn;
+        v.z *= rn;
+    }
+    return v;
+}
+// L2Norm (APP/vector3.cpp:145-148)
+__device__ __forceinline__ float length(V3 v) { return sqrtf(v.x * v.x + v.y * v.y + v.z * v.z); }
+// Matrix3x3 * Vector3 (APP/matrix3x3.cpp:68-73)
+__device__ __forceinline__ V3 mat_mul(const float* m, V3 b) {
+    return v3(m[0] * b.x + m[1] * b.y + m[2] * b.z, m[3] * b.x + m[4] * b.y + m[5] * b.z,
+              m[6] * b.x + m[7] * b.y + m[8] * b.z);
+}
+
+// rtcInterpolate0 over de-indexed per-vertex attributes, Embree's madd(w,p0,madd(u,p1,v*p2))
+__device__ __forceinline__ float interp1(float a0, float a1, float a2, float u, float v) {
+    const float w = 1.0f - u - v;
+    return fmaf(w, a0, fmaf(u, a1, v * a2));
+}
+
+// Texture::get_pixel (APP/texture.cpp:56-62): Color3f{B,G,R}/255; bytes outside the decoded
+// buffer read as 0 (the reference reads out of bounds there).
+__device__ __forceinline__ V3 tex_pixel(const DevTexture& t, const unsigned char* pool, int x, int y) {
+    long long off = (long long)y * t.pitch + (long long)x * t.bpp;
+    if (off < 0 || off + 2 >= t.size) return v3(0, 0, 0);
+    const unsigned char* p = pool + t.offset + off;
+    return v3(p[0] / 255.0f, p[1] / 255.0f, p[2] / 255.0f);
+}
+
+// Texture::get_texel (APP/texture.cpp:77-130): bilinear with the reference's edge quirks.
+__device__ inline V3 tex_texel(const DevTexture& t, const unsigned char* pool, float u, float v) {
+    const float x = u * (float)t.width;
+    const float y = v * (float)t.height;
+    if (!(fabsf(x) < 16777216.0f) || !(fabsf(y) < 16777216.0f)) return v3(0, 0, 0);
+    const int tmp_x1 = (int)floorf(x), tmp_x2 = (int)ceilf(x);
+    const int tmp_y1 = (int)floorf(y), tmp_y2 = (int)ceilf(y);
+    const int x1 = (tmp_x1 < 1) ? tmp_x1 + 1 : tmp_x1;
+    const int x2 = (tmp_x2 == t.width) ? 0 : tmp_x2;
+    const int y1 = (tmp_y1 < 1) ? tmp_y1 + 1 : tmp_y1;
+    const int y2 = (tmp_y2 == t.height) ? tmp_y1 : tmp_y2;
+    if (x1 == x2 || y1 == y2) return v3(0, 0, 0);
+    const V3 x1y1 = tex_pixel(t, pool, x1, y1), x2y1 = tex_pixel(t, pool, x2, y1);
+    const V3 x1y2 = tex_pixel(t, pool, x1, y2), x2y2 = tex_pixel(t, pool, x2, y2);
+    const float Q11 = ((float)x2 - x) / (float)(x2 - x1);
+    const float Q21 = (x - (float)x1) / (float)(x2 - x1);
+    const float Q12 = Q11, Q22 = Q21;
+    const V3 f1 = v3(x1y1.x * Q11 + x2y1.x * Q21, x1y1.y * Q11 + x2y1.y * Q21, x1y1.z * Q11 + x2y1.z * Q21);
+    const V3 f2 = v3(x1y2.x * Q12 + x2y2.x * Q22, x1y2.y * Q12 + x2y2.y * Q22, x1y2.z * Q12 + x2y2.z * Q22);
+    const float wy2 = ((float)y2 - y) / (float)(y2 - y1);
+    const float wy1 = (y - (float)y1) / (float)(y2 - y1);
+    return v3(f1.x * wy2 + f2.x * wy1, f1.y * wy2 + f2.y * wy1, f1.z * wy2 + f2.z * wy1);
+}
+
+// SphericalMap::get_texel (APP/SphericalMap.cpp:17-29): returns RGBA with a = 1.
+__device__ inline float4 env_texel(const SceneView& s, V3 d) {
+    if (s.env < 0) return make_float4(0, 0, 0, 1);
+    const V3 vec = normalize(v3(d.x, d.z, d.y));
+    const float u = (float)(0.5 + (double)pg_atan2f(vec.x, vec.z) / (2 * 3.14159265358979323846));
+    const float v = (float)(0.5 - (double)pg_asinf(vec.y) / 3.14159265358979323846);
+    const V3 c = tex_texel(s.tex[s.env], s.texels, u, v);
+    return make_float4(c.z, c.y, c.x, 1.0f);
+}
+
+// utils.cpp:204-241
+__device__ inline float srgb_compress(float u) {
+    if (u <= 0) return 0.0f;
+    if (u >= 1) return 1.0f;
+    if ((double)u <= 0.00313080) return (float)(12.92 * (double)u);
+    return (float)(1.00 * pg_pow_d((double)u, 1 / 2.4) - 0.055);
+}
+__device__ inline float srgb_expand(float u) {
+    if (u <= 0) return 0.0f;
+    if (u >= 1) return 1.0f;
+    if ((double)u <= 0.04045) return (float)((double)u / 12.92);
+    return (float)pg_pow_d(((double)u + 0.055) / 1.055, 2.4);
+}
+// mix_srgb = compress(mix_linear(expand(c0), expand(c1), a)); each of the three swaps r<->b.
+__device__ inline float4 mix_srgb(float4 c0, float4 c1, float a) {
+    const float4 e0 = make_float4(srgb_expand(c0.z), srgb_expand(c0.y), srgb_expand(c0.x), 0.1f);
+    const float4 e1 = make_float4(srgb_expand(c1.z), srgb_expand(c1.y), srgb_expand(c1.x), 0.1f);
+    const float4 m = make_float4(a * e0.z + (1 - a) * e1.z, a * e0.y + (1 - a) * e1.y,
+                                 a * e0.x + (1 - a) * e1.x, 1.0f);
+    return make_float4(srgb_compress(m.z), srgb_compress(m.y), srgb_compress(m.x), 0.1f);
+}
+
+// Raytracer::gamma (APP/raytracer.cpp:439-446) on Color4f{b,g,r} input: returns r,g,b order.
+__device__ inline float4 gamma_rgba(float in_r, float in_g, float in_b, float g) {
+    const float b = pg_powf(in_b, g) * pg_powf(in_b, g);
+    const float gg = pg_powf(in_g, g) * pg_powf(in_g, g);
+    const float r = pg_powf(in_r, g) * pg_powf(in_r, g);
+    return make_float4(b, gg, r, 1.0f);
+}
+
+// Embree's Moeller-Trumbore triangle test (restated; see oracle.c tri_hit).
+__device__ __forceinline__ float xorsign(float a, float s) {
+    return __uint_as_float(__float_as_uint(a) ^ (__float_as_uint(s) & 0x80000000u));
+}
+
+}  // namespace pgrt

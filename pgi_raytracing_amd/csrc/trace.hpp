@@ -1,0 +1,93 @@
+// trace.hpp -- launchers of the hand-written gfx950 kernels (host-callable).
+#pragma once
+
+#include "common.hpp"
+
+namespace pgrt {
+
+constexpr int kGlobalStack = 96;  // per-thread overflow entries past the LDS stack
+constexpr int kTile = 64;         // image tile side (multi-GPU unit, level-0 ray order)
+constexpr int kMaxLevels = 16;    // max_level + 1 <= kMaxLevels
+
+// Per-frame device counters (zeroed by one hipMemsetAsync per batch).
+struct FrameCounters {
+    int count[kMaxLevels];         // rays queued per level
+    int shadow_count[kMaxLevels];  // shadow rays emitted per level
+    int refract[kMaxLevels];       // refraction rays among count[L]
+    int overflow;                  // set when an emit exceeded a queue capacity
+    int pad[3];
+    unsigned long long trav[2];    // node visits, triangle tests (profile == 2)
+};
+
+struct FrameParams {
+    int spp_side;
+    int max_level;
+    int dof;
+    float focal, aperture, gamma;
+    int jitter;
+    unsigned seed, frame;
+    int s0, nsb;   // first sample and samples in this batch
+    int ntiles;
+};
+
+// level-L queue view
+struct Queue {
+    float4* ro;      // org.xyz, tnear
+    float4* rd;      // dir.xyz, tfar
+    float* time;     // medium IOR (RTCRay::time as used by the reference)
+    float4* hit;     // t, u, v, prim bits
+    int cap;
+};
+
+struct LevelNodes {  // per-level node records kept until the combine pass
+    float4* color;
+    int4* link;      // dielectric: (refl child, refr child or -1, -, -); opaque: (-1,-1,shadow base, n)
+    float4* att;     // dielectric: (att.r, att.g, att.b, R)
+};
+
+struct ShadowQueue {
+    float4* ro;
+    float4* rd;
+    float4* hit;
+    float4* contrib;  // (blue, green, red, -) Phong term of the owning node for this light
+    int cap;
+};
+
+void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4* hits, const int* count_dev,
+                  int count_host, int max_count, int* gstack, int gstack_threads, unsigned long long* counters,
+                  bool count, hipStream_t stream);
+int trace_block_size();
+
+void launch_raygen(const CameraView& cam, const FrameParams& fp, const int4* tiles, Queue q, int n0,
+                   FrameCounters* fc, hipStream_t stream);
+void launch_shade(const SceneView& s, const FrameParams& fp, int level, Queue q, Queue next, LevelNodes nodes,
+                  ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream);
+void launch_shadow_resolve(const SceneView& s, int level, LevelNodes nodes, ShadowQueue sq, const FrameCounters* fc,
+                           int max_count, hipStream_t stream);
+void launch_combine(int level, LevelNodes nodes, LevelNodes child, const FrameCounters* fc, int max_count,
+                    hipStream_t stream);
+void launch_accumulate(const FrameParams& fp, const int4* tiles, LevelNodes l0, float4* accum, int npix,
+                       bool first, hipStream_t stream);
+// out_mode 0: framebuffer (rect origin ox,oy, row pitch in pixels); 1: tile-compact
+void launch_resolve(const FrameParams& fp, const int4* tiles, const float4* accum, float* out, int out_mode,
+                    int ox, int oy, int pitch, int npix, hipStream_t stream);
+void launch_unpack_tiles(const float* gathered, float* rgba, int width, int height, int world, int tiles_per_rank,
+                         hipStream_t stream);
+
+// scene / BVH build
+struct BuildOut {
+    int root;
+    int num_nodes;
+    int max_depth;
+};
+void build_lbvh(const float* pos_dev, int ntri, float4* tri_out, BvhNode* nodes_out, int* scratch_int,
+                void* sort_tmp, size_t sort_tmp_bytes, float pad, BuildOut* out, hipStream_t stream);
+size_t lbvh_sort_temp_bytes(int ntri);
+size_t lbvh_scratch_ints(int ntri);
+void launch_pack_attributes(const float* nrm, const float* uv, const int* mat, int ntri, float* attr,
+                            hipStream_t stream);
+
+// math self-test hook (tests/test_gpu_*): evaluates the shared math on the device
+void launch_selftest_math(const float* in, int n, float* out, hipStream_t stream);
+
+}  // namespace pgrt

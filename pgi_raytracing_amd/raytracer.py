@@ -1,0 +1,267 @@
+"""Python host API over libpgrt's C ABI, mirroring the reference's renderer interface.
+
+Reference: ``class Raytracer`` (src/pg/pg1_embree/raytracer.h:15-52) with ``LoadScene``
+(raytracer.cpp:48-128), ``get_pixel`` (:396-437, driven per pixel by SimpleGuiDX11::Producer,
+simpleguidx11.cpp:86-128), ``gamma_level`` (:23) and ``trace``'s ray query ``get_ray_hit``
+(:130-148).  Here a frame is rendered in one call on the GPU (``render``) and ``get_pixel``
+reads the last frame; ``intersect`` is the batched ``rtcIntersect1``.
+
+There is no CPU fallback: if libpgrt.so (the gfx950 HIP build) cannot be loaded, importing
+this module's ``lib()`` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+from .scene import LightData, MaterialData, Scene, TextureData
+
+_LIB = None
+
+
+class PgrtError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{abi.ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+def lib():
+    """Load libpgrt.so (raises if it is missing -- the product never falls back to the CPU)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(abi.LIB_PATH):
+        raise ImportError(f"{abi.LIB_PATH} not built: run `make` (or __graft_entry__.build())")
+    L = C.CDLL(abi.LIB_PATH)
+    vp, ip, fp = C.c_void_p, C.c_int, C.POINTER(C.c_float)
+    sig = {
+        "pgrt_version": (C.c_char_p, []),
+        "pgrt_device_count": (ip, [C.POINTER(C.c_int)]),
+        "pgrt_create": (ip, [ip, C.POINTER(vp)]),
+        "pgrt_destroy": (None, [vp]),
+        "pgrt_last_error": (C.c_char_p, [vp]),
+        "pgrt_set_scene": (ip, [vp, C.POINTER(abi.SceneDesc)]),
+        "pgrt_bvh_get_info": (ip, [vp, C.POINTER(abi.BvhInfo)]),
+        "pgrt_set_camera": (ip, [vp, C.POINTER(abi.Camera)]),
+        "pgrt_render": (ip, [vp, C.POINTER(abi.RenderParams), fp, C.POINTER(abi.Stats)]),
+        "pgrt_render_device": (ip, [vp, C.POINTER(abi.RenderParams), vp, C.POINTER(abi.Stats)]),
+        "pgrt_device_alloc": (ip, [vp, C.c_size_t, C.POINTER(vp)]),
+        "pgrt_device_free": (ip, [vp, vp]),
+        "pgrt_copy_to_host": (ip, [vp, vp, vp, C.c_size_t]),
+        "pgrt_synchronize": (ip, [vp]),
+        "pgrt_intersect_closest": (ip, [vp, fp, ip, fp]),
+        "pgrt_tile_count": (ip, [ip, ip, ip, ip, ip]),
+        "pgrt_tile_rect": (ip, [ip, ip, ip, ip, C.POINTER(C.c_int)]),
+        "pgrt_unpack_tiles_host": (ip, [ip, ip, ip, ip, fp, fp]),
+        "pgrt_comm_unique_id": (ip, [C.c_char_p]),
+        "pgrt_comm_init": (ip, [vp, ip, ip, C.c_char_p]),
+        "pgrt_render_distributed": (ip, [vp, C.POINTER(abi.RenderParams), fp, C.POINTER(abi.Stats)]),
+        "pgrt_render_distributed_device": (ip, [vp, C.POINTER(abi.RenderParams), vp, C.POINTER(abi.Stats)]),
+        "pgrt_obj_load": (ip, [C.c_char_p, ip, C.POINTER(vp)]),
+        "pgrt_obj_free": (None, [vp]),
+        "pgrt_obj_error": (C.c_char_p, []),
+        "pgrt_obj_scene": (ip, [vp, C.POINTER(abi.SceneDesc)]),
+        "pgrt_obj_counts": (ip, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+        "pgrt_obj_texture_path": (C.c_char_p, [vp, ip]),
+        "pgrt_obj_material_name": (C.c_char_p, [vp, ip]),
+        "pgrt_obj_surface_range": (ip, [vp, ip, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+        "pgrt_selftest_math": (ip, [vp, fp, ip, fp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _LIB = L
+    return L
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    lib().pgrt_device_count(C.byref(n))
+    return n.value
+
+
+def _check(ctx, rc: int):
+    if rc != abi.PGRT_OK:
+        msg = lib().pgrt_last_error(ctx).decode() if ctx else ""
+        raise PgrtError(rc, msg)
+
+
+class Context:
+    """One libpgrt context on one HIP device (one process per GPU)."""
+
+    def __init__(self, device: int = 0):
+        self.L = lib()
+        h = C.c_void_p()
+        rc = self.L.pgrt_create(device, C.byref(h))
+        if rc != abi.PGRT_OK:
+            raise PgrtError(rc, f"pgrt_create(device={device})")
+        self.h = h
+        self.device = device
+        self.scene = None
+        self.camera = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.pgrt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def set_scene(self, scene: Scene):
+        d = scene.desc()
+        _check(self.h, self.L.pgrt_set_scene(self.h, C.byref(d)))
+        self.scene = scene
+
+    def bvh_info(self) -> abi.BvhInfo:
+        info = abi.BvhInfo()
+        _check(self.h, self.L.pgrt_bvh_get_info(self.h, C.byref(info)))
+        return info
+
+    def set_camera(self, cam: abi.Camera):
+        _check(self.h, self.L.pgrt_set_camera(self.h, C.byref(cam)))
+        self.camera = cam
+
+    def render(self, params: abi.RenderParams):
+        w = params.rect_w if params.rect_w > 0 else self.camera.width
+        h = params.rect_h if params.rect_h > 0 else self.camera.height
+        out = np.empty((h, w, 4), np.float32)
+        st = abi.Stats()
+        _check(self.h, self.L.pgrt_render(self.h, C.byref(params), abi.fptr(out), C.byref(st)))
+        return out, st
+
+    def render_device(self, params: abi.RenderParams, dev_ptr: int):
+        st = abi.Stats()
+        _check(self.h, self.L.pgrt_render_device(self.h, C.byref(params), C.c_void_p(dev_ptr), C.byref(st)))
+        return st
+
+    def alloc(self, nbytes: int) -> int:
+        p = C.c_void_p()
+        _check(self.h, self.L.pgrt_device_alloc(self.h, nbytes, C.byref(p)))
+        return p.value
+
+    def free(self, ptr: int):
+        _check(self.h, self.L.pgrt_device_free(self.h, C.c_void_p(ptr)))
+
+    def to_host(self, ptr: int, shape, dtype=np.float32) -> np.ndarray:
+        out = np.empty(shape, dtype)
+        _check(self.h, self.L.pgrt_copy_to_host(self.h, out.ctypes.data_as(C.c_void_p), C.c_void_p(ptr),
+                                                out.nbytes))
+        return out
+
+    def synchronize(self):
+        _check(self.h, self.L.pgrt_synchronize(self.h))
+
+    def intersect(self, rays: np.ndarray) -> np.ndarray:
+        """rtcIntersect1 over a batch: rays (n, 8) {org, tnear, dir, tfar} -> (n, 4) {t, u, v, prim}."""
+        rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+        hits = np.zeros((rays.shape[0], 4), np.float32)
+        _check(self.h, self.L.pgrt_intersect_closest(self.h, abi.fptr(rays), rays.shape[0], abi.fptr(hits)))
+        return hits
+
+    def selftest_math(self, pairs: np.ndarray) -> np.ndarray:
+        pairs = np.ascontiguousarray(pairs, np.float32).reshape(-1, 2)
+        out = np.zeros((pairs.shape[0], 8), np.float32)
+        _check(self.h, self.L.pgrt_selftest_math(self.h, abi.fptr(pairs), pairs.shape[0], abi.fptr(out)))
+        return out
+
+    # ---- multi-GPU ----
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = C.create_string_buffer(128)
+        rc = lib().pgrt_comm_unique_id(buf)
+        if rc != abi.PGRT_OK:
+            raise PgrtError(rc, "pgrt_comm_unique_id")
+        return buf.raw
+
+    def comm_init(self, world: int, rank: int, uid: bytes):
+        _check(self.h, self.L.pgrt_comm_init(self.h, world, rank, C.c_char_p(uid)))
+
+    def render_distributed_device(self, params, dev_ptr: int | None):
+        st = abi.Stats()
+        _check(self.h, self.L.pgrt_render_distributed_device(self.h, C.byref(params),
+                                                             C.c_void_p(dev_ptr or 0), C.byref(st)))
+        return st
+
+    def render_distributed(self, params):
+        out = np.empty((self.camera.height, self.camera.width, 4), np.float32)
+        st = abi.Stats()
+        _check(self.h, self.L.pgrt_render_distributed(self.h, C.byref(params), abi.fptr(out), C.byref(st)))
+        return out, st
+
+
+# ---------------------------------------------------------------- scene ingest (product path)
+
+def load_obj(obj_path: str, flip_yz: bool = False) -> Scene:
+    """LoadOBJ/LoadMTL (objloader.cpp:53-507) through the C++ loader in libpgrt, textures
+    decoded host-side (Texture::Texture, texture.cpp:5-54)."""
+    L = lib()
+    h = C.c_void_p()
+    rc = L.pgrt_obj_load(obj_path.encode(), int(flip_yz), C.byref(h))
+    if rc != abi.PGRT_OK:
+        raise PgrtError(rc, L.pgrt_obj_error().decode())
+    try:
+        d = abi.SceneDesc()
+        L.pgrt_obj_scene(h, C.byref(d))
+        n = d.num_triangles
+        pos = np.ctypeslib.as_array(d.positions, shape=(9 * n,)).copy()
+        nrm = np.ctypeslib.as_array(d.normals, shape=(9 * n,)).copy()
+        uv = np.ctypeslib.as_array(d.uvs, shape=(6 * n,)).copy()
+        mid = np.ctypeslib.as_array(d.material_ids, shape=(n,)).copy()
+        ns, nm, nt = C.c_int(), C.c_int(), C.c_int()
+        L.pgrt_obj_counts(h, C.byref(ns), C.byref(nm), C.byref(nt))
+        mats = []
+        for i in range(nm.value):
+            m = d.materials[i]
+            mats.append(MaterialData(L.pgrt_obj_material_name(h, i).decode(), tuple(m.diffuse), tuple(m.specular),
+                                     m.shininess, m.ior, m.type, m.diffuse_tex))
+        textures = [TextureData.from_file(L.pgrt_obj_texture_path(h, i).decode()) for i in range(nt.value)]
+        surfaces = []
+        for i in range(ns.value):
+            f, c = C.c_int(), C.c_int()
+            L.pgrt_obj_surface_range(h, i, C.byref(f), C.byref(c))
+            surfaces.append(("", f.value, c.value))
+    finally:
+        L.pgrt_obj_free(h)
+    return Scene(pos, nrm, uv, mid, mats, textures, -1, [LightData()], surfaces)
+
+
+class Raytracer:
+    """Raytracer(width, height, fov_y, view_from, view_at) (raytracer.h:18-20)."""
+
+    def __init__(self, width: int, height: int, fov_y: float, view_from, view_at, device: int = 0):
+        self.ctx = Context(device)
+        self.camera = abi.make_camera(width, height, fov_y, view_from, view_at)
+        self.ctx.set_camera(self.camera)
+        self.gamma_level = 0.5  # UI slider default (raytracer.cpp:450,464-465)
+        self.frame = None
+        self.scene = None
+
+    def LoadScene(self, object_file_name: str, background_file_name: str | None = None):  # noqa: N802
+        sc = load_obj(object_file_name)
+        if background_file_name:
+            sc.set_environment(background_file_name)
+        self.load_scene(sc)
+
+    def load_scene(self, scene: Scene):
+        self.ctx.set_scene(scene)
+        self.scene = scene
+
+    def render(self, params: abi.RenderParams | None = None, **kw):
+        if params is None:
+            kw.setdefault("gamma_level", self.gamma_level)
+            params = abi.make_params(**kw)
+        self.frame, st = self.ctx.render(params)
+        return self.frame, st
+
+    def get_pixel(self, x: int, y: int, t: float = 0.0):  # noqa: ARG002 (t is unused, as in the reference)
+        if self.frame is None:
+            self.render()
+        return self.frame[y, x].copy()
+
+    def intersect(self, rays):
+        return self.ctx.intersect(rays)

@@ -1,0 +1,144 @@
+"""C ABI of libpgrt.so without a GPU: it loads, exports every symbol include/pgrt.h declares,
+fails loudly (no CPU fallback) when no device is visible, and its host-side pieces (tile
+plan, tile unpack, OBJ/MTL ingest) behave like the reference."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from pgi_raytracing_amd import abi
+from pgi_raytracing_amd.raytracer import lib, load_obj
+
+HEADER = os.path.join(ROOT, "include", "pgrt.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(pgrt_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = lib()
+    names = declared_functions()
+    assert len(names) >= 30
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    # and the shared library is the in-tree gfx950 build
+    assert os.path.realpath(L._name) == os.path.realpath(abi.LIB_PATH)
+    assert b"gfx950" in L.pgrt_version()
+
+
+def test_create_without_device_fails_loudly():
+    from pgi_raytracing_amd.raytracer import device_count
+
+    if device_count() > 0:
+        pytest.skip("a GPU is visible")
+    h = C.c_void_p()
+    assert lib().pgrt_create(0, C.byref(h)) == -8  # PGRT_ERR_NO_DEVICE, never a CPU fallback
+    assert not h.value
+
+
+def test_argument_validation():
+    L = lib()
+    assert L.pgrt_render(None, None, None, None) == -1
+    assert L.pgrt_tile_count(0, 10, 64, 0, 1) == -1
+    assert L.pgrt_tile_count(100, 100, 64, 2, 2) == -1
+
+
+@pytest.mark.parametrize("W,H,world", [(1920, 1080, 8), (640, 480, 3), (100, 70, 2), (64, 64, 4)])
+def test_tile_plan_partitions_the_frame(W, H, world):
+    L = lib()
+    tiles_x, tiles_y = -(-W // 64), -(-H // 64)
+    counts = [L.pgrt_tile_count(W, H, 64, r, world) for r in range(world)]
+    assert sum(counts) == tiles_x * tiles_y
+    assert max(counts) - min(counts) <= 1
+    cover = np.zeros((H, W), np.int32)
+    rect = (C.c_int * 4)()
+    for t in range(tiles_x * tiles_y):
+        assert L.pgrt_tile_rect(W, H, 64, t, rect) == 0
+        x, y, w, h = rect
+        cover[y:y + h, x:x + w] += 1
+    assert (cover == 1).all()
+
+
+@pytest.mark.parametrize("W,H,world", [(200, 130, 3), (64, 64, 1), (130, 70, 4)])
+def test_unpack_tiles_host(W, H, world):
+    """Rank-major gathered tiles (tile t on rank t % world) reassemble into the frame."""
+    L = lib()
+    T = 64
+    tx, ty = -(-W // T), -(-H // T)
+    total = tx * ty
+    per_rank = -(-total // world)
+    frame = np.random.default_rng(0).random((H, W, 4), dtype=np.float32)
+    g = np.zeros((world, per_rank, T, T, 4), np.float32)
+    for t in range(total):
+        r, j = t % world, t // world
+        x0, y0 = (t % tx) * T, (t // tx) * T
+        blk = frame[y0:y0 + T, x0:x0 + T]
+        g[r, j, :blk.shape[0], :blk.shape[1]] = blk
+    out = np.zeros_like(frame)
+    assert L.pgrt_unpack_tiles_host(W, H, T, world, abi.fptr(g.reshape(-1)), abi.fptr(out.reshape(-1))) == 0
+    assert (out == frame).all()
+
+
+def test_cpp_loader_matches_reference_restatement(avenger_obj):
+    """pgrt_obj_load (C++) == the Python restatement of LoadOBJ, array for array."""
+    import pyoracle
+
+    ref = pyoracle.scene_from_obj_ref(avenger_obj)
+    got = load_obj(avenger_obj)
+    assert got.num_triangles == ref.num_triangles == sum(s[2] for s in ref.surfaces)
+    assert len(got.surfaces) == 94  # "Surfaces = 94" (data/raytraced_avenger.png)
+    assert len(got.materials) == 5 + 1  # 5 MTL materials + trailing default Material()
+    for name in ("positions", "normals", "uvs", "material_ids"):
+        assert (getattr(got, name) == getattr(ref, name)).all(), name
+    ks = {m.name: m.specular for m in got.materials}
+    # "Ks 1.0. 1.0 1.0": sscanf reads only the first float (objloader.cpp:150-153)
+    assert np.allclose(ks["black_plastic"], (1.0, 0.8, 0.8))
+    glass = [m for m in got.materials if m.name == "green_plastic_transparent"][0]
+    assert glass.type == 4 and abs(glass.ior - 1.5) < 1e-7 and np.allclose(glass.diffuse, (0.85, 1.0, 0.01))
+    assert [os.path.basename(t.name) for t in got.textures] == ["4150p04.jpg", "3069bp13.jpg"]
+
+
+def test_cpp_loader_quirks(tmp_path):
+    import pyoracle  # noqa: F401
+    from objloader_ref import load_obj as ref_load
+
+    (tmp_path / "m.mtl").write_text(
+        "newmtl a\n\tKd 0.1 0.2 0.3\n\tshader 4\n\tNi 1.33\n\n# comment\nnewmtl b\nKs 0.5\nNs 16\n"
+        "newmtl a\nKd 0.9 0.9 0.9\n")
+    (tmp_path / "s.obj").write_text(
+        "mtllib m.mtl\n"
+        "v 0 0 0\nv 1 0 0\nv 1 1 0\nv 0 1 0\n\n\nv 0 0 1\n"
+        "vn 0 0 2\nvn 0 0 -3\n"
+        "vt 0 0\nvt 1 0\nvt 1 1\nvt 0 1\n"
+        "g first\nusemtl b\nf 1/1/1 2/2/1 3/3/1 4/4/1\nusemtl a\n"
+        "f 1/1/2 2/2/2 5/3/2   \n"  # trailing spaces trimmed before counting
+        "g second\nusemtl nosuch\nf 2/2/1 3/3/1 5/1/1\n"
+        "g third\nusemtl b\nf 1/1/1 2/2/1 3/3/1 4/4/1 5/1/1\n")  # 5 spaces: re-uses previous tokens
+    got = load_obj(str(tmp_path / "s.obj"))
+    surfaces, mats = ref_load(str(tmp_path / "s.obj"))
+    # the file's last material is appended without the MaterialExists check (:193-198)
+    assert [m["name"] for m in mats] == [m.name for m in got.materials[:-1]] == ["a", "b", "a"]
+    assert got.surfaces[0][2] == 3 and got.surfaces[1][2] == 1 and got.surfaces[2][2] == 1
+    # group 'first' closes with the LAST usemtl (a, first match wins); 'second' has an
+    # unknown name -> trailing default material; 'third' re-uses the previous face tokens
+    assert list(got.material_ids) == [0, 0, 0, 3, 1]
+    pos = np.concatenate([s["positions"].reshape(-1) for s in surfaces])
+    assert (got.positions == pos).all()
+    assert np.allclose(got.normals.reshape(-1, 3)[0], (0, 0, 1))  # vn normalised
+    a = got.materials[0]
+    assert a.type == 4 and abs(a.ior - 1.33) < 1e-6 and np.allclose(a.diffuse, (0.1, 0.2, 0.3))
+    b = got.materials[1]
+    assert np.allclose(b.specular, (0.5, 0.8, 0.8)) and b.shininess == 16.0
+
+
+def test_loader_missing_file_reports_error():
+    from pgi_raytracing_amd.raytracer import PgrtError
+
+    with pytest.raises(PgrtError):
+        load_obj("/nonexistent/file.obj")

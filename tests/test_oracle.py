@@ -1,0 +1,236 @@
+"""The CPU restatement (oracle/) against the reference's own known-answer demos and against
+independent checks.  No GPU needed.
+
+Pins (reference demos with derivable outputs):
+  * tutorial_1 (tutorials.cpp:29-139): one triangle (0,0,0),(2,0,0),(0,3,0), ray from
+    (0.1,0.2,2) along -z, tnear FLT_MIN -> prints normal = (0.000, 0.000, 1.000),
+    tex_coord = (0.050, 0.933); the hit is t = 2, u = 0.05, v = 1/15.
+  * tutorial_2 (tutorials.cpp:170-178): Texture("test4.png").get_texel(2.5/64, 0) -> prints
+    (r = 1.000, g = 0.000, b = 0.500) (texture.cpp:96-99,125-127 put all weight on row 0).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle
+from conftest import ASSETS, ENV_MAP
+from pgi_raytracing_amd import abi
+from pgi_raytracing_amd.scene import TextureData, single_triangle_scene
+
+FLT_MIN = np.float32(1.17549435e-38)
+FLT_MAX = np.float32(3.402823466e38)
+
+
+def interp(a0, a1, a2, u, v):
+    """rtcInterpolate0's madd(w,p0,madd(u,p1,v*p2)) (exact via float64 for the KAT print)."""
+    w = np.float32(np.float32(1) - u) - v
+    return np.float32(w * np.float64(a0) + (u * np.float64(a1) + np.float64(v * a2)))
+
+
+def test_tutorial1_kat():
+    sc = single_triangle_scene()
+    o = pyoracle.OracleScene(sc, accel=0)
+    ray = np.array([0.1, 0.2, 2.0, FLT_MIN, 0.0, 0.0, -1.0, FLT_MAX], np.float32)
+    t, u, v, prim = o.intersect(ray)[0]
+    assert prim.view(np.int32) == 0
+    assert t == np.float32(2.0)
+    assert f"{u:0.3f}" == "0.050" and abs(v - 1 / 15) < 1e-6
+    n = [interp(sc.normals[k], sc.normals[3 + k], sc.normals[6 + k], u, v) for k in range(3)]
+    tc = [interp(sc.uvs[k], sc.uvs[2 + k], sc.uvs[4 + k], u, v) for k in range(2)]
+    assert "normal = (%0.3f, %0.3f, %0.3f)" % tuple(n) == "normal = (0.000, 0.000, 1.000)"
+    assert "tex_coord = (%0.3f, %0.3f)" % tuple(tc) == "tex_coord = (0.050, 0.933)"
+    # the same query through the oracle's BVH
+    assert (pyoracle.OracleScene(sc, accel=1).intersect(ray) == o.intersect(ray)).all()
+
+
+def test_tutorial1_miss_and_range():
+    o = pyoracle.OracleScene(single_triangle_scene(), accel=1)
+    rays = np.array([
+        [3.0, 3.0, 2.0, 0.0, 0.0, 0.0, -1.0, FLT_MAX],  # outside the triangle
+        [0.1, 0.2, 2.0, 0.0, 0.0, 0.0, -1.0, 1.5],      # tfar before the hit
+        [0.1, 0.2, 2.0, 2.0, 0.0, 0.0, -1.0, FLT_MAX],  # tnear == t: (tnear, tfar] excludes it
+        [0.1, 0.2, 2.0, 0.0, 0.0, 0.0, -1.0, 2.0],      # tfar == t: included
+    ], np.float32)
+    h = o.intersect(rays)
+    prims = h[:, 3].view(np.int32)
+    assert list(prims) == [-1, -1, -1, 0]
+
+
+def test_tutorial2_kat():
+    tex = TextureData.from_file(os.path.join(ASSETS, "test4.png"))
+    assert (tex.width, tex.height, tex.bpp) == (64, 32, 4)
+    c = pyoracle.get_texel(tex, (np.float32(1.0) / np.float32(64)) * np.float32(2.5), 0.0)
+    assert "(r = %0.3f, g = %0.3f, b = %0.3f)" % tuple(c) == "(r = 1.000, g = 0.000, b = 0.500)"
+
+
+def test_texel_quirks():
+    tex = TextureData.from_file(os.path.join(ASSETS, "test3.png"))  # 64x32 RGB
+    # x in [0,1) -> x1 bumped to 1 == x2 -> black; integer coordinates -> black
+    assert (pyoracle.get_texel(tex, 0.5 / 64, 0.5) == 0).all()
+    assert (pyoracle.get_texel(tex, 10 / 64, 0.5) == 0).all()
+    # v*h in (h-1, h): y2 = tmp_y1 = y1 -> black
+    assert (pyoracle.get_texel(tex, 10.5 / 64, 31.5 / 32) == 0).all()
+    # interior: bilinear of the four BGR texels, r-field = B byte
+    img = np.frombuffer(tex.data, np.uint8).reshape(32, tex.pitch)[:, : 64 * 3].reshape(32, 64, 3)
+    x, y = np.float32(10.25), np.float32(5.5)
+    got = pyoracle.get_texel(tex, x / 64, y / 32)
+    p = img.astype(np.float32) / np.float32(255.0)
+    f1 = p[5, 10] * np.float32(0.75) + p[5, 11] * np.float32(0.25)
+    f2 = p[6, 10] * np.float32(0.75) + p[6, 11] * np.float32(0.25)
+    exp = f1 * np.float32(0.5) + f2 * np.float32(0.5)
+    assert np.allclose(got, exp, atol=1e-6)
+
+
+def test_camera_basis_matches_survey_values():
+    """PinHoleCamera ctor for raytrace_loop's pose (tutorials.cpp:186-191)."""
+    for h, fy in ((480, 622.217), (1080, 1399.988), (2160, 2799.977)):
+        b = pyoracle.camera_basis(abi.default_camera(h * 4 // 3, h))
+        assert abs(b[0] - fy) < 2e-3
+    m = pyoracle.camera_basis(abi.default_camera(640, 480))[1:].reshape(3, 3)
+    assert np.allclose(m[:, 0], [0.78087, -0.62470, 0.0], atol=1e-4)
+    assert np.allclose(m[:, 1], [0.10976, 0.13720, 0.98444], atol=1e-4)
+    assert np.allclose(m[:, 2], [-0.61498, -0.76872, 0.17571], atol=1e-4)
+
+
+def test_pinhole_uses_integer_half_size():
+    cam = abi.default_camera(641, 481)  # odd sizes: W/2 = 320, H/2 = 240 (int division)
+    r = pyoracle.generate_ray(cam, 320.0, 240.0)
+    b = pyoracle.camera_basis(cam)
+    assert np.allclose(r[3:6], -b[1:].reshape(3, 3)[:, 2], atol=1e-6)  # straight down -z_c
+    assert r[6] == np.float32(0.001)
+    rd = pyoracle.generate_ray(cam, 320.0, 240.0, dof=1, focal=200.0, aperture=5.0, r1=1.0, r2=-2.0)
+    assert rd[6] == np.float32(0.01)
+    # thin lens: every lens offset still passes through the focal point
+    fp = r[:3] + 200.0 * r[3:6]
+    t = np.dot(fp - rd[:3], rd[3:6])
+    assert np.linalg.norm(rd[:3] + t * rd[3:6] - fp) < 1e-3
+
+
+def _X(u):  # _expand restated in float64 (utils.cpp:211-216)
+    if u <= 0:
+        return 0.0
+    if u >= 1:
+        return 1.0
+    if u <= 0.04045:
+        return np.float32(u / 12.92)
+    return np.float32(((u + 0.055) / 1.055) ** 2.4)
+
+
+def _C(u):  # _compress restated (utils.cpp:204-209): note the missing 1.055 factor
+    if u <= 0:
+        return 0.0
+    if u >= 1:
+        return 1.0
+    if u <= 0.0031308:
+        return np.float32(12.92 * u)
+    return np.float32(1.00 * u ** (1 / 2.4) - 0.055)
+
+
+@pytest.mark.parametrize("libm", [False, True])
+def test_mix_srgb_channel_swaps(libm):
+    c0 = np.array([0.2, 0.5, 0.8, 1.0], np.float32)
+    c1 = np.array([0.9, 0.1, 0.3, 1.0], np.float32)
+    a = np.float32(0.25)
+    got = pyoracle.mix_srgb(c0, c1, a, libm=libm)
+    # out.r is built from the inputs' .b (expand, mix_linear and compress each swap r<->b)
+    for k_out, k_in in ((0, 2), (1, 1), (2, 0)):
+        x0, x1 = np.float32(_X(float(c0[k_in]))), np.float32(_X(float(c1[k_in])))
+        m = np.float32(a * x0 + np.float32(1 - a) * x1)
+        assert abs(got[k_out] - _C(float(m))) <= 2e-7
+    assert got[3] == np.float32(0.1)
+
+
+def test_compress_expand_edges():
+    L = pyoracle.lib()
+    assert L.orc_compress(-1.0) == 0.0 and L.orc_compress(1.0) == 1.0 and L.orc_compress(2.0) == 1.0
+    assert abs(L.orc_compress(0.5) - (0.5 ** (1 / 2.4) - 0.055)) < 1e-7
+    assert abs(L.orc_expand(0.02) - 0.02 / 12.92) < 1e-9
+    assert abs(L.orc_expand(0.5) - ((0.5 + 0.055) / 1.055) ** 2.4) < 1e-7
+
+
+def test_gamma_squares_sqrt_and_nan_for_negative():
+    g = pyoracle.gamma([0.25, 0.5, -0.1, 1.0], 0.5)
+    # Color4f{b,g,r} in, swapped back out: out = (f(in.b), f(in.g), f(in.r))
+    assert np.isnan(g[0]) and abs(g[1] - 0.5) < 1e-7 and abs(g[2] - 0.25) < 1e-7 and g[3] == 1.0
+
+
+def test_jitter_is_counter_based_and_in_range():
+    L = pyoracle.lib()
+    import ctypes as C
+
+    out = (C.c_float * 4)()
+    vals = []
+    for pixel in range(200):
+        L.orc_jitter(1234, 0, pixel, 3, out)
+        vals += list(out)
+    v = np.array(vals)
+    assert (v >= 0).all() and (v < 1).all() and 0.4 < v.mean() < 0.6
+    L.orc_jitter(1234, 0, 7, 3, out)
+    a = list(out)
+    L.orc_jitter(1234, 0, 7, 3, out)
+    assert a == list(out)
+
+
+def test_bvh_equals_brute_force(avenger_scene):
+    """The oracle's own SAH BVH returns exactly the brute-force closest hit (t, u, v, prim)."""
+    rng = np.random.default_rng(1)
+    n = 3000
+    lo = np.array([-150, -150, -50], np.float32)
+    hi = np.array([150, 150, 150], np.float32)
+    org = rng.uniform(lo, hi, size=(n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.concatenate([org, np.full((n, 1), 0.01, np.float32), d, np.full((n, 1), FLT_MAX, np.float32)], 1)
+    # also aim at triangle vertices and edges (ties, grazing hits)
+    p = avenger_scene.positions.reshape(-1, 3, 3)
+    idx = rng.integers(0, p.shape[0], size=500)
+    target = 0.5 * (p[idx, 0] + p[idx, 1])
+    o2 = np.array([-140, -175, 80], np.float32) + np.zeros((500, 3), np.float32)
+    d2 = (target - o2).astype(np.float32)
+    rays2 = np.concatenate([o2, np.full((500, 1), 0.001, np.float32), d2, np.full((500, 1), FLT_MAX, np.float32)], 1)
+    rays = np.concatenate([rays, rays2]).astype(np.float32)
+    hb = pyoracle.OracleScene(avenger_scene, accel=1).intersect(rays)
+    hf = pyoracle.OracleScene(avenger_scene, accel=0).intersect(rays)
+    assert (hb.view(np.int32) == hf.view(np.int32)).all()
+    assert (hb[:, 3].view(np.int32) >= 0).sum() > 500
+
+
+def test_libm_and_detmath_oracles_agree(avenger_scene):
+    """pgrt_detmath.h vs glibc transcendentals.  A 1-ulp change of the env-map coordinate u
+    (float, ~6e-8) moves the sample by 4000 * 6e-8 = 2.4e-4 texel on the 4000-px map, so a
+    colour can move by up to ~2.4e-4 x the local texel gradient; everything else agrees to
+    float rounding.  (GPU and oracle share pgrt_detmath.h, so they agree bit for bit.)"""
+    cam = abi.default_camera(80, 60)
+    p = abi.make_params(spp_side=1, max_level=5)
+    a, _ = pyoracle.OracleScene(avenger_scene, libm=False).render(cam, p)
+    b, _ = pyoracle.OracleScene(avenger_scene, libm=True).render(cam, p)
+    assert (np.isnan(a) == np.isnan(b)).all()
+    d = np.nan_to_num(np.abs(a - b))
+    assert d.max() < 5e-4
+    assert (d > 1e-6).mean() < 0.05
+
+
+def test_oracle_frame_basic_properties(avenger_scene):
+    cam = abi.default_camera(64, 48)
+    img, st = pyoracle.OracleScene(avenger_scene).render(cam, abi.make_params(spp_side=1, max_level=5))
+    assert st.rays_primary == 64 * 48
+    assert st.rays_shadow > 0 and st.rays_reflect > 0 and st.rays_refract > 0
+    assert (img[..., 3] == 1).all()
+    assert np.isfinite(img).mean() > 0.9
+    # rendering a sub-rectangle gives the same pixels
+    sub, _ = pyoracle.OracleScene(avenger_scene).render(cam, abi.make_params(spp_side=1, max_level=5,
+                                                                            rect=(10, 20, 30, 16)))
+    assert (np.nan_to_num(sub, nan=7) == np.nan_to_num(img[20:36, 10:40], nan=7)).all()
+
+
+def test_env_map_lookup_orientation():
+    tex = TextureData.from_file(ENV_MAP)
+    near_up = pyoracle.env_texel(tex, 0.001, 0.0, 1.0)  # v*h in (0,1): y1 bumped to 1 == y2 -> black
+    assert (near_up[:3] == 0).all() and near_up[3] == 1.0
+    up = pyoracle.env_texel(tex, 0.3, 0.2, 1.0)
+    assert up[:3].sum() > 0 and up[3] == 1.0
+    axis = pyoracle.env_texel(tex, 1.0, 0.0, 0.0)  # u = 0.75 -> x = 3000 exactly: black quirk
+    assert (axis[:3] == 0).all()
+    side = pyoracle.env_texel(tex, 1.0, 0.3, 0.1)
+    assert side[3] == 1.0 and side[:3].sum() > 0
