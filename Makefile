@@ -10,7 +10,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off \
             -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -I$(SRC) -Wall -Wno-unused-result
 OBJS := $(BUILD)/trace.o $(BUILD)/render.o $(BUILD)/bvh.o $(BUILD)/context.o $(BUILD)/objloader.o
 
-all: $(LIBDIR)/libpgrt.so oracle
+all: $(LIBDIR)/libpgrt.so oracle $(BUILD)/pg1_pgrt
 
 $(BUILD) $(LIBDIR):
 	mkdir -p $@
@@ -25,6 +25,10 @@ $(BUILD)/%.o: $(SRC)/%.cpp $(HDRS) | $(BUILD)
 
 $(LIBDIR)/libpgrt.so: $(OBJS) | $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+
+# C++ host example over the C ABI (include/pgrt_raytracer.hpp)
+$(BUILD)/pg1_pgrt: examples/pg1_pgrt.cpp include/pgrt_raytracer.hpp include/pgrt.h $(LIBDIR)/libpgrt.so | $(BUILD)
+	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ $< -L$(LIBDIR) -lpgrt -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
 
 oracle:
 	$(MAKE) -C oracle

@@ -748,7 +748,6 @@ int pgrt_comm_init(pgrt_ctx* ctx, int world, int rank, const char id[128]) {
         }
         ctx->world = world;
         ctx->rank = rank;
-        if (world == 1) return;
         ncclUniqueId u;
         std::memcpy(u.internal, id, 128);
         ncclResult_t r = ncclCommInitRank(&ctx->comm, world, u, rank);
@@ -772,7 +771,7 @@ int pgrt_render_distributed_device(pgrt_ctx* ctx, const pgrt_render_params* p, v
             PGRT_HIP(hipMemsetAsync(ctx->tilebuf.p, 0, ctx->tilebuf.bytes(), ctx->stream));
         render_tiles(ctx, p, mine, ctx->tilebuf.p, 1, 0, 0, 0, st);
         auto tg = std::chrono::steady_clock::now();
-        if (ctx->world == 1) {
+        if (ctx->world == 1 && !ctx->comm) {
             launch_unpack_tiles(ctx->tilebuf.p, static_cast<float*>(rgba_device), W, H, 1, per_rank, ctx->stream);
         } else {
             PGRT_REQUIRE(ctx->comm, PGRT_ERR_RCCL, "pgrt_comm_init has not been called");

@@ -1,0 +1,67 @@
+"""include/pgrt_detmath.h (host build, via the oracle library) against float64 references.
+
+The functions replace the reference's calls to expf/powf (float), pow (double) and the float
+atan2/asin overloads; GPU and oracle both use them (bit-identity is checked on the device in
+tests/test_gpu_parity.py::test_device_math_bit_exact)."""
+import numpy as np
+
+import pyoracle
+from pgi_raytracing_amd import abi
+
+
+def _eval(a, b):
+    pairs = np.ascontiguousarray(np.stack([a, b], 1).astype(np.float32))
+    out = np.zeros((pairs.shape[0], 8), np.float32)
+    pyoracle.lib().orc_detmath_eval(abi.fptr(pairs.reshape(-1)), pairs.shape[0], abi.fptr(out.reshape(-1)))
+    return out
+
+
+def _ulps(x, ref):
+    x = x.astype(np.float32)
+    ref = ref.astype(np.float32)
+    xi = x.view(np.int32).astype(np.int64)
+    ri = ref.view(np.int32).astype(np.int64)
+    xi = np.where(xi < 0, -(xi & 0x7FFFFFFF), xi)
+    ri = np.where(ri < 0, -(ri & 0x7FFFFFFF), ri)
+    return np.abs(xi - ri)
+
+
+def test_pow_exp_within_one_ulp():
+    rng = np.random.default_rng(0)
+    a = np.concatenate([rng.uniform(0, 2, 20000), rng.uniform(-1, 1, 5000), 10 ** rng.uniform(-30, 30, 5000)])
+    b = np.concatenate([rng.uniform(-40, 40, 20000), rng.integers(-8, 40, 5000).astype(np.float64),
+                        rng.uniform(-1.5, 1.5, 5000)])
+    a, b = a.astype(np.float32), b.astype(np.float32)
+    out = _eval(a, b)
+    with np.errstate(all="ignore"):
+        ref_pow = np.power(a.astype(np.float64), b.astype(np.float64))
+        ref_exp = np.exp(a.astype(np.float64))
+    ok = np.isfinite(ref_pow) & (np.abs(ref_pow) < 3e38) & (np.abs(ref_pow) > 1.2e-38)
+    assert (_ulps(out[ok, 2], ref_pow[ok]) <= 1).all()
+    ok = np.abs(ref_exp) < 3e38
+    assert (_ulps(out[ok, 3], ref_exp[ok]) <= 1).all()
+    # negative base: integer exponent keeps the sign rule, non-integer gives NaN (C99 Annex F)
+    s = _eval(np.array([-0.5, -0.5, -2.0, 0.0, -0.0], np.float32), np.array([32.0, 3.0, 0.5, -1.0, 3.0], np.float32))
+    assert s[0, 2] == np.float32(0.5 ** 32) and s[1, 2] == np.float32(-0.125) and np.isnan(s[2, 2])
+    assert np.isinf(s[3, 2]) and s[4, 2] == 0 and np.signbit(s[4, 2])
+
+
+def test_atan2_asin_within_one_ulp():
+    rng = np.random.default_rng(1)
+    v = rng.normal(size=(30000, 3)).astype(np.float32)
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    out = _eval(v[:, 0], v[:, 2])
+    ref = np.arctan2(v[:, 0].astype(np.float64), v[:, 2].astype(np.float64))
+    assert (_ulps(out[:, 4], ref) <= 1).all()
+    ref = np.arcsin(v[:, 0].astype(np.float64))
+    assert (_ulps(out[:, 5], ref) <= 1).all()
+    z = _eval(np.array([0.0, -0.0, 0.0, 1.0], np.float32), np.array([-1.0, -1.0, 1.0, 0.0], np.float32))
+    assert z[0, 4] == np.float32(np.pi) and z[1, 4] == np.float32(-np.pi) and z[2, 4] == 0
+    assert z[3, 4] == np.float32(np.pi / 2) and z[3, 5] == np.float32(np.pi / 2)
+
+
+def test_double_pow_for_srgb():
+    u = np.linspace(0.0032, 1.0, 5000).astype(np.float32)
+    out = _eval(u, np.full_like(u, 1 / 2.4))
+    ref = np.power(u.astype(np.float64), np.float64(np.float32(1 / 2.4)))
+    assert np.max(np.abs(out[:, 7] - ref) / ref) < 1.2e-7
