@@ -205,6 +205,16 @@ const char* pgrt_obj_texture_path(const pgrt_obj* obj, int i);
 const char* pgrt_obj_material_name(const pgrt_obj* obj, int i);
 int pgrt_obj_surface_range(const pgrt_obj* obj, int i, int* first_triangle, int* count);
 
+/* ---- diagnostics of the last pgrt_render* call (traversal counters need profile == 2):
+ *      per level L, rays traced at L and shadow rays emitted at L, with their BVH node visits
+ *      and triangle tests (sum and the maximum of one ray).  Returns the levels filled. ---- */
+typedef struct pgrt_level_diag {
+    uint64_t rays, shadow_rays;
+    uint64_t visits, tests, max_visits, max_tests;
+    uint64_t shadow_visits, shadow_tests, shadow_max_visits, shadow_max_tests;
+} pgrt_level_diag;
+int pgrt_frame_diag(const pgrt_ctx* ctx, pgrt_level_diag* out, int max_levels);
+
 /* ---- test hook: evaluates the shared math of pgrt_detmath.h on the device.  in: n (a,b)
  *      pairs; out: n x 8 {sqrtf(a), a/b, powf(a,b), expf(a), atan2f(a,b), asinf(a),
  *      1/sqrtf(a), (float)pow((double)a,(double)b)} ---- */

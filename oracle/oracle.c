@@ -455,6 +455,7 @@ static Hit scene_intersect(const orc_scene* s, const Ray* r, uint64_t* tests)
             }
             continue;
         }
+        if (tests) ++tests[1]; /* node visits (tests[1] is Counters.visits) */
         float ta, tb;
         int ha = slab(&s->nodes[n->left], o, id, tcur, &ta);
         int hb = slab(&s->nodes[n->right], o, id, tcur, &tb);
@@ -577,7 +578,7 @@ static C4 gamma4(C4 in, float g)
 
 /* ------------------------------------------------------------------ raytracer.cpp */
 typedef struct {
-    uint64_t primary, shadow, reflect, refract, tests;
+    uint64_t primary, shadow, reflect, refract, tests, visits; /* tests, visits adjacent */
 } Counters;
 
 /* Raytracer::is_illuminated + LightSource::GenerateRay (raytracer.cpp:150-176,
@@ -834,20 +835,20 @@ int orc_render(const orc_scene* s, const pgrt_camera* cam, const pgrt_render_par
     int rx = p->rect_x, ry = p->rect_y, rw = p->rect_w, rh = p->rect_h;
     if (rw <= 0 || rh <= 0) { rx = 0; ry = 0; rw = cam->width; rh = cam->height; }
     int nrows = (rh + row_step - 1) / row_step;
-    uint64_t prim = 0, shd = 0, rfl = 0, rfr = 0, tst = 0;
+    uint64_t prim = 0, shd = 0, rfl = 0, rfr = 0, tst = 0, vis = 0;
 #ifdef _OPENMP
     int nt = threads > 0 ? threads : omp_get_max_threads();
-#pragma omp parallel for schedule(dynamic, 1) num_threads(nt) reduction(+ : prim, shd, rfl, rfr, tst)
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nt) reduction(+ : prim, shd, rfl, rfr, tst, vis)
 #endif
     for (int ri = 0; ri < nrows; ++ri) {
-        Counters cn = {0, 0, 0, 0, 0};
+        Counters cn = {0, 0, 0, 0, 0, 0};
         int y = ry + ri * row_step;
         for (int x = rx; x < rx + rw; ++x) {
             C4 c = get_pixel(s, &k, p, x, y, &cn);
             float* o = rgba + ((size_t)(y - ry) * (size_t)rw + (size_t)(x - rx)) * 4;
             o[0] = c.r; o[1] = c.g; o[2] = c.b; o[3] = c.a;
         }
-        prim += cn.primary; shd += cn.shadow; rfl += cn.reflect; rfr += cn.refract; tst += cn.tests;
+        prim += cn.primary; shd += cn.shadow; rfl += cn.reflect; rfr += cn.refract; tst += cn.tests; vis += cn.visits;
     }
     (void)threads;
     if (st) {
@@ -857,6 +858,7 @@ int orc_render(const orc_scene* s, const pgrt_camera* cam, const pgrt_render_par
         st->rays_reflect = rfl;
         st->rays_refract = rfr;
         st->tri_tests = tst;
+        st->node_visits = vis;
     }
     return PGRT_OK;
 }

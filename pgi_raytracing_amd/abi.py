@@ -135,6 +135,11 @@ class Stats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class LevelDiag(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("rays", "shadow_rays", "visits", "tests", "max_visits", "max_tests",
+                                          "shadow_visits", "shadow_tests", "shadow_max_visits", "shadow_max_tests")]
+
+
 class BvhInfo(C.Structure):
     _fields_ = [
         ("num_triangles", C.c_int),

@@ -109,6 +109,9 @@ struct pgrt_ctx {
     DevBuf<int> gstack;
     DevBuf<float> out_tmp;
     StageTimer timer;
+    std::vector<FrameCounters> last_fc;  // per batch, for pgrt_frame_diag
+    int expect_count[kMaxLevels] = {0};   // grid hints from the previous frame (0 = unknown)
+    int expect_shadow[kMaxLevels] = {0};
 
     // multi-GPU
     ncclComm_t comm = nullptr;
@@ -398,23 +401,27 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
                 qc.cap = maxc;
                 qn.cap = std::min(ctx->q_cap, L + 1 < levels ? ctx->level_cap[L + 1] : ctx->q_cap);
                 LevelNodes ln{ctx->n_color[L]->p, ctx->n_link[L]->p, ctx->n_att[L]->p};
+                // grid hints: last frame's per-level counts (+25 %); level 0 is exact
+                const int ex = L == 0 ? n0 : ctx->expect_count[L];
+                const int exs = ctx->expect_shadow[L];
                 id = ctx->timer.begin(s, CAT_TRACE);
-                launch_trace(ctx->view, qc.ro, qc.rd, qc.hit, &fcd->count[L], 0, maxc, ctx->gstack.p,
-                             kTraceGridThreads, fcd->trav, p->profile >= 2, s);
+                launch_trace(ctx->view, qc.ro, qc.rd, qc.hit, &fcd->count[L], 0, maxc, &fcd->fetch[L],
+                             ctx->gstack.p, kTraceGridThreads, fcd->trav[L], p->profile >= 2, s, ex);
                 ctx->timer.end(s, id);
                 ++trace_launches;
                 id = ctx->timer.begin(s, CAT_SHADE);
-                launch_shade(ctx->view, fp, L, qc, qn, ln, sq, fcd, maxc, s);
+                launch_shade(ctx->view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex);
                 ctx->timer.end(s, id);
                 if (ctx->view.nlight > 0 && L < p->max_level) {
                     const int smax = std::min((long long)ctx->s_cap, (long long)maxc * ctx->view.nlight);
                     id = ctx->timer.begin(s, CAT_TRACE);
                     launch_trace(ctx->view, sq.ro, sq.rd, sq.hit, &fcd->shadow_count[L], 0, (int)smax,
-                                 ctx->gstack.p, kTraceGridThreads, fcd->trav, p->profile >= 2, s);
+                                 &fcd->fetch[kMaxLevels + L], ctx->gstack.p, kTraceGridThreads,
+                                 fcd->trav[kMaxLevels + L], p->profile >= 2, s, exs);
                     ctx->timer.end(s, id);
                     ++trace_launches;
                     id = ctx->timer.begin(s, CAT_SHADOW);
-                    launch_shadow_resolve(ctx->view, L, ln, sq, fcd, maxc, s);
+                    launch_shadow_resolve(ctx->view, L, ln, sq, fcd, maxc, s, ex);
                     ctx->timer.end(s, id);
                 }
             }
@@ -422,7 +429,8 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
             for (int L = levels - 2; L >= 0; --L) {
                 LevelNodes ln{ctx->n_color[L]->p, ctx->n_link[L]->p, ctx->n_att[L]->p};
                 LevelNodes lc{ctx->n_color[L + 1]->p, ctx->n_link[L + 1]->p, ctx->n_att[L + 1]->p};
-                launch_combine(L, ln, lc, fcd, L == 0 ? n0 : std::min(ctx->q_cap, ctx->level_cap[L]), s);
+                launch_combine(L, ln, lc, fcd, L == 0 ? n0 : std::min(ctx->q_cap, ctx->level_cap[L]), s,
+                               L == 0 ? n0 : ctx->expect_count[L]);
             }
             LevelNodes l0{ctx->n_color[0]->p, ctx->n_link[0]->p, ctx->n_att[0]->p};
             launch_accumulate(fp, ctx->tiles.p, l0, ctx->accum.p, (int)npix, s0 == 0, s);
@@ -436,6 +444,16 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
         PGRT_HIP(hipGetLastError());
         bool overflow = false;
         for (auto& h : host_fc) overflow |= h.overflow != 0;
+        ctx->last_fc = host_fc;
+        for (int L = 0; L < kMaxLevels; ++L) {  // grid hints for the next frame
+            int c = 0, sc = 0;
+            for (auto& h : host_fc) {
+                c = std::max(c, h.count[L]);
+                sc = std::max(sc, h.shadow_count[L]);
+            }
+            ctx->expect_count[L] = c + c / 4 + 1024;
+            ctx->expect_shadow[L] = sc + sc / 4 + 1024;
+        }
         if (overflow) {
             // grow every level queue to what was requested (2x margin) and redo the frame
             for (auto& h : host_fc)
@@ -482,8 +500,10 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
                     rays_reflect += (uint64_t)(h.count[L] - h.refract[L]);
                 }
             }
-            trav_nodes += h.trav[0];
-            trav_tests += h.trav[1];
+            for (int k = 0; k < 2 * kMaxLevels; ++k) {
+                trav_nodes += h.trav[k][0];
+                trav_tests += h.trav[k][1];
+            }
         }
         break;
     }
@@ -683,8 +703,10 @@ int pgrt_intersect_closest(pgrt_ctx* ctx, const float* rays, int n, float* hits)
         PGRT_HIP(hipMemcpyAsync(ro.p, a.data(), sizeof(float4) * n, hipMemcpyHostToDevice, ctx->stream));
         PGRT_HIP(hipMemcpyAsync(rd.p, b.data(), sizeof(float4) * n, hipMemcpyHostToDevice, ctx->stream));
         if (ctx->gstack.n == 0) ctx->gstack.alloc((size_t)kTraceGridThreads * kGlobalStack);
-        launch_trace(ctx->view, ro.p, rd.p, h.p, nullptr, n, n, ctx->gstack.p, kTraceGridThreads, nullptr, false,
-                     ctx->stream);
+        ctx->fc.alloc(1);
+        PGRT_HIP(hipMemsetAsync(ctx->fc.p, 0, sizeof(FrameCounters), ctx->stream));
+        launch_trace(ctx->view, ro.p, rd.p, h.p, nullptr, n, n, &ctx->fc.p->fetch[0], ctx->gstack.p,
+                     kTraceGridThreads, nullptr, false, ctx->stream);
         PGRT_HIP(hipGetLastError());
         PGRT_HIP(hipMemcpyAsync(hits, h.p, sizeof(float4) * n, hipMemcpyDeviceToHost, ctx->stream));
         PGRT_HIP(hipStreamSynchronize(ctx->stream));
@@ -803,6 +825,27 @@ int pgrt_render_distributed(pgrt_ctx* ctx, const pgrt_render_params* p, float* r
     rc = pgrt_render_distributed_device(ctx, p, ctx->rank == 0 ? ctx->fb_dev.p : nullptr, st);
     if (rc != PGRT_OK || ctx->rank != 0 || !rgba_host) return rc;
     return pgrt_copy_to_host(ctx, rgba_host, ctx->fb_dev.p, (size_t)W * H * 4 * sizeof(float));
+}
+
+int pgrt_frame_diag(const pgrt_ctx* ctx, pgrt_level_diag* out, int max_levels) {
+    if (!ctx || !out || max_levels <= 0) return PGRT_ERR_INVALID_ARGUMENT;
+    const int n = std::min(max_levels, kMaxLevels);
+    std::memset(out, 0, sizeof(pgrt_level_diag) * n);
+    for (const FrameCounters& h : ctx->last_fc)
+        for (int L = 0; L < n; ++L) {
+            pgrt_level_diag& d = out[L];
+            d.rays += (uint64_t)h.count[L];
+            d.shadow_rays += (uint64_t)h.shadow_count[L];
+            d.visits += h.trav[L][0];
+            d.tests += h.trav[L][1];
+            d.max_visits = std::max<uint64_t>(d.max_visits, h.trav[L][2]);
+            d.max_tests = std::max<uint64_t>(d.max_tests, h.trav[L][3]);
+            d.shadow_visits += h.trav[kMaxLevels + L][0];
+            d.shadow_tests += h.trav[kMaxLevels + L][1];
+            d.shadow_max_visits = std::max<uint64_t>(d.shadow_max_visits, h.trav[kMaxLevels + L][2]);
+            d.shadow_max_tests = std::max<uint64_t>(d.shadow_max_tests, h.trav[kMaxLevels + L][3]);
+        }
+    return n;
 }
 
 // test hook: device evaluation of the shared math (sqrt, div, powf, expf, atan2f, asinf, rsqrt, pow)

@@ -16,6 +16,13 @@ namespace pgrt {
 
 constexpr int kBlock = 256;
 
+// grid of a grid-stride kernel: cover the expected count, at most 4096 workgroups
+static int grid_for(int max_count, int expect) {
+    const int n = (expect > 0 && expect < max_count) ? expect : max_count;
+    const int g = ceil_div(n, kBlock);
+    return g < 1 ? 1 : (g > 4096 ? 4096 : g);
+}
+
 // wave-level exclusive prefix allocation: every lane of the wave must call it (k = 0 allowed)
 __device__ __forceinline__ int wave_alloc(int* counter, int k) {
     const int lane = __lane_id();
@@ -277,10 +284,9 @@ __global__ __launch_bounds__(kBlock) void k_shade(SceneView s, FrameParams fp, i
 }
 
 void launch_shade(const SceneView& s, const FrameParams& fp, int level, Queue q, Queue next, LevelNodes nodes,
-                  ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream) {
+                  ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect) {
     if (max_count <= 0) return;
-    int grid = ceil_div(max_count, kBlock);
-    if (grid > 4096) grid = 4096;
+    const int grid = grid_for(max_count, expect);
     hipLaunchKernelGGL(k_shade, dim3(grid), dim3(kBlock), 0, stream, s, fp, level, q, next, nodes, sq, fc);
 }
 
@@ -313,10 +319,9 @@ __global__ __launch_bounds__(kBlock) void k_shadow_resolve(SceneView s, int leve
 }
 
 void launch_shadow_resolve(const SceneView& s, int level, LevelNodes nodes, ShadowQueue sq, const FrameCounters* fc,
-                           int max_count, hipStream_t stream) {
+                           int max_count, hipStream_t stream, int expect) {
     if (max_count <= 0) return;
-    int grid = ceil_div(max_count, kBlock);
-    if (grid > 4096) grid = 4096;
+    const int grid = grid_for(max_count, expect);
     hipLaunchKernelGGL(k_shadow_resolve, dim3(grid), dim3(kBlock), 0, stream, s, level, nodes, sq, fc, max_count);
 }
 
@@ -343,10 +348,9 @@ __global__ __launch_bounds__(kBlock) void k_combine(int level, LevelNodes nodes,
 }
 
 void launch_combine(int level, LevelNodes nodes, LevelNodes child, const FrameCounters* fc, int max_count,
-                    hipStream_t stream) {
+                    hipStream_t stream, int expect) {
     if (max_count <= 0) return;
-    int grid = ceil_div(max_count, kBlock);
-    if (grid > 4096) grid = 4096;
+    const int grid = grid_for(max_count, expect);
     hipLaunchKernelGGL(k_combine, dim3(grid), dim3(kBlock), 0, stream, level, nodes, child, fc, max_count);
 }
 

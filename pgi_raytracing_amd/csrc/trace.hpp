@@ -16,7 +16,10 @@ struct FrameCounters {
     int refract[kMaxLevels];       // refraction rays among count[L]
     int overflow;                  // set when an emit exceeded a queue capacity
     int pad[3];
-    unsigned long long trav[2];    // node visits, triangle tests (profile == 2)
+    int fetch[2 * kMaxLevels];     // work counters of the closest-hit launches (level, shadow)
+    // profile == 2: per closest-hit launch {sum node visits, sum triangle tests, max visits of
+    // one ray, max tests of one ray}; [0, kMaxLevels) level queues, [kMaxLevels, 2k) shadows
+    unsigned long long trav[2 * kMaxLevels][4];
 };
 
 struct FrameParams {
@@ -53,19 +56,22 @@ struct ShadowQueue {
     int cap;
 };
 
+// fetch: a zeroed device int per launch (persistent waves pull 64 rays per atomic)
 void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4* hits, const int* count_dev,
-                  int count_host, int max_count, int* gstack, int gstack_threads, unsigned long long* counters,
-                  bool count, hipStream_t stream);
+                  int count_host, int max_count, int* fetch, int* gstack, int gstack_threads,
+                  unsigned long long* counters, bool count, hipStream_t stream, int expect = 0);
 int trace_block_size();
 
+// `expect` sizes the grid of a grid-stride kernel (counts live on the device; any value is
+// correct, a good guess -- last frame's count -- avoids dispatching empty workgroups)
 void launch_raygen(const CameraView& cam, const FrameParams& fp, const int4* tiles, Queue q, int n0,
                    FrameCounters* fc, hipStream_t stream);
 void launch_shade(const SceneView& s, const FrameParams& fp, int level, Queue q, Queue next, LevelNodes nodes,
-                  ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream);
+                  ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect = 0);
 void launch_shadow_resolve(const SceneView& s, int level, LevelNodes nodes, ShadowQueue sq, const FrameCounters* fc,
-                           int max_count, hipStream_t stream);
+                           int max_count, hipStream_t stream, int expect = 0);
 void launch_combine(int level, LevelNodes nodes, LevelNodes child, const FrameCounters* fc, int max_count,
-                    hipStream_t stream);
+                    hipStream_t stream, int expect = 0);
 void launch_accumulate(const FrameParams& fp, const int4* tiles, LevelNodes l0, float4* accum, int npix,
                        bool first, hipStream_t stream);
 // out_mode 0: framebuffer (rect origin ox,oy, row pitch in pixels); 1: tile-compact

@@ -69,6 +69,7 @@ def lib():
         "pgrt_obj_material_name": (C.c_char_p, [vp, ip]),
         "pgrt_obj_surface_range": (ip, [vp, ip, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "pgrt_selftest_math": (ip, [vp, fp, ip, fp]),
+        "pgrt_frame_diag": (ip, [vp, C.POINTER(abi.LevelDiag), ip]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -162,6 +163,14 @@ class Context:
         hits = np.zeros((rays.shape[0], 4), np.float32)
         _check(self.h, self.L.pgrt_intersect_closest(self.h, abi.fptr(rays), rays.shape[0], abi.fptr(hits)))
         return hits
+
+    def frame_diag(self) -> list:
+        """Per-level counters of the last frame (traversal counts need params.profile == 2)."""
+        arr = (abi.LevelDiag * 16)()
+        n = self.L.pgrt_frame_diag(self.h, arr, 16)
+        if n < 0:
+            raise PgrtError(n, "pgrt_frame_diag")
+        return [{k: int(getattr(arr[i], k)) for k, _ in abi.LevelDiag._fields_} for i in range(n)]
 
     def selftest_math(self, pairs: np.ndarray) -> np.ndarray:
         pairs = np.ascontiguousarray(pairs, np.float32).reshape(-1, 2)

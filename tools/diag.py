@@ -1,0 +1,50 @@
+"""Per-level traversal diagnostics of one frame (GPU): rays, node visits and the worst ray.
+
+usage: python tools/diag.py [W H d S dof]"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import scenes  # noqa: E402
+from pgi_raytracing_amd import abi  # noqa: E402
+from pgi_raytracing_amd.raytracer import Context, load_obj  # noqa: E402
+
+
+def main():
+    a = [int(x) for x in sys.argv[1:]] + [1920, 1080, 5, 1, 0][len(sys.argv) - 1:]
+    W, H, d, S, dof = a[:5]
+    sc = load_obj(scenes.AVENGER_OBJ)
+    sc.set_environment(os.path.join(ROOT, "assets", "spherical_map_windows.jpg"))
+    ctx = Context(0)
+    t = time.time()
+    ctx.set_scene(sc)
+    info = ctx.bvh_info()
+    print(json.dumps({"bvh": {"tris": info.num_triangles, "nodes": info.num_nodes, "depth": info.max_depth,
+                              "build_ms": round(info.build_ms, 3), "set_scene_s": round(time.time() - t, 3)}}))
+    ctx.set_camera(abi.default_camera(W, H))
+    p = abi.make_params(spp_side=S, max_level=d, dof=dof,
+                        jitter=abi.PGRT_JITTER_HASH if S > 1 or dof else abi.PGRT_JITTER_NONE)
+    ctx.render(p)
+    p.profile = 1
+    _, st = ctx.render(p)
+    print(json.dumps({"stage_ms": {k: round(v, 4) for k, v in st.as_dict().items() if k.startswith("ms_")},
+                      "rays": st.rays(), "trace_launches": st.trace_launches}))
+    p.profile = 2
+    ctx.render(p)
+    for L, dd in enumerate(ctx.frame_diag()):
+        if dd["rays"] == 0 and dd["shadow_rays"] == 0:
+            continue
+        r = max(1, dd["rays"])
+        s = max(1, dd["shadow_rays"])
+        print(f"L{L}: rays {dd['rays']:9d} visits/ray {dd['visits'] / r:7.1f} max {dd['max_visits']:6d} "
+              f"tests/ray {dd['tests'] / r:6.1f} max {dd['max_tests']:5d} | shadow {dd['shadow_rays']:8d} "
+              f"visits/ray {dd['shadow_visits'] / s:6.1f} max {dd['shadow_max_visits']:5d}")
+
+
+if __name__ == "__main__":
+    main()
