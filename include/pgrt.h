@@ -141,6 +141,8 @@ typedef struct pgrt_bvh_info {
     double build_ms;
     float scene_lo[3], scene_hi[3];
     size_t device_bytes;
+    int builder;          /* 0 Karras LBVH, 1 PLOC over the Morton order (default) */
+    int build_iterations; /* PLOC merge iterations */
 } pgrt_bvh_info;
 
 /* ---- context ---- */

@@ -149,6 +149,8 @@ class BvhInfo(C.Structure):
         ("scene_lo", C.c_float * 3),
         ("scene_hi", C.c_float * 3),
         ("device_bytes", C.c_size_t),
+        ("builder", C.c_int),
+        ("build_iterations", C.c_int),
     ]
 
 

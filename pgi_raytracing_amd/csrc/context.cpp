@@ -273,6 +273,11 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
     DevBuf<unsigned char> sort_tmp;
     sort_tmp.alloc(tmp_bytes);
     BuildOut bo{};
+    static const int builder = [] {  // PGRT_BVH=lbvh selects the plain Karras LBVH
+        const char* e = getenv("PGRT_BVH");
+        return (e && std::string(e) == "lbvh") ? kBuilderLbvh : kBuilderPloc;
+    }();
+    bo.builder = builder;
     auto tb = std::chrono::steady_clock::now();
     build_lbvh(pos.p, n, ctx->tri.p, ctx->nodes.p, scratch.p, sort_tmp.p, tmp_bytes, pad, &bo, st);
     auto te = std::chrono::steady_clock::now();
@@ -297,6 +302,8 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
     bi.num_nodes = bo.num_nodes;
     bi.max_depth = bo.max_depth;
     bi.build_ms = std::chrono::duration<double, std::milli>(te - tb).count();
+    bi.builder = bo.builder;
+    bi.build_iterations = bo.iterations;
     for (int k = 0; k < 3; ++k) {
         bi.scene_lo[k] = lo[k];
         bi.scene_hi[k] = hi[k];

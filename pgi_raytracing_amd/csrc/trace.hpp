@@ -81,11 +81,17 @@ void launch_unpack_tiles(const float* gathered, float* rgba, int width, int heig
                          hipStream_t stream);
 
 // scene / BVH build
+constexpr int kBuilderLbvh = 0;  // Karras 2012 over 63-bit Morton codes
+constexpr int kBuilderPloc = 1;  // PLOC clustering over the same Morton order + SAH collapse
 struct BuildOut {
+    int builder;  // in: kBuilder*
     int root;
     int num_nodes;
     int max_depth;
+    int iterations;  // PLOC merge iterations
 };
+void build_ploc(const float* pos_dev, const int* order, int n, float4* tri_out, BvhNode* nodes_out, float pad,
+                BuildOut* out, int* iterations, hipStream_t stream);
 void build_lbvh(const float* pos_dev, int ntri, float4* tri_out, BvhNode* nodes_out, int* scratch_int,
                 void* sort_tmp, size_t sort_tmp_bytes, float pad, BuildOut* out, hipStream_t stream);
 size_t lbvh_sort_temp_bytes(int ntri);

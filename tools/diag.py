@@ -24,7 +24,8 @@ def main():
     t = time.time()
     ctx.set_scene(sc)
     info = ctx.bvh_info()
-    print(json.dumps({"bvh": {"tris": info.num_triangles, "nodes": info.num_nodes, "depth": info.max_depth,
+    print(json.dumps({"bvh": {"builder": ["lbvh", "ploc"][info.builder], "iters": info.build_iterations,
+                              "tris": info.num_triangles, "nodes": info.num_nodes, "depth": info.max_depth,
                               "build_ms": round(info.build_ms, 3), "set_scene_s": round(time.time() - t, 3)}}))
     ctx.set_camera(abi.default_camera(W, H))
     p = abi.make_params(spp_side=S, max_level=d, dof=dof,
