@@ -130,6 +130,11 @@ typedef struct pgrt_stats {
     uint64_t rays_primary, rays_shadow, rays_reflect, rays_refract;
     uint64_t node_visits, tri_tests; /* only with profile == 2 */
     double ms_total;                 /* host wall time of the call */
+    /* profile >= 1: ms_trace = every closest-hit launch (level queues + the shadow queue);
+     * ms_shadow = the shadow-queue launch alone (a part of ms_trace); ms_combine = the finish
+     * kernel (shadow resolve + bottom-up combine + sample accumulation + gamma); ms_resolve =
+     * 0 (the resolve is part of the finish kernel); ms_gather = host wall time of the RCCL
+     * gather + tile unpack (distributed calls) */
     double ms_raygen, ms_trace, ms_shade, ms_shadow, ms_combine, ms_resolve, ms_gather;
     int trace_launches;              /* launches of the closest-hit kernel in ms_trace */
     int levels;                      /* trace levels executed */

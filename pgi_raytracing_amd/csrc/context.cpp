@@ -70,7 +70,7 @@ struct StageTimer {
     }
 };
 
-enum { CAT_RAYGEN, CAT_TRACE, CAT_SHADE, CAT_SHADOW, CAT_COMBINE, CAT_RESOLVE, CAT_GATHER, CAT_N };
+enum { CAT_RAYGEN, CAT_TRACE, CAT_SHADE, CAT_SHADOW, CAT_COMBINE, CAT_N };
 
 }  // namespace
 
@@ -111,7 +111,7 @@ struct pgrt_ctx {
     StageTimer timer;
     std::vector<FrameCounters> last_fc;  // per batch, for pgrt_frame_diag
     int expect_count[kMaxLevels] = {0};   // grid hints from the previous frame (0 = unknown)
-    int expect_shadow[kMaxLevels] = {0};
+    int expect_shadow_total = 0;
 
     // multi-GPU
     ncclComm_t comm = nullptr;
@@ -410,7 +410,6 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
                 LevelNodes ln{ctx->n_color[L]->p, ctx->n_link[L]->p, ctx->n_att[L]->p};
                 // grid hints: last frame's per-level counts (+25 %); level 0 is exact
                 const int ex = L == 0 ? n0 : ctx->expect_count[L];
-                const int exs = ctx->expect_shadow[L];
                 id = ctx->timer.begin(s, CAT_TRACE);
                 launch_trace(ctx->view, qc.ro, qc.rd, qc.hit, &fcd->count[L], 0, maxc, &fcd->fetch[L],
                              ctx->gstack.p, kTraceGridThreads, fcd->trav[L], p->profile >= 2, s, ex);
@@ -419,28 +418,26 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
                 id = ctx->timer.begin(s, CAT_SHADE);
                 launch_shade(ctx->view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex);
                 ctx->timer.end(s, id);
-                if (ctx->view.nlight > 0 && L < p->max_level) {
-                    const int smax = std::min((long long)ctx->s_cap, (long long)maxc * ctx->view.nlight);
-                    id = ctx->timer.begin(s, CAT_TRACE);
-                    launch_trace(ctx->view, sq.ro, sq.rd, sq.hit, &fcd->shadow_count[L], 0, (int)smax,
-                                 &fcd->fetch[kMaxLevels + L], ctx->gstack.p, kTraceGridThreads,
-                                 fcd->trav[kMaxLevels + L], p->profile >= 2, s, exs);
-                    ctx->timer.end(s, id);
-                    ++trace_launches;
-                    id = ctx->timer.begin(s, CAT_SHADOW);
-                    launch_shadow_resolve(ctx->view, L, ln, sq, fcd, maxc, s, ex);
-                    ctx->timer.end(s, id);
-                }
+            }
+            if (ctx->view.nlight > 0 && p->max_level > 0) {  // every level's shadow rays, one launch
+                id = ctx->timer.begin(s, CAT_TRACE);
+                const int sid = ctx->timer.begin(s, CAT_SHADOW);
+                launch_trace(ctx->view, sq.ro, sq.rd, sq.hit, &fcd->shadow_count[0], 0, sq.cap,
+                             &fcd->fetch[kMaxLevels], ctx->gstack.p, kTraceGridThreads, fcd->trav[kMaxLevels],
+                             p->profile >= 2, s, ctx->expect_shadow_total, levels);
+                ctx->timer.end(s, sid);
+                ctx->timer.end(s, id);
+                ++trace_launches;
             }
             id = ctx->timer.begin(s, CAT_COMBINE);
-            for (int L = levels - 2; L >= 0; --L) {
+            for (int L = p->max_level - 1; L >= 1; --L) {
                 LevelNodes ln{ctx->n_color[L]->p, ctx->n_link[L]->p, ctx->n_att[L]->p};
-                LevelNodes lc{ctx->n_color[L + 1]->p, ctx->n_link[L + 1]->p, ctx->n_att[L + 1]->p};
-                launch_combine(L, ln, lc, fcd, L == 0 ? n0 : std::min(ctx->q_cap, ctx->level_cap[L]), s,
-                               L == 0 ? n0 : ctx->expect_count[L]);
+                launch_combine(ctx->view, L, ln, ctx->n_color[L + 1]->p, sq, fcd,
+                               std::min(ctx->q_cap, ctx->level_cap[L]), s, ctx->expect_count[L]);
             }
             LevelNodes l0{ctx->n_color[0]->p, ctx->n_link[0]->p, ctx->n_att[0]->p};
-            launch_accumulate(fp, ctx->tiles.p, l0, ctx->accum.p, (int)npix, s0 == 0, s);
+            launch_finish(ctx->view, fp, ctx->tiles.p, l0, levels > 1 ? ctx->n_color[1]->p : ctx->n_color[0]->p, sq,
+                          ctx->accum.p, out, out_mode, ox, oy, pitch, (int)npix, s0 == 0, s0 + fp.nsb >= spp, s);
             ctx->timer.end(s, id);
             FrameCounters hfc;
             PGRT_HIP(hipMemcpyAsync(&hfc, fcd, sizeof(FrameCounters), hipMemcpyDeviceToHost, s));
@@ -452,15 +449,18 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
         bool overflow = false;
         for (auto& h : host_fc) overflow |= h.overflow != 0;
         ctx->last_fc = host_fc;
-        for (int L = 0; L < kMaxLevels; ++L) {  // grid hints for the next frame
-            int c = 0, sc = 0;
-            for (auto& h : host_fc) {
-                c = std::max(c, h.count[L]);
-                sc = std::max(sc, h.shadow_count[L]);
-            }
-            ctx->expect_count[L] = c + c / 4 + 1024;
-            ctx->expect_shadow[L] = sc + sc / 4 + 1024;
+        int shadow_need = 0;  // largest batch-wide shadow queue requested
+        for (auto& h : host_fc) {
+            int sc = 0;
+            for (int L = 0; L < kMaxLevels; ++L) sc += h.shadow_count[L];
+            shadow_need = std::max(shadow_need, sc);
         }
+        for (int L = 0; L < kMaxLevels; ++L) {  // grid hints for the next frame
+            int c = 0;
+            for (auto& h : host_fc) c = std::max(c, h.count[L]);
+            ctx->expect_count[L] = c + c / 4 + 1024;
+        }
+        ctx->expect_shadow_total = shadow_need + shadow_need / 4 + 1024;
         if (overflow) {
             // grow every level queue to what was requested (2x margin) and redo the frame
             for (auto& h : host_fc)
@@ -482,16 +482,15 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
                             ctx->n_att[L2]->alloc(ctx->level_cap[L2]);
                             ctx->n_link[L2]->alloc(ctx->level_cap[L2]);
                         }
-                    int sh = 0;
-                    for (int L2 = 0; L2 < levels; ++L2) sh = std::max(sh, h.shadow_count[L2] * 2);
-                    if (sh > ctx->s_cap) {
-                        ctx->s_ro.alloc(sh);
-                        ctx->s_rd.alloc(sh);
-                        ctx->s_hit.alloc(sh);
-                        ctx->s_contrib.alloc(sh);
-                        ctx->s_cap = sh;
-                    }
                 }
+            if (shadow_need * 2 > ctx->s_cap) {
+                const int sh = shadow_need * 2;
+                ctx->s_ro.alloc(sh);
+                ctx->s_rd.alloc(sh);
+                ctx->s_hit.alloc(sh);
+                ctx->s_contrib.alloc(sh);
+                ctx->s_cap = sh;
+            }
             ctx->timer.collect(ms);
             std::fill(ms, ms + CAT_N, 0.0);
             ++retries;
@@ -514,9 +513,6 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
         }
         break;
     }
-    int id = ctx->timer.begin(s, CAT_RESOLVE);
-    launch_resolve(fp, ctx->tiles.p, ctx->accum.p, out, out_mode, ox, oy, pitch, (int)npix, s);
-    ctx->timer.end(s, id);
     PGRT_HIP(hipGetLastError());
     if (st) {
         PGRT_HIP(hipStreamSynchronize(s));
@@ -534,7 +530,6 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
         st->ms_shade = ms[CAT_SHADE];
         st->ms_shadow = ms[CAT_SHADOW];
         st->ms_combine = ms[CAT_COMBINE];
-        st->ms_resolve = ms[CAT_RESOLVE];
         st->trace_launches = trace_launches;
         st->levels = levels;
         st->overflow_retries = retries;

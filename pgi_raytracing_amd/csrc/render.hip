@@ -6,9 +6,10 @@
 // The recursion of trace() becomes one ray queue per level: level L+1 holds the reflection /
 // refraction children of the dielectric hits of level L, appended with one atomic per wave
 // (__ballot-free prefix by __shfl_up, the wave's total claimed by its last lane).  Shadow rays
-// of each level live in one queue traced by the same closest-hit kernel.  Because mix_srgb is
-// non-linear (it clamps and sRGB-encodes before the attenuation multiply, :318-321), colours
-// are combined bottom-up per level once every level is traced.
+// of every level go to one batch-wide queue, traced once after the last level by the same
+// closest-hit kernel.  Because mix_srgb is non-linear (it clamps and sRGB-encodes before the
+// attenuation multiply, :318-321), colours are combined bottom-up, one level per launch,
+// once every level is traced.
 #include "shade_ops.hpp"
 #include "trace.hpp"
 
@@ -125,6 +126,9 @@ __global__ __launch_bounds__(kBlock) void k_shade(SceneView s, FrameParams fp, i
                                                   LevelNodes nodes, ShadowQueue sq, FrameCounters* fc) {
     const int n = min(fc->count[level], q.cap);
     const int tid = threadIdx.x;
+    // one shadow queue for the whole batch: level L's rays follow those of levels < L (final by now)
+    int sq_base = 0;
+    for (int l = 0; l < level; ++l) sq_base += fc->shadow_count[l];
     for (int base_i = blockIdx.x * kBlock; base_i < n; base_i += gridDim.x * kBlock) {
         const int i = base_i + tid;
         const bool active = i < n;
@@ -222,7 +226,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(SceneView s, FrameParams fp, i
         }
         // ---- queue allocation (wave-uniform control flow) ----
         const int cbase = wave_alloc(&fc->count[level + 1 < kMaxLevels ? level + 1 : level], nchild);
-        const int sbase = wave_alloc(&fc->shadow_count[level], nshadow);
+        const int sbase = sq_base + wave_alloc(&fc->shadow_count[level], nshadow);
         const int nref = wave_alloc(&fc->refract[level + 1 < kMaxLevels ? level + 1 : level], nchild == 2 ? 1 : 0);
         (void)nref;
         if (!active) continue;
@@ -279,7 +283,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(SceneView s, FrameParams fp, i
             }
         }
         nodes.link[i] = link;
-        nodes.color[i] = color;
+        if (link.x < 0 && link.z < 0) nodes.color[i] = color;  // else derived by k_finish
     }
 }
 
@@ -290,105 +294,90 @@ void launch_shade(const SceneView& s, const FrameParams& fp, int level, Queue q,
     hipLaunchKernelGGL(k_shade, dim3(grid), dim3(kBlock), 0, stream, s, fp, level, q, next, nodes, sq, fc);
 }
 
-// ------------------------------------------------------------------ shadow resolve
+// ------------------------------------------------------------------ combine + finish
+//
+// Colours are settled bottom-up.  k_combine(L), for L = max_level-1 .. 1, gives every level-L
+// node its final colour: an opaque node is the sum of its lit Phong terms (the shadow resolve,
+// raytracer.cpp:344-386 with is_illuminated :150-175), a dielectric node mixes its children of
+// level L+1 (raytracer.cpp:316-321), any other node already carries its colour.  k_finish does
+// the same for level 0 and then sums each pixel's samples in order (raytracer.cpp:422-429); the
+// last batch applies the gamma (:431-435) and writes the framebuffer, earlier batches keep the
+// running sum in `accum`.
 
-__global__ __launch_bounds__(kBlock) void k_shadow_resolve(SceneView s, int level, LevelNodes nodes, ShadowQueue sq,
-                                                           const FrameCounters* fc, int cap) {
-    const int n = min(fc->count[level], cap);
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        const int4 link = nodes.link[i];
-        if (link.z < 0) continue;
-        float blue = 0, green = 0, red = 0;
-        for (int j = 0; j < link.w; ++j) {
-            const int k = link.z + j;
-            const int prim = __float_as_int(sq.hit[k].w);
-            bool lit = true;  // is_illuminated (raytracer.cpp:163-173): closest hit decides
-            if (prim >= 0) {
-                const int mid = __float_as_int(s.attr[16 * (size_t)prim + 15]);
-                lit = s.mats[mid].type == PGRT_MATERIAL_DIELECTRIC;
-            }
-            if (lit) {
-                const float4 c = sq.contrib[k];
-                blue += c.x;
-                green += c.y;
-                red += c.z;
-            }
+__device__ __forceinline__ float4 opaque_color(const SceneView& s, const ShadowQueue& sq, int base, int cnt) {
+    float blue = 0, green = 0, red = 0;
+    for (int j = 0; j < cnt; ++j) {
+        const int k = base + j;
+        const int prim = __float_as_int(sq.hit[k].w);
+        bool lit = true;  // is_illuminated (raytracer.cpp:163-173): closest hit decides
+        if (prim >= 0) {
+            const int mid = __float_as_int(s.attr[16 * (size_t)prim + 15]);
+            lit = s.mats[mid].type == PGRT_MATERIAL_DIELECTRIC;
         }
-        nodes.color[i] = make_float4(blue, green, red, 1.0f);
+        if (lit) {
+            const float4 c = sq.contrib[k];
+            blue += c.x;
+            green += c.y;
+            red += c.z;
+        }
     }
+    return make_float4(blue, green, red, 1.0f);
 }
 
-void launch_shadow_resolve(const SceneView& s, int level, LevelNodes nodes, ShadowQueue sq, const FrameCounters* fc,
-                           int max_count, hipStream_t stream, int expect) {
-    if (max_count <= 0) return;
-    const int grid = grid_for(max_count, expect);
-    hipLaunchKernelGGL(k_shadow_resolve, dim3(grid), dim3(kBlock), 0, stream, s, level, nodes, sq, fc, max_count);
+// final colour of node i of a level whose children (next level) are final
+__device__ __forceinline__ float4 node_color(const SceneView& s, const ShadowQueue& sq, LevelNodes nodes,
+                                             const float4* __restrict__ child, int i) {
+    const int4 lk = nodes.link[i];
+    if (lk.x >= 0) {
+        const float4 att = nodes.att[i];
+        const float4 refl = child[lk.x];
+        // raytracer.cpp:318-319 (refraction present) or :321 (total internal reflection)
+        const float4 c = lk.y >= 0 ? mix_srgb(refl, child[lk.y], att.w) : refl;
+        return make_float4(c.x * att.x, c.y * att.y, c.z * att.z, 1);
+    }
+    if (lk.z >= 0) return opaque_color(s, sq, lk.z, lk.w);
+    return nodes.color[i];
 }
 
-// ------------------------------------------------------------------ combine (dielectric nodes)
-
-__global__ __launch_bounds__(kBlock) void k_combine(int level, LevelNodes nodes, LevelNodes child,
+__global__ __launch_bounds__(kBlock) void k_combine(SceneView s, int level, LevelNodes nodes,
+                                                    const float4* __restrict__ child, ShadowQueue sq,
                                                     const FrameCounters* fc, int cap) {
     const int n = min(fc->count[level], cap);
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        const int4 link = nodes.link[i];
-        if (link.x < 0) continue;
-        const float4 att = nodes.att[i];
-        const float4 refl = child.color[link.x];
-        float4 out;
-        if (link.y >= 0) {  // raytracer.cpp:318-319
-            const float4 refr = child.color[link.y];
-            const float4 c = mix_srgb(refl, refr, att.w);
-            out = make_float4(c.x * att.x, c.y * att.y, c.z * att.z, 1);
-        } else {  // total internal reflection (raytracer.cpp:321)
-            out = make_float4(refl.x * att.x, refl.y * att.y, refl.z * att.z, 1);
-        }
-        nodes.color[i] = out;
+        const int4 lk = nodes.link[i];
+        if (lk.x < 0 && lk.z < 0) continue;  // colour written by k_shade
+        nodes.color[i] = node_color(s, sq, nodes, child, i);
     }
 }
 
-void launch_combine(int level, LevelNodes nodes, LevelNodes child, const FrameCounters* fc, int max_count,
-                    hipStream_t stream, int expect) {
+void launch_combine(const SceneView& s, int level, LevelNodes nodes, const float4* child, ShadowQueue sq,
+                    const FrameCounters* fc, int max_count, hipStream_t stream, int expect) {
     if (max_count <= 0) return;
     const int grid = grid_for(max_count, expect);
-    hipLaunchKernelGGL(k_combine, dim3(grid), dim3(kBlock), 0, stream, level, nodes, child, fc, max_count);
+    hipLaunchKernelGGL(k_combine, dim3(grid), dim3(kBlock), 0, stream, s, level, nodes, child, sq, fc, max_count);
 }
 
-// ------------------------------------------------------------------ accumulate + resolve
-
-__global__ __launch_bounds__(kBlock) void k_accumulate(FrameParams fp, LevelNodes l0, float4* __restrict__ accum,
-                                                       int npix, int first) {
+__global__ __launch_bounds__(kBlock) void k_finish(SceneView s, FrameParams fp, const int4* __restrict__ tiles,
+                                                   LevelNodes l0, const float4* __restrict__ child, ShadowQueue sq,
+                                                   float4* __restrict__ accum, float* __restrict__ out, int out_mode,
+                                                   int ox, int oy, int pitch, int npix, int first, int last) {
     const int p = blockIdx.x * kBlock + threadIdx.x;
     if (p >= npix) return;
     float4 acc = first ? make_float4(0.0f, 0.0f, 0.0f, 1.0f) : accum[p];
-    const float4* c = l0.color + (size_t)p * fp.nsb;
     for (int k = 0; k < fp.nsb; ++k) {  // final_color += result_colors[x][y] (raytracer.cpp:422-429)
-        const float4 v = c[k];
+        const float4 v = node_color(s, sq, l0, child, p * fp.nsb + k);
         acc.x += v.x;
         acc.y += v.y;
         acc.z += v.z;
     }
-    accum[p] = acc;
-}
-
-void launch_accumulate(const FrameParams& fp, const int4* tiles, LevelNodes l0, float4* accum, int npix, bool first,
-                       hipStream_t stream) {
-    (void)tiles;
-    if (npix <= 0) return;
-    hipLaunchKernelGGL(k_accumulate, dim3(ceil_div(npix, kBlock)), dim3(kBlock), 0, stream, fp, l0, accum, npix,
-                       first ? 1 : 0);
-}
-
-__global__ __launch_bounds__(kBlock) void k_resolve(FrameParams fp, const int4* __restrict__ tiles,
-                                                    const float4* __restrict__ accum, float* __restrict__ out,
-                                                    int out_mode, int ox, int oy, int pitch, int npix) {
-    const int p = blockIdx.x * kBlock + threadIdx.x;
-    if (p >= npix) return;
+    if (!last) {
+        accum[p] = acc;
+        return;
+    }
     int px, py;
     bool valid;
     tile_pixel(p, tiles, px, py, valid);
     if (!valid) return;
-    const float4 acc = accum[p];
     const int area = fp.spp_side * fp.spp_side;
     // gamma(Color4f{final.b/area, final.g/area, final.r/area}) (raytracer.cpp:431-435)
     const float4 o = gamma_rgba(acc.z / (float)area, acc.y / (float)area, acc.x / (float)area, fp.gamma);
@@ -403,11 +392,12 @@ __global__ __launch_bounds__(kBlock) void k_resolve(FrameParams fp, const int4* 
     *reinterpret_cast<float4*>(dst) = o;
 }
 
-void launch_resolve(const FrameParams& fp, const int4* tiles, const float4* accum, float* out, int out_mode, int ox,
-                    int oy, int pitch, int npix, hipStream_t stream) {
+void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles, LevelNodes l0, const float4* child,
+                   ShadowQueue sq, float4* accum, float* out, int out_mode, int ox, int oy, int pitch, int npix,
+                   bool first, bool last, hipStream_t stream) {
     if (npix <= 0) return;
-    hipLaunchKernelGGL(k_resolve, dim3(ceil_div(npix, kBlock)), dim3(kBlock), 0, stream, fp, tiles, accum, out,
-                       out_mode, ox, oy, pitch, npix);
+    hipLaunchKernelGGL(k_finish, dim3(ceil_div(npix, kBlock)), dim3(kBlock), 0, stream, s, fp, tiles, l0, child, sq,
+                       accum, out, out_mode, ox, oy, pitch, npix, first ? 1 : 0, last ? 1 : 0);
 }
 
 // ------------------------------------------------------------------ multi-GPU unpack

@@ -44,13 +44,19 @@ template <bool COUNT, bool PERSIST, bool WW>
 __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4* __restrict__ ro,
                                                        const float4* __restrict__ rd,
                                                        float4* __restrict__ hits,
-                                                       const int* __restrict__ count_dev, int count_host, int cap,
-                                                       int* __restrict__ fetch, int* __restrict__ gstack,
+                                                       const int* __restrict__ count_dev, int count_terms,
+                                                       int count_host, int cap, int* __restrict__ fetch,
+                                                       int* __restrict__ gstack,
                                                        unsigned long long* __restrict__ counters) {
     __shared__ int lstack[kLdsStack * kTraceBlock];
     const int tid = threadIdx.x;
     const int lane = __lane_id();
-    const int n = count_dev ? min(*count_dev, cap) : count_host;
+    int n = count_host;
+    if (count_dev) {
+        n = 0;
+        for (int k = 0; k < count_terms; ++k) n += count_dev[k];
+        n = min(n, cap);
+    }
     int* gst = gstack + (size_t)(blockIdx.x * kTraceBlock + tid) * kGlobalStack;
     unsigned long long nvis = 0, ntest = 0, mvis = 0, mtest = 0;
 #define PUSH(v)                                                  \
@@ -188,7 +194,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
 
 void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4* hits, const int* count_dev,
                   int count_host, int max_count, int* fetch, int* gstack, int gstack_threads,
-                  unsigned long long* counters, bool count, hipStream_t stream, int expect) {
+                  unsigned long long* counters, bool count, hipStream_t stream, int expect, int count_terms) {
     if (max_count <= 0) return;
     // schedule A/B switch (PGRT_TRACE_VARIANT = bit0 persistent fetch | bit1 while-while).
     // Measured on the C2 frame (r1, profiles/r1/trace_variants.txt): 2 = grid-stride +
@@ -205,7 +211,7 @@ void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4
     if (grid > gstack_threads / kTraceBlock) grid = gstack_threads / kTraceBlock;
 #define PGRT_LAUNCH(C, P, W)                                                                               \
     hipLaunchKernelGGL((k_trace<C, P, W>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits, count_dev, \
-                       count_host, max_count, fetch, gstack, counters)
+                       count_terms, count_host, max_count, fetch, gstack, counters)
     if (count) {
         if (persist) { if (ww) PGRT_LAUNCH(true, true, true); else PGRT_LAUNCH(true, true, false); }
         else { if (ww) PGRT_LAUNCH(true, false, true); else PGRT_LAUNCH(true, false, false); }

@@ -48,7 +48,7 @@ struct LevelNodes {  // per-level node records kept until the combine pass
     float4* att;     // dielectric: (att.r, att.g, att.b, R)
 };
 
-struct ShadowQueue {
+struct ShadowQueue {  // one per batch: the shadow rays of every level, level-major
     float4* ro;
     float4* rd;
     float4* hit;
@@ -56,10 +56,12 @@ struct ShadowQueue {
     int cap;
 };
 
-// fetch: a zeroed device int per launch (persistent waves pull 64 rays per atomic)
+// fetch: a zeroed device int per launch (persistent waves pull 64 rays per atomic).
+// Ray count: sum of count_dev[0 .. count_terms) when count_dev is set, else count_host.
 void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4* hits, const int* count_dev,
                   int count_host, int max_count, int* fetch, int* gstack, int gstack_threads,
-                  unsigned long long* counters, bool count, hipStream_t stream, int expect = 0);
+                  unsigned long long* counters, bool count, hipStream_t stream, int expect = 0,
+                  int count_terms = 1);
 int trace_block_size();
 
 // `expect` sizes the grid of a grid-stride kernel (counts live on the device; any value is
@@ -68,15 +70,14 @@ void launch_raygen(const CameraView& cam, const FrameParams& fp, const int4* til
                    FrameCounters* fc, hipStream_t stream);
 void launch_shade(const SceneView& s, const FrameParams& fp, int level, Queue q, Queue next, LevelNodes nodes,
                   ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect = 0);
-void launch_shadow_resolve(const SceneView& s, int level, LevelNodes nodes, ShadowQueue sq, const FrameCounters* fc,
-                           int max_count, hipStream_t stream, int expect = 0);
-void launch_combine(int level, LevelNodes nodes, LevelNodes child, const FrameCounters* fc, int max_count,
-                    hipStream_t stream, int expect = 0);
-void launch_accumulate(const FrameParams& fp, const int4* tiles, LevelNodes l0, float4* accum, int npix,
-                       bool first, hipStream_t stream);
+// level L's final colours from its shadow hits and level L+1's colours (child)
+void launch_combine(const SceneView& s, int level, LevelNodes nodes, const float4* child, ShadowQueue sq,
+                    const FrameCounters* fc, int max_count, hipStream_t stream, int expect = 0);
+// level-0 combine + sample accumulation (+ gamma and framebuffer write on the last batch).
 // out_mode 0: framebuffer (rect origin ox,oy, row pitch in pixels); 1: tile-compact
-void launch_resolve(const FrameParams& fp, const int4* tiles, const float4* accum, float* out, int out_mode,
-                    int ox, int oy, int pitch, int npix, hipStream_t stream);
+void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles, LevelNodes l0, const float4* child,
+                   ShadowQueue sq, float4* accum, float* out, int out_mode, int ox, int oy, int pitch, int npix,
+                   bool first, bool last, hipStream_t stream);
 void launch_unpack_tiles(const float* gathered, float* rgba, int width, int height, int world, int tiles_per_rank,
                          hipStream_t stream);
 

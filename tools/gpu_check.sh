@@ -28,6 +28,7 @@ for s in "$@"; do
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
         bench_quick) step bench_quick 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+        diag) step diag 300 python tools/diag.py ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done
