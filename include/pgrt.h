@@ -148,6 +148,7 @@ typedef struct pgrt_bvh_info {
     size_t device_bytes;
     int builder;          /* 0 Karras LBVH, 1 PLOC over the Morton order (default) */
     int build_iterations; /* PLOC merge iterations */
+    int width;            /* traversal layout: 2 (binary, default) or 8 (quantized 8-wide) */
 } pgrt_bvh_info;
 
 /* ---- context ---- */

@@ -151,6 +151,7 @@ class BvhInfo(C.Structure):
         ("device_bytes", C.c_size_t),
         ("builder", C.c_int),
         ("build_iterations", C.c_int),
+        ("width", C.c_int),
     ]
 
 

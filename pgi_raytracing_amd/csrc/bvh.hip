@@ -95,7 +95,7 @@ __device__ __forceinline__ int delta(const unsigned long long* __restrict__ k, i
 
 // kids[2*i], kids[2*i+1]: children in combined index space (internal 0..n-2, leaf n-1+k)
 __global__ __launch_bounds__(kB) void k_karras(const unsigned long long* __restrict__ k, int n, BvhNode* nodes,
-                                               int* __restrict__ parent, int* __restrict__ kids) {
+                                               int* __restrict__ parent, int* __restrict__ kids, int leaf_max) {
     const int i = blockIdx.x * kB + threadIdx.x;
     if (i >= n - 1) return;
     const int d = (delta(k, n, i, i + 1) - delta(k, n, i, i - 1)) >= 0 ? 1 : -1;
@@ -123,8 +123,8 @@ __global__ __launch_bounds__(kB) void k_karras(const unsigned long long* __restr
     parent[right] = i;
     const int cl = g - first + 1, cr = last - g;
     int4 dd;
-    dd.x = cl <= kLeafMaxTris ? leaf_encode(first, cl) : g;
-    dd.y = cr <= kLeafMaxTris ? leaf_encode(g + 1, cr) : g + 1;
+    dd.x = cl <= leaf_max ? leaf_encode(first, cl) : g;
+    dd.y = cr <= leaf_max ? leaf_encode(g + 1, cr) : g + 1;
     dd.z = first;
     dd.w = last;
     nodes[i].d = dd;
@@ -242,7 +242,8 @@ void build_lbvh(const float* pos, int n, float4* tri, BvhNode* nodes, int* scrat
     }
     hipLaunchKernelGGL(k_gather_tris, dim3(grid), dim3(kB), 0, stream, pos, vals_b, n, tri);
     if (n >= 2) {
-        hipLaunchKernelGGL(k_karras, dim3(ceil_div(n - 1, kB)), dim3(kB), 0, stream, keys_b, n, nodes, parent, kids);
+        hipLaunchKernelGGL(k_karras, dim3(ceil_div(n - 1, kB)), dim3(kB), 0, stream, keys_b, n, nodes, parent, kids,
+                           out->leaf_max);
         hipLaunchKernelGGL(k_refit, dim3(grid), dim3(kB), 0, stream, pos, vals_b, n, pad, nodes, parent, kids, flags);
         hipLaunchKernelGGL(k_depth, dim3(grid), dim3(kB), 0, stream, n, parent, depth);
     }

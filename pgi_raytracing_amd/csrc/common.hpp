@@ -98,10 +98,27 @@ __host__ __device__ inline int leaf_encode(int first, int count) {
 __host__ __device__ inline int leaf_first(int c) { return (int)((unsigned)c & 0x07ffffffu); }
 __host__ __device__ inline int leaf_count(int c) { return (int)(((unsigned)c >> 27) & 0xfu) + 1; }
 
+// 8-wide BVH node, 80 B (five 16-B loads): 8 child boxes quantized to 8 bits per plane
+// relative to origin p with per-axis scale 2^e (conservative: floor / ceil).
+//   p  = (origin.xyz, bits: e.x+127 | e.y+127 << 8 | e.z+127 << 16 | imask << 24)
+//   m  = (child_base, tri_base, meta[0..3], meta[4..7])
+//   qx = (lo.x[0..3], lo.x[4..7], hi.x[0..3], hi.x[4..7]) bytes, likewise qy, qz
+// imask bit s: slot s is an internal node, stored at child_base + popc(imask below s).
+// meta[s] of a leaf: unary triangle count << 5 | offset from tri_base (count <= 3, <= 24
+// triangles per node); 0 = empty slot.
+struct Bvh8Node {
+    float4 p;
+    uint4 m;
+    uint4 qx, qy, qz;
+};
+constexpr int kWideLeafMaxTris = 3;
+
 struct SceneView {  // kernel-argument view of the device scene
     const float4* tri;     // 3 x float4 per sorted triangle: (v0, orig id bits) (e1) (e2)
     const BvhNode* nodes;
     int root;              // node index, or a leaf code for tiny scenes
+    const Bvh8Node* nodes8;  // 8-wide BVH (root = node 0) when wide != 0; tri is then in its order
+    int wide;
     int ntri;
     const float* attr;     // 16 floats per ORIGINAL triangle: n0 n1 n2 uv0 uv1 uv2, mat (bits)
     const DevMaterial* mats;

@@ -82,6 +82,7 @@ struct pgrt_ctx {
     // scene
     DevBuf<float4> tri;
     DevBuf<BvhNode> nodes;
+    DevBuf<Bvh8Node> nodes8;
     DevBuf<float> attr;
     DevBuf<DevMaterial> mats;
     DevBuf<DevTexture> texd;
@@ -273,21 +274,41 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
     DevBuf<unsigned char> sort_tmp;
     sort_tmp.alloc(tmp_bytes);
     BuildOut bo{};
-    static const int builder = [] {  // PGRT_BVH=lbvh selects the plain Karras LBVH
-        const char* e = getenv("PGRT_BVH");
-        return (e && std::string(e) == "lbvh") ? kBuilderLbvh : kBuilderPloc;
-    }();
+    // layout knobs, read per set_scene so one process can compare them (tests, tools/ab_bvh.sh):
+    // PGRT_BVH=lbvh selects the plain Karras LBVH (default PLOC); PGRT_BVH_WIDTH=8 the
+    // quantized 8-wide traversal layout (default binary, faster on the avenger proxy)
+    const char* eb = getenv("PGRT_BVH");
+    const int builder = (eb && std::string(eb) == "lbvh") ? kBuilderLbvh : kBuilderPloc;
+    const char* ew = getenv("PGRT_BVH_WIDTH");
+    const int width = (ew && std::string(ew) == "8") ? 8 : 2;
     bo.builder = builder;
+    bo.leaf_max = width == 8 ? kWideLeafMaxTris : kLeafMaxTris;
     auto tb = std::chrono::steady_clock::now();
     build_lbvh(pos.p, n, ctx->tri.p, ctx->nodes.p, scratch.p, sort_tmp.p, tmp_bytes, pad, &bo, st);
+    int wide_nodes = 0, wide_depth = 0;
+    if (width == 8) {
+        ctx->nodes8.alloc((size_t)std::max(1, n));
+        DevBuf<float4> tri8;
+        tri8.alloc((size_t)n * 3);
+        const float4 rlo = make_float4(lo[0] - pad, lo[1] - pad, lo[2] - pad, 0.0f);
+        const float4 rhi = make_float4(hi[0] + pad, hi[1] + pad, hi[2] + pad, 0.0f);
+        build_bvh8(ctx->nodes.p, ctx->tri.p, bo.root, n, rlo, rhi, ctx->nodes8.p, tri8.p, &wide_nodes, &wide_depth,
+                   st);
+        std::swap(ctx->tri.p, tri8.p);  // traversal reads the triangles in wide-leaf order
+        std::swap(ctx->tri.n, tri8.n);
+    } else {
+        ctx->nodes8.release();
+    }
     auto te = std::chrono::steady_clock::now();
-    PGRT_REQUIRE(bo.max_depth <= 32 + kGlobalStack - 2, PGRT_ERR_INVALID_ARGUMENT,
+    PGRT_REQUIRE(bo.max_depth <= kLdsStack + kGlobalStack - 2, PGRT_ERR_INVALID_ARGUMENT,
                  "BVH depth " + std::to_string(bo.max_depth) + " exceeds the traversal stack");
 
     SceneView& v = ctx->view;
     v.tri = ctx->tri.p;
     v.nodes = ctx->nodes.p;
     v.root = bo.root;
+    v.nodes8 = width == 8 ? ctx->nodes8.p : nullptr;
+    v.wide = width == 8 ? 1 : 0;
     v.ntri = n;
     v.attr = ctx->attr.p;
     v.mats = ctx->mats.p;
@@ -299,8 +320,9 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
     ctx->has_scene = true;
     pgrt_bvh_info& bi = ctx->info;
     bi.num_triangles = n;
-    bi.num_nodes = bo.num_nodes;
-    bi.max_depth = bo.max_depth;
+    bi.num_nodes = width == 8 ? wide_nodes : bo.num_nodes;
+    bi.max_depth = width == 8 ? wide_depth : bo.max_depth;
+    bi.width = width;
     bi.build_ms = std::chrono::duration<double, std::milli>(te - tb).count();
     bi.builder = bo.builder;
     bi.build_iterations = bo.iterations;
@@ -308,7 +330,8 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
         bi.scene_lo[k] = lo[k];
         bi.scene_hi[k] = hi[k];
     }
-    bi.device_bytes = ctx->tri.bytes() + ctx->nodes.bytes() + ctx->attr.bytes() + ctx->texels.bytes();
+    bi.device_bytes = ctx->tri.bytes() + (width == 8 ? ctx->nodes8.bytes() : ctx->nodes.bytes()) +
+                      ctx->attr.bytes() + ctx->texels.bytes();
     (void)t0;
 }
 

@@ -12,7 +12,8 @@
 // flags, one 64-bit exclusive scan (merges << 32 | survivors), compaction that also writes the
 // new internal nodes.  Then: bottom-up counts + SAH cost with per-node arrival counters
 // (agent-scope release/acquire as in the LBVH refit), leaf ranges by walking to the root,
-// and the 64-byte BvhNode layout with leaves of <= kLeafMaxTris contiguous triangles.
+// and the 64-byte BvhNode layout with leaves of <= leaf_max (<= kLeafMaxTris) contiguous
+// triangles.
 #include <hipcub/hipcub.hpp>
 
 #include "trace.hpp"
@@ -138,7 +139,7 @@ __global__ __launch_bounds__(kB) void k_ploc_compact(int m, const int* __restric
 __global__ __launch_bounds__(kB) void k_ploc_cost(int n, const float4* __restrict__ nlo,
                                                   const float4* __restrict__ nhi, const int2* __restrict__ kids,
                                                   const int* __restrict__ parent, int* count, float* cost,
-                                                  int* collapse, int* flags) {
+                                                  int* collapse, int* flags, int leaf_max) {
     const int i = blockIdx.x * kB + threadIdx.x;
     if (i >= n) return;
     count[i] = 1;
@@ -156,7 +157,7 @@ __global__ __launch_bounds__(kB) void k_ploc_cost(int n, const float4* __restric
         const float a = half_area(nlo[par], nhi[par]);
         const float node_cost = kCostNode * a + cost[k.x] + cost[k.y];
         const float leaf_cost = kCostTri * a * (float)c;
-        const bool leaf = c <= kLeafMaxTris && leaf_cost <= node_cost;
+        const bool leaf = c <= leaf_max && leaf_cost <= node_cost;
         count[par] = c;
         cost[par] = leaf ? leaf_cost : node_cost;
         collapse[par] = leaf ? 1 : 0;
@@ -280,7 +281,7 @@ void build_ploc(const float* pos, const int* order, int n, float4* tri, BvhNode*
     PGRT_HIP(hipMemsetAsync(flags.p, 0, sizeof(int) * total, stream));
     PGRT_HIP(hipMemsetAsync(misc.p, 0, sizeof(int) * 4, stream));
     hipLaunchKernelGGL(k_ploc_cost, dim3(grid), dim3(kB), 0, stream, n, nlo.p, nhi.p, kids.p, parent.p, count.p,
-                       cost.p, collapse.p, flags.p);
+                       cost.p, collapse.p, flags.p, out->leaf_max);
     hipLaunchKernelGGL(k_ploc_offsets, dim3(ceil_div(total, kB)), dim3(kB), 0, stream, total, kids.p, parent.p,
                        count.p, offset.p, misc.p);
     if (n >= 2)

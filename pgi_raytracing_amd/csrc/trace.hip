@@ -21,9 +21,8 @@
 namespace pgrt {
 
 constexpr int kTraceBlock = 256;
-constexpr int kLdsStack = 32;
 constexpr int kSentinel = 0x7fffffff;  // bottom of every stack: "traversal finished"
-constexpr int kResidentBlocks = 256 * 5;  // 32 KB LDS per block -> 5 blocks per CU
+constexpr int kResidentBlocks = 256 * 7;  // persistent variant: ~7 waves per SIMD
 
 __device__ __forceinline__ bool box_hit(float lox, float hix, float loy, float hiy, float loz,
                                         float hiz, float idx, float idy, float idz, float oix,
@@ -35,6 +34,47 @@ __device__ __forceinline__ bool box_hit(float lox, float hix, float loy, float h
     const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
     tent = t0;
     return t0 <= t1 * 1.000001f;  // conservative: rounding never culls a box a hit lies in
+}
+
+// Moeller-Trumbore as Embree's closest-hit path evaluates it (see oracle/oracle.c): e1 = v0 - v1,
+// e2 = v2 - v0 (precomputed), Ng = e2 x e1, scaled edge tests, IEEE divisions.  Closest hit in
+// (tnear, tfar]; ties in t go to the smaller original triangle index.
+__device__ __forceinline__ void tri_test(float4 q0, float4 q1, float4 q2, float ox, float oy, float oz, float dx,
+                                         float dy, float dz, float tnear, float tfar, float& best_t, float& best_u,
+                                         float& best_v, int& best_prim) {
+    const float e1x = q1.x, e1y = q1.y, e1z = q1.z;
+    const float e2x = q2.x, e2y = q2.y, e2z = q2.z;
+    const float ngx = e2y * e1z - e2z * e1y;
+    const float ngy = e2z * e1x - e2x * e1z;
+    const float ngz = e2x * e1y - e2y * e1x;
+    const float cx = q0.x - ox, cy = q0.y - oy, cz = q0.z - oz;
+    const float rx = cy * dz - cz * dy;
+    const float ry = cz * dx - cx * dz;
+    const float rz = cx * dy - cy * dx;
+    const float den = ngx * dx + ngy * dy + ngz * dz;
+    const float absden = fabsf(den);
+    const float U = xorsign(rx * e2x + ry * e2y + rz * e2z, den);
+    const float V = xorsign(rx * e1x + ry * e1y + rz * e1z, den);
+    if (den != 0.0f && U >= 0.0f && V >= 0.0f && U + V <= absden) {
+        const float T = xorsign(ngx * cx + ngy * cy + ngz * cz, den);
+        const float t = T / absden;
+        if (t > tnear && t <= tfar) {
+            const int prim = __float_as_int(q0.w);
+            if (best_prim < 0 || t < best_t || (t == best_t && prim < best_prim)) {
+                best_t = t;
+                best_u = U / absden;
+                best_v = V / absden;
+                best_prim = prim;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ int ray_count(const int* count_dev, int count_terms, int count_host, int cap) {
+    if (!count_dev) return count_host;
+    int n = 0;
+    for (int k = 0; k < count_terms; ++k) n += count_dev[k];
+    return min(n, cap);
 }
 
 // PERSIST: waves pull 64-ray batches from `fetch` (else: static grid-stride assignment).
@@ -51,12 +91,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
     __shared__ int lstack[kLdsStack * kTraceBlock];
     const int tid = threadIdx.x;
     const int lane = __lane_id();
-    int n = count_host;
-    if (count_dev) {
-        n = 0;
-        for (int k = 0; k < count_terms; ++k) n += count_dev[k];
-        n = min(n, cap);
-    }
+    const int n = ray_count(count_dev, count_terms, count_host, cap);
     int* gst = gstack + (size_t)(blockIdx.x * kTraceBlock + tid) * kGlobalStack;
     unsigned long long nvis = 0, ntest = 0, mvis = 0, mtest = 0;
 #define PUSH(v)                                                  \
@@ -135,37 +170,19 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
             }
             // ---- triangle tests for the parked leaves ----
             while (leaf < 0) {
-                const int first = leaf_first(leaf), cnt = leaf_count(leaf);
-                for (int k = first; k < first + cnt; ++k) {
+                const int first = leaf_first(leaf), end = first + leaf_count(leaf);
+                // software-pipelined: the next triangle's loads are in flight while this one is
+                // tested, so a leaf costs about one memory latency instead of one per triangle
+                float4 p0 = s.tri[3 * first], p1 = s.tri[3 * first + 1], p2 = s.tri[3 * first + 2];
+                for (int k = first; k < end; ++k) {
                     if (COUNT) ++rtest;
-                    const float4 q0 = s.tri[3 * k], q1 = s.tri[3 * k + 1], q2 = s.tri[3 * k + 2];
-                    // e1 = v0 - v1, e2 = v2 - v0 (precomputed), Ng = e2 x e1
-                    const float e1x = q1.x, e1y = q1.y, e1z = q1.z;
-                    const float e2x = q2.x, e2y = q2.y, e2z = q2.z;
-                    const float ngx = e2y * e1z - e2z * e1y;
-                    const float ngy = e2z * e1x - e2x * e1z;
-                    const float ngz = e2x * e1y - e2y * e1x;
-                    const float cx = q0.x - ox, cy = q0.y - oy, cz = q0.z - oz;
-                    const float rx = cy * dz - cz * dy;
-                    const float ry = cz * dx - cx * dz;
-                    const float rz = cx * dy - cy * dx;
-                    const float den = ngx * dx + ngy * dy + ngz * dz;
-                    const float absden = fabsf(den);
-                    const float U = xorsign(rx * e2x + ry * e2y + rz * e2z, den);
-                    const float V = xorsign(rx * e1x + ry * e1y + rz * e1z, den);
-                    if (den != 0.0f && U >= 0.0f && V >= 0.0f && U + V <= absden) {
-                        const float T = xorsign(ngx * cx + ngy * cy + ngz * cz, den);
-                        const float t = T / absden;
-                        if (t > tnear && t <= tfar) {
-                            const int prim = __float_as_int(q0.w);
-                            if (best_prim < 0 || t < best_t || (t == best_t && prim < best_prim)) {
-                                best_t = t;
-                                best_u = U / absden;
-                                best_v = V / absden;
-                                best_prim = prim;
-                            }
-                        }
+                    const float4 q0 = p0, q1 = p1, q2 = p2;
+                    if (k + 1 < end) {
+                        p0 = s.tri[3 * k + 3];
+                        p1 = s.tri[3 * k + 4];
+                        p2 = s.tri[3 * k + 5];
                     }
+                    tri_test(q0, q1, q2, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v, best_prim);
                 }
                 leaf = 0;
                 if (node < 0) {  // the node popped after parking is a leaf too: test it now
@@ -192,6 +209,143 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
     }
 }
 
+// ---------------------------------------------------------------- 8-wide traversal
+//
+// Stack entries are node groups (child_base, hit bits << 24 | imask): the children of one wide
+// node still to visit.  Hit bits sit at 24 + (slot ^ oct) with oct = the ray's direction octant,
+// so taking the highest bit first visits children on the side the ray comes from first
+// (slot bit k = child on the + side of axis k).  A visited node's leaf triangles are tested
+// right away; its internal hits become the current group.
+constexpr int kLdsStack8 = 8;  // 8-B groups: 8 x 8 B x 256 lanes = 16 KB per block
+
+__device__ __forceinline__ float qb(unsigned w, int j) { return (float)((w >> (8 * j)) & 0xffu); }
+
+template <bool COUNT>
+__global__ __launch_bounds__(kTraceBlock) void k_trace8(SceneView s, const float4* __restrict__ ro,
+                                                        const float4* __restrict__ rd, float4* __restrict__ hits,
+                                                        const int* __restrict__ count_dev, int count_terms,
+                                                        int count_host, int cap, int* __restrict__ gstack,
+                                                        unsigned long long* __restrict__ counters) {
+    __shared__ uint2 lstack[kLdsStack8 * kTraceBlock];
+    const int tid = threadIdx.x;
+    const int n = ray_count(count_dev, count_terms, count_host, cap);
+    uint2* gst = reinterpret_cast<uint2*>(gstack + (size_t)(blockIdx.x * kTraceBlock + tid) * kGlobalStack);
+    unsigned long long nvis = 0, ntest = 0, mvis = 0, mtest = 0;
+    for (int i = blockIdx.x * kTraceBlock + tid; i < n; i += gridDim.x * kTraceBlock) {
+        const float4 o4 = ro[i];
+        const float4 d4 = rd[i];
+        const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
+        const float dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
+        const float sdx = fabsf(dx) < 1e-30f ? copysignf(1e-30f, dx) : dx;
+        const float sdy = fabsf(dy) < 1e-30f ? copysignf(1e-30f, dy) : dy;
+        const float sdz = fabsf(dz) < 1e-30f ? copysignf(1e-30f, dz) : dz;
+        const float idx = __builtin_amdgcn_rcpf(sdx), idy = __builtin_amdgcn_rcpf(sdy),
+                    idz = __builtin_amdgcn_rcpf(sdz);
+        const bool px = idx >= 0.0f, py = idy >= 0.0f, pz = idz >= 0.0f;
+        const unsigned oct = (dx > 0.0f ? 1u : 0u) | (dy > 0.0f ? 2u : 0u) | (dz > 0.0f ? 4u : 0u);
+        float best_t = tfar, best_u = 0.0f, best_v = 0.0f;
+        int best_prim = -1;
+        unsigned rvis = 0, rtest = 0;
+        int sp = 0;
+        // current node group: the root alone (slot 0 of a virtual parent with child_base 0)
+        unsigned gbase = 0, gbits = (1u << (24 + oct)) | 1u;
+        if (!(tfar >= 0.0f)) gbits = 0;  // padding slots / empty segments
+        unsigned tbase = 0, tbits = 0;
+        for (;;) {
+            // ---- node phase: lanes without pending triangles descend until every lane of the
+            // wave holds a triangle group or is finished ("while-while", Aila & Laine 2009) ----
+            while (tbits == 0u) {
+                if (gbits <= 0x00ffffffu) {
+                    if (sp == 0) break;  // traversal finished
+                    --sp;
+                    const uint2 g = sp < kLdsStack8 ? lstack[sp * kTraceBlock + tid] : gst[sp - kLdsStack8];
+                    gbase = g.x;
+                    gbits = g.y;
+                }
+                const int pb = 31 - __clz((int)gbits);
+                gbits &= ~(1u << pb);
+                const unsigned slot = (unsigned)(pb - 24) ^ oct;
+                const int child = (int)gbase + __popc(gbits & 0xffu & ((1u << slot) - 1u));
+                if (gbits > 0x00ffffffu) {  // siblings left: save the group
+                    if (sp < kLdsStack8) lstack[sp * kTraceBlock + tid] = make_uint2(gbase, gbits);
+                    else gst[sp - kLdsStack8] = make_uint2(gbase, gbits);
+                    ++sp;
+                }
+                const Bvh8Node* nd = s.nodes8 + child;
+                const float4 p = nd->p;
+                const uint4 m = nd->m, qx = nd->qx, qy = nd->qy, qz = nd->qz;
+                if (COUNT) ++rvis;
+                const unsigned eb = __float_as_uint(p.w);
+                const float ax = __uint_as_float((eb & 0xffu) << 23) * idx;
+                const float ay = __uint_as_float(((eb >> 8) & 0xffu) << 23) * idy;
+                const float az = __uint_as_float(((eb >> 16) & 0xffu) << 23) * idz;
+                const float bx = (p.x - ox) * idx, by = (p.y - oy) * idy, bz = (p.z - oz) * idz;
+                const unsigned imask = eb >> 24;
+                // near / far planes by the ray's sign per axis
+                const unsigned nx0 = px ? qx.x : qx.z, nx1 = px ? qx.y : qx.w;
+                const unsigned fx0 = px ? qx.z : qx.x, fx1 = px ? qx.w : qx.y;
+                const unsigned ny0 = py ? qy.x : qy.z, ny1 = py ? qy.y : qy.w;
+                const unsigned fy0 = py ? qy.z : qy.x, fy1 = py ? qy.w : qy.y;
+                const unsigned nz0 = pz ? qz.x : qz.z, nz1 = pz ? qz.y : qz.w;
+                const unsigned fz0 = pz ? qz.z : qz.x, fz1 = pz ? qz.w : qz.y;
+                unsigned nbits = 0, tb = 0;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int j = k & 3;
+                    const unsigned wnx = k < 4 ? nx0 : nx1, wfx = k < 4 ? fx0 : fx1;
+                    const unsigned wny = k < 4 ? ny0 : ny1, wfy = k < 4 ? fy0 : fy1;
+                    const unsigned wnz = k < 4 ? nz0 : nz1, wfz = k < 4 ? fz0 : fz1;
+                    const float t0 = fmaxf(fmaxf(fmaf(qb(wnx, j), ax, bx), fmaf(qb(wny, j), ay, by)),
+                                           fmaxf(fmaf(qb(wnz, j), az, bz), 0.0f));
+                    const float t1 = fminf(fminf(fmaf(qb(wfx, j), ax, bx), fmaf(qb(wfy, j), ay, by)),
+                                           fminf(fmaf(qb(wfz, j), az, bz), best_t));
+                    const unsigned meta = ((k < 4 ? m.z : m.w) >> (8 * j)) & 0xffu;
+                    if (meta != 0u && t0 <= t1 * 1.000001f) {
+                        if ((imask >> k) & 1u) nbits |= 1u << (24 + (k ^ oct));
+                        else tb |= (meta >> 5) << (meta & 31u);
+                    }
+                }
+                gbase = m.x;
+                gbits = nbits | imask;
+                tbase = m.y;
+                tbits = tb;
+            }
+            if (tbits == 0u) break;  // no triangles pending and no nodes left
+            // ---- triangle phase: loads of the next triangle overlap the current test ----
+            int k = (int)tbase + __ffs((int)tbits) - 1;
+            tbits &= tbits - 1u;
+            float4 p0 = s.tri[3 * k], p1 = s.tri[3 * k + 1], p2 = s.tri[3 * k + 2];
+            for (;;) {
+                const float4 q0 = p0, q1 = p1, q2 = p2;
+                const bool more = tbits != 0u;
+                if (more) {
+                    k = (int)tbase + __ffs((int)tbits) - 1;
+                    tbits &= tbits - 1u;
+                    p0 = s.tri[3 * k];
+                    p1 = s.tri[3 * k + 1];
+                    p2 = s.tri[3 * k + 2];
+                }
+                if (COUNT) ++rtest;
+                tri_test(q0, q1, q2, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v, best_prim);
+                if (!more) break;
+            }
+        }
+        hits[i] = make_float4(best_t, best_u, best_v, __int_as_float(best_prim));
+        if (COUNT) {
+            nvis += rvis;
+            ntest += rtest;
+            mvis = rvis > mvis ? rvis : mvis;
+            mtest = rtest > mtest ? rtest : mtest;
+        }
+    }
+    if (COUNT) {
+        atomicAdd(&counters[0], nvis);
+        atomicAdd(&counters[1], ntest);
+        atomicMax(&counters[2], mvis);
+        atomicMax(&counters[3], mtest);
+    }
+}
+
 void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4* hits, const int* count_dev,
                   int count_host, int max_count, int* fetch, int* gstack, int gstack_threads,
                   unsigned long long* counters, bool count, hipStream_t stream, int expect, int count_terms) {
@@ -203,6 +357,17 @@ void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4
         const char* e = getenv("PGRT_TRACE_VARIANT");
         return e ? atoi(e) : 2;
     }();
+    if (s.wide) {
+        int grid = ceil_div(expect > 0 && expect < max_count ? expect : max_count, kTraceBlock);
+        if (grid > gstack_threads / kTraceBlock) grid = gstack_threads / kTraceBlock;
+        if (count)
+            hipLaunchKernelGGL((k_trace8<true>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
+                               count_dev, count_terms, count_host, max_count, gstack, counters);
+        else
+            hipLaunchKernelGGL((k_trace8<false>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
+                               count_dev, count_terms, count_host, max_count, gstack, counters);
+        return;
+    }
     const bool persist = variant & 1, ww = variant & 2;
     // size the grid to the expected count; persistent waves need no more than the machine
     // keeps resident; never more than the global overflow stacks cover

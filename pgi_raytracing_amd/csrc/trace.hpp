@@ -5,7 +5,11 @@
 
 namespace pgrt {
 
-constexpr int kGlobalStack = 96;  // per-thread overflow entries past the LDS stack
+// traversal stack: kLdsStack entries per lane in LDS (16 x 4 B x 256 lanes = 16 KB per block,
+// so LDS does not cap occupancy below the VGPR limit), deeper entries in a per-thread global
+// region of kGlobalStack entries
+constexpr int kLdsStack = 16;
+constexpr int kGlobalStack = 112;
 constexpr int kTile = 64;         // image tile side (multi-GPU unit, level-0 ray order)
 constexpr int kMaxLevels = 16;    // max_level + 1 <= kMaxLevels
 
@@ -85,7 +89,8 @@ void launch_unpack_tiles(const float* gathered, float* rgba, int width, int heig
 constexpr int kBuilderLbvh = 0;  // Karras 2012 over 63-bit Morton codes
 constexpr int kBuilderPloc = 1;  // PLOC clustering over the same Morton order + SAH collapse
 struct BuildOut {
-    int builder;  // in: kBuilder*
+    int builder;   // in: kBuilder*
+    int leaf_max;  // in: triangles per binary leaf (<= kLeafMaxTris; kWideLeafMaxTris for BVH8)
     int root;
     int num_nodes;
     int max_depth;
@@ -95,6 +100,10 @@ void build_ploc(const float* pos_dev, const int* order, int n, float4* tri_out, 
                 BuildOut* out, int* iterations, hipStream_t stream);
 void build_lbvh(const float* pos_dev, int ntri, float4* tri_out, BvhNode* nodes_out, int* scratch_int,
                 void* sort_tmp, size_t sort_tmp_bytes, float pad, BuildOut* out, hipStream_t stream);
+// collapse the binary BVH (root: node index or leaf code; root box used for a leaf root) into
+// the 8-wide quantized layout; tri_out receives the triangles in wide-leaf order
+void build_bvh8(const BvhNode* bin, const float4* tri_in, int root, int n, float4 root_lo, float4 root_hi,
+                Bvh8Node* out, float4* tri_out, int* num_nodes, int* depth, hipStream_t stream);
 size_t lbvh_sort_temp_bytes(int ntri);
 size_t lbvh_scratch_ints(int ntri);
 void launch_pack_attributes(const float* nrm, const float* uv, const int* mat, int ntri, float* attr,

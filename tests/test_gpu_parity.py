@@ -175,3 +175,31 @@ def test_distributed_world1_equals_render(gpu_ctx, avenger_scene):
     a, _ = gpu_ctx.render(p)
     b, _ = gpu_ctx.render_distributed(p)
     assert (np.nan_to_num(a, nan=5) == np.nan_to_num(b, nan=5)).all()
+
+
+@pytest.mark.parametrize("builder,width", [("lbvh", "2"), ("ploc", "8"), ("lbvh", "8")])
+def test_bvh_layouts_bit_exact(gpu_ctx, avenger_scene, monkeypatch, builder, width):
+    """Every BVH builder / traversal layout gives the same closest hits and frames: the hit is
+    order-independent (ties to the smaller triangle index, conservative box tests)."""
+    monkeypatch.setenv("PGRT_BVH", builder)
+    monkeypatch.setenv("PGRT_BVH_WIDTH", width)
+    try:
+        gpu_ctx.set_scene(avenger_scene)
+        info = gpu_ctx.bvh_info()
+        assert info.width == int(width) and info.builder == (0 if builder == "lbvh" else 1)
+        rays = _random_rays(avenger_scene, 20000, 11)
+        hg = gpu_ctx.intersect(rays)
+        ho = _oracle(avenger_scene).intersect(rays)
+        eq = (hg.view(np.int32) == ho.view(np.int32)).all(1)
+        assert eq.all(), f"{(~eq).sum()} / {len(eq)} hit records differ"
+        cam = abi.default_camera(96, 64)
+        gpu_ctx.set_camera(cam)
+        p = abi.make_params(spp_side=2, max_level=5, dof=1, jitter=abi.PGRT_JITTER_HASH)
+        img, _ = gpu_ctx.render(p)
+        ref, _ = _oracle(avenger_scene).render(cam, p)
+        _, exact = assert_frames_match(img, ref)
+        assert exact == 1.0
+    finally:
+        monkeypatch.delenv("PGRT_BVH")
+        monkeypatch.delenv("PGRT_BVH_WIDTH")
+        gpu_ctx.set_scene(avenger_scene)

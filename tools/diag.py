@@ -26,7 +26,7 @@ def main():
     info = ctx.bvh_info()
     print(json.dumps({"bvh": {"builder": ["lbvh", "ploc"][info.builder], "iters": info.build_iterations,
                               "tris": info.num_triangles, "nodes": info.num_nodes, "depth": info.max_depth,
-                              "build_ms": round(info.build_ms, 3), "set_scene_s": round(time.time() - t, 3)}}))
+                              "width": info.width, "build_ms": round(info.build_ms, 3), "set_scene_s": round(time.time() - t, 3)}}))
     ctx.set_camera(abi.default_camera(W, H))
     p = abi.make_params(spp_side=S, max_level=d, dof=dof,
                         jitter=abi.PGRT_JITTER_HASH if S > 1 or dof else abi.PGRT_JITTER_NONE)
