@@ -149,6 +149,8 @@ typedef struct pgrt_bvh_info {
     int builder;          /* 0 Karras LBVH, 1 PLOC over the Morton order (default) */
     int build_iterations; /* PLOC merge iterations */
     int width;            /* traversal layout: 2 (binary, default) or 8 (quantized 8-wide) */
+    int num_references;   /* BVH leaf entries: triangles plus early-split-clipping duplicates */
+    float split_beta;     /* split budget used (extra references / triangles), 0 = off */
 } pgrt_bvh_info;
 
 /* ---- context ---- */
@@ -220,6 +222,15 @@ typedef struct pgrt_level_diag {
     uint64_t rays, shadow_rays;
     uint64_t visits, tests, max_visits, max_tests;
     uint64_t shadow_visits, shadow_tests, shadow_max_visits, shadow_max_tests;
+    uint64_t max_wave_iterations; /* binary traversal: node steps + leaf rounds of the longest
+                                     wave (lower bound) -- the latency chain of the level */
+    uint64_t max_ray_ticks;       /* longest single-ray traversal, 100 MHz wall-clock ticks */
+    uint64_t stack_spills;        /* traversal stack pushes past the LDS part (global memory) */
+    uint64_t max_stack;           /* deepest traversal stack of one ray */
+    uint64_t longest_ray[6];      /* the longest ray: visits, tests, leaf rounds, node-phase,
+                                     leaf-phase and node-load shader cycles / 64 */
+    double ms_trace, ms_shade;    /* this level's launches (profile >= 1 on the call; summed
+                                     over sample batches) */
 } pgrt_level_diag;
 int pgrt_frame_diag(const pgrt_ctx* ctx, pgrt_level_diag* out, int max_levels);
 

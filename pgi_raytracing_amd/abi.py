@@ -137,7 +137,10 @@ class Stats(C.Structure):
 
 class LevelDiag(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("rays", "shadow_rays", "visits", "tests", "max_visits", "max_tests",
-                                          "shadow_visits", "shadow_tests", "shadow_max_visits", "shadow_max_tests")]
+                                          "shadow_visits", "shadow_tests", "shadow_max_visits", "shadow_max_tests",
+                                          "max_wave_iterations", "max_ray_ticks", "stack_spills", "max_stack",
+                                          "lr_visits", "lr_tests", "lr_leaves", "lr_node_cyc64", "lr_leaf_cyc64",
+                                          "lr_load_cyc64")] + [("ms_trace", C.c_double), ("ms_shade", C.c_double)]
 
 
 class BvhInfo(C.Structure):
@@ -152,6 +155,8 @@ class BvhInfo(C.Structure):
         ("builder", C.c_int),
         ("build_iterations", C.c_int),
         ("width", C.c_int),
+        ("num_references", C.c_int),
+        ("split_beta", C.c_float),
     ]
 
 

@@ -236,10 +236,6 @@ void build_lbvh(const float* pos, int n, float4* tri, BvhNode* nodes, int* scrat
     hipLaunchKernelGGL(k_morton, dim3(grid), dim3(kB), 0, stream, pos, n, bounds, keys_a, vals_a);
     size_t tb = sort_tmp_bytes;
     PGRT_HIP(hipcub::DeviceRadixSort::SortPairs(sort_tmp, tb, keys_a, keys_b, vals_a, vals_b, n, 0, 63, stream));
-    if (out->builder == kBuilderPloc && n >= 2) {  // PLOC clustering over the Morton order
-        build_ploc(pos, vals_b, n, tri, nodes, pad, out, &out->iterations, stream);
-        return;
-    }
     hipLaunchKernelGGL(k_gather_tris, dim3(grid), dim3(kB), 0, stream, pos, vals_b, n, tri);
     if (n >= 2) {
         hipLaunchKernelGGL(k_karras, dim3(ceil_div(n - 1, kB)), dim3(kB), 0, stream, keys_b, n, nodes, parent, kids,
@@ -254,6 +250,7 @@ void build_lbvh(const float* pos, int n, float4* tri, BvhNode* nodes, int* scrat
     out->root = (n >= 2) ? 0 : leaf_encode(0, 1);
     out->num_nodes = n >= 2 ? n - 1 : 0;
     out->max_depth = md;
+    out->refs = n;
 }
 
 }  // namespace pgrt

@@ -120,6 +120,7 @@ struct SceneView {  // kernel-argument view of the device scene
     const Bvh8Node* nodes8;  // 8-wide BVH (root = node 0) when wide != 0; tri is then in its order
     int wide;
     int ntri;
+    int depth;             // binary BVH depth (bounds the traversal stack)
     const float* attr;     // 16 floats per ORIGINAL triangle: n0 n1 n2 uv0 uv1 uv2, mat (bits)
     const DevMaterial* mats;
     const DevTexture* tex;

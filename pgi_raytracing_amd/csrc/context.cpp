@@ -26,7 +26,7 @@ constexpr int kTraceGridThreads = 2048 * 256;    // persistent trace grid (globa
 struct StageTimer {
     struct Rec {
         hipEvent_t a, b;
-        int cat;
+        int cat, cat2;  // cat2: optional second bucket (per-level time), -1 none
     };
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;
@@ -41,9 +41,9 @@ struct StageTimer {
         PGRT_HIP(hipEventCreate(&e));
         return e;
     }
-    int begin(hipStream_t s, int cat) {
+    int begin(hipStream_t s, int cat, int cat2 = -1) {
         if (!on) return -1;
-        Rec r{get(), get(), cat};
+        Rec r{get(), get(), cat, cat2};
         PGRT_HIP(hipEventRecord(r.a, s));
         recs.push_back(r);
         return (int)recs.size() - 1;
@@ -56,6 +56,7 @@ struct StageTimer {
             float t = 0;
             PGRT_HIP(hipEventElapsedTime(&t, r.a, r.b));
             ms[r.cat] += t;
+            if (r.cat2 >= 0) ms[r.cat2] += t;
             pool.push_back(r.a);
             pool.push_back(r.b);
         }
@@ -70,7 +71,8 @@ struct StageTimer {
     }
 };
 
-enum { CAT_RAYGEN, CAT_TRACE, CAT_SHADE, CAT_SHADOW, CAT_COMBINE, CAT_N };
+enum { CAT_RAYGEN, CAT_TRACE, CAT_SHADE, CAT_SHADOW, CAT_COMBINE, CAT_LTRACE, CAT_LSHADE = CAT_LTRACE + kMaxLevels,
+       CAT_N = CAT_LSHADE + kMaxLevels };
 
 }  // namespace
 
@@ -111,6 +113,7 @@ struct pgrt_ctx {
     DevBuf<float> out_tmp;
     StageTimer timer;
     std::vector<FrameCounters> last_fc;  // per batch, for pgrt_frame_diag
+    double level_ms[kMaxLevels][2] = {};  // per-level trace / shade ms of the last profiled call
     int expect_count[kMaxLevels] = {0};   // grid hints from the previous frame (0 = unknown)
     int expect_shadow_total = 0;
 
@@ -266,33 +269,42 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
     DevBuf<float> pos;
     pos.alloc((size_t)n * 9);
     PGRT_HIP(hipMemcpyAsync(pos.p, d->positions, (size_t)n * 9 * sizeof(float), hipMemcpyHostToDevice, st));
-    ctx->tri.alloc((size_t)n * 3);
-    ctx->nodes.alloc((size_t)std::max(1, n - 1));
-    DevBuf<int> scratch;
-    scratch.alloc(lbvh_scratch_ints(n));
-    const size_t tmp_bytes = lbvh_sort_temp_bytes(n);
-    DevBuf<unsigned char> sort_tmp;
-    sort_tmp.alloc(tmp_bytes);
     BuildOut bo{};
-    // layout knobs, read per set_scene so one process can compare them (tests, tools/ab_bvh.sh):
+    // layout knobs, read per set_scene so one process can compare them (tests, tools/ab_env.sh):
     // PGRT_BVH=lbvh selects the plain Karras LBVH (default PLOC); PGRT_BVH_WIDTH=8 the
-    // quantized 8-wide traversal layout (default binary, faster on the avenger proxy)
+    // quantized 8-wide traversal layout (default binary, faster on the avenger proxy);
+    // PGRT_SPLIT=beta the early-split-clipping budget of the PLOC build (extra references as a
+    // fraction of the triangle count, 0 = off)
     const char* eb = getenv("PGRT_BVH");
-    const int builder = (eb && std::string(eb) == "lbvh") ? kBuilderLbvh : kBuilderPloc;
+    const int builder = (eb && std::string(eb) == "lbvh") || n < 2 ? kBuilderLbvh : kBuilderPloc;
     const char* ew = getenv("PGRT_BVH_WIDTH");
     const int width = (ew && std::string(ew) == "8") ? 8 : 2;
+    const char* es = getenv("PGRT_SPLIT");
+    const float beta = es ? std::max(0.0f, std::min(4.0f, (float)atof(es))) : kDefaultSplitBeta;
     bo.builder = builder;
     bo.leaf_max = width == 8 ? kWideLeafMaxTris : kLeafMaxTris;
     auto tb = std::chrono::steady_clock::now();
-    build_lbvh(pos.p, n, ctx->tri.p, ctx->nodes.p, scratch.p, sort_tmp.p, tmp_bytes, pad, &bo, st);
+    if (builder == kBuilderPloc) {
+        build_ploc_refs(pos.p, n, beta, pad, ext, ctx->tri, ctx->nodes, &bo, st);
+    } else {
+        ctx->tri.alloc((size_t)n * 3);
+        ctx->nodes.alloc((size_t)std::max(1, n - 1));
+        DevBuf<int> scratch;
+        scratch.alloc(lbvh_scratch_ints(n));
+        const size_t tmp_bytes = lbvh_sort_temp_bytes(n);
+        DevBuf<unsigned char> sort_tmp;
+        sort_tmp.alloc(tmp_bytes);
+        build_lbvh(pos.p, n, ctx->tri.p, ctx->nodes.p, scratch.p, sort_tmp.p, tmp_bytes, pad, &bo, st);
+    }
+    const int m = bo.refs;
     int wide_nodes = 0, wide_depth = 0;
     if (width == 8) {
-        ctx->nodes8.alloc((size_t)std::max(1, n));
+        ctx->nodes8.alloc((size_t)std::max(1, m));
         DevBuf<float4> tri8;
-        tri8.alloc((size_t)n * 3);
+        tri8.alloc((size_t)m * 3);
         const float4 rlo = make_float4(lo[0] - pad, lo[1] - pad, lo[2] - pad, 0.0f);
         const float4 rhi = make_float4(hi[0] + pad, hi[1] + pad, hi[2] + pad, 0.0f);
-        build_bvh8(ctx->nodes.p, ctx->tri.p, bo.root, n, rlo, rhi, ctx->nodes8.p, tri8.p, &wide_nodes, &wide_depth,
+        build_bvh8(ctx->nodes.p, ctx->tri.p, bo.root, m, rlo, rhi, ctx->nodes8.p, tri8.p, &wide_nodes, &wide_depth,
                    st);
         std::swap(ctx->tri.p, tri8.p);  // traversal reads the triangles in wide-leaf order
         std::swap(ctx->tri.n, tri8.n);
@@ -310,6 +322,7 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
     v.nodes8 = width == 8 ? ctx->nodes8.p : nullptr;
     v.wide = width == 8 ? 1 : 0;
     v.ntri = n;
+    v.depth = bo.max_depth;
     v.attr = ctx->attr.p;
     v.mats = ctx->mats.p;
     v.tex = ctx->texd.p;
@@ -326,6 +339,8 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
     bi.build_ms = std::chrono::duration<double, std::milli>(te - tb).count();
     bi.builder = bo.builder;
     bi.build_iterations = bo.iterations;
+    bi.num_references = bo.refs;
+    bi.split_beta = builder == kBuilderPloc ? beta : 0.0f;
     for (int k = 0; k < 3; ++k) {
         bi.scene_lo[k] = lo[k];
         bi.scene_hi[k] = hi[k];
@@ -433,12 +448,12 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
                 LevelNodes ln{ctx->n_color[L]->p, ctx->n_link[L]->p, ctx->n_att[L]->p};
                 // grid hints: last frame's per-level counts (+25 %); level 0 is exact
                 const int ex = L == 0 ? n0 : ctx->expect_count[L];
-                id = ctx->timer.begin(s, CAT_TRACE);
+                id = ctx->timer.begin(s, CAT_TRACE, CAT_LTRACE + L);
                 launch_trace(ctx->view, qc.ro, qc.rd, qc.hit, &fcd->count[L], 0, maxc, &fcd->fetch[L],
                              ctx->gstack.p, kTraceGridThreads, fcd->trav[L], p->profile >= 2, s, ex);
                 ctx->timer.end(s, id);
                 ++trace_launches;
-                id = ctx->timer.begin(s, CAT_SHADE);
+                id = ctx->timer.begin(s, CAT_SHADE, CAT_LSHADE + L);
                 launch_shade(ctx->view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex);
                 ctx->timer.end(s, id);
             }
@@ -553,6 +568,10 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
         st->ms_shade = ms[CAT_SHADE];
         st->ms_shadow = ms[CAT_SHADOW];
         st->ms_combine = ms[CAT_COMBINE];
+        for (int L = 0; L < kMaxLevels; ++L) {
+            ctx->level_ms[L][0] = ms[CAT_LTRACE + L];
+            ctx->level_ms[L][1] = ms[CAT_LSHADE + L];
+        }
         st->trace_launches = trace_launches;
         st->levels = levels;
         st->overflow_retries = retries;
@@ -865,6 +884,14 @@ int pgrt_frame_diag(const pgrt_ctx* ctx, pgrt_level_diag* out, int max_levels) {
             d.tests += h.trav[L][1];
             d.max_visits = std::max<uint64_t>(d.max_visits, h.trav[L][2]);
             d.max_tests = std::max<uint64_t>(d.max_tests, h.trav[L][3]);
+            d.max_wave_iterations = std::max<uint64_t>(d.max_wave_iterations, h.trav[L][4]);
+            d.max_ray_ticks = std::max<uint64_t>(d.max_ray_ticks, h.trav[L][5]);
+            d.stack_spills += h.trav[L][6];
+            d.max_stack = std::max<uint64_t>(d.max_stack, h.trav[L][7]);
+            for (int k = 0; k < 6; ++k)
+                d.longest_ray[k] = std::max<uint64_t>(d.longest_ray[k], h.trav[L][8 + k] & 0xffffffull);
+            d.ms_trace = ctx->level_ms[L][0];
+            d.ms_shade = ctx->level_ms[L][1];
             d.shadow_visits += h.trav[kMaxLevels + L][0];
             d.shadow_tests += h.trav[kMaxLevels + L][1];
             d.shadow_max_visits = std::max<uint64_t>(d.shadow_max_visits, h.trav[kMaxLevels + L][2]);

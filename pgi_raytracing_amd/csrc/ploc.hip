@@ -32,19 +32,14 @@ __device__ __forceinline__ float half_area(float4 lo, float4 hi) {
     return dx * dy + dy * dz + dz * dx;
 }
 
-__global__ __launch_bounds__(kB) void k_ploc_init(const float* __restrict__ pos, const int* __restrict__ order, int n,
-                                                  float pad, float4* nlo, float4* nhi, int* cl_node, float4* cl_lo,
-                                                  float4* cl_hi, int* parent) {
+// leaves = references (padded boxes; rlo.w = triangle id bits) in Morton order
+__global__ __launch_bounds__(kB) void k_ploc_init(const float4* __restrict__ rlo, const float4* __restrict__ rhi,
+                                                  const int* __restrict__ order, int n, float4* nlo, float4* nhi,
+                                                  int* cl_node, float4* cl_lo, float4* cl_hi, int* parent) {
     const int i = blockIdx.x * kB + threadIdx.x;
     if (i >= n) return;
-    const float* p = pos + 9 * (size_t)order[i];
-    float4 lo, hi;
-    lo.x = fminf(fminf(p[0], p[3]), p[6]) - pad;
-    lo.y = fminf(fminf(p[1], p[4]), p[7]) - pad;
-    lo.z = fminf(fminf(p[2], p[5]), p[8]) - pad;
-    hi.x = fmaxf(fmaxf(p[0], p[3]), p[6]) + pad;
-    hi.y = fmaxf(fmaxf(p[1], p[4]), p[7]) + pad;
-    hi.z = fmaxf(fmaxf(p[2], p[5]), p[8]) + pad;
+    const int r = order[i];
+    float4 lo = rlo[r], hi = rhi[r];
     lo.w = hi.w = 0.0f;
     nlo[i] = lo;
     nhi[i] = hi;
@@ -205,11 +200,12 @@ __global__ __launch_bounds__(kB) void k_ploc_write(int n, const float4* __restri
     out[q] = nd;
 }
 
-__global__ __launch_bounds__(kB) void k_ploc_tris(const float* __restrict__ pos, const int* __restrict__ order,
-                                                  const int* __restrict__ offset, int n, float4* __restrict__ tri) {
+__global__ __launch_bounds__(kB) void k_ploc_tris(const float* __restrict__ pos, const float4* __restrict__ rlo,
+                                                  const int* __restrict__ order, const int* __restrict__ offset, int n,
+                                                  float4* __restrict__ tri) {
     const int i = blockIdx.x * kB + threadIdx.x;
     if (i >= n) return;
-    const int o = order[i];
+    const int o = __float_as_int(rlo[order[i]].w);  // triangle of this reference
     const int k = offset[i];
     const float* p = pos + 9 * (size_t)o;
     const float v0x = p[0], v0y = p[1], v0z = p[2];
@@ -220,9 +216,10 @@ __global__ __launch_bounds__(kB) void k_ploc_tris(const float* __restrict__ pos,
 
 }  // namespace
 
-// order: triangle indices in Morton order (device); builds nodes/tri like build_lbvh.
-void build_ploc(const float* pos, const int* order, int n, float4* tri, BvhNode* nodes, float pad, BuildOut* out,
-                int* iterations, hipStream_t stream) {
+// order: reference indices in Morton order (device); n references; builds nodes/tri like
+// build_lbvh (one 48-B triangle record per reference, in leaf order).
+void build_ploc(const float* pos, const float4* rlo, const float4* rhi, const int* order, int n, float4* tri,
+                BvhNode* nodes, BuildOut* out, int* iterations, hipStream_t stream) {
     const int total = 2 * n - 1;
     DevBuf<float4> nlo, nhi, cl_lo[2], cl_hi[2];
     DevBuf<int2> kids;
@@ -247,7 +244,7 @@ void build_ploc(const float* pos, const int* order, int n, float4* tri, BvhNode*
     scan_tmp.alloc(scan_bytes);
     misc.alloc(4);
     const int grid = ceil_div(n, kB);
-    hipLaunchKernelGGL(k_ploc_init, dim3(grid), dim3(kB), 0, stream, pos, order, n, pad, nlo.p, nhi.p, cl_node[0].p,
+    hipLaunchKernelGGL(k_ploc_init, dim3(grid), dim3(kB), 0, stream, rlo, rhi, order, n, nlo.p, nhi.p, cl_node[0].p,
                        cl_lo[0].p, cl_hi[0].p, parent.p);
     int m = n, node_base = n, cur = 0, iters = 0;
     unsigned long long tail[2];
@@ -287,7 +284,7 @@ void build_ploc(const float* pos, const int* order, int n, float4* tri, BvhNode*
     if (n >= 2)
         hipLaunchKernelGGL(k_ploc_write, dim3(ceil_div(n - 1, kB)), dim3(kB), 0, stream, n, nlo.p, nhi.p, kids.p,
                            count.p, offset.p, collapse.p, nodes);
-    hipLaunchKernelGGL(k_ploc_tris, dim3(grid), dim3(kB), 0, stream, pos, order, offset.p, n, tri);
+    hipLaunchKernelGGL(k_ploc_tris, dim3(grid), dim3(kB), 0, stream, pos, rlo, order, offset.p, n, tri);
     PGRT_HIP(hipGetLastError());
     int root_collapse = 0, root_count = 1, md = 0;
     const int root = total - 1;

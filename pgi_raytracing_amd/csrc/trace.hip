@@ -22,7 +22,6 @@ namespace pgrt {
 
 constexpr int kTraceBlock = 256;
 constexpr int kSentinel = 0x7fffffff;  // bottom of every stack: "traversal finished"
-constexpr int kResidentBlocks = 256 * 7;  // persistent variant: ~7 waves per SIMD
 
 __device__ __forceinline__ bool box_hit(float lox, float hix, float loy, float hiy, float loz,
                                         float hiz, float idx, float idy, float idz, float oix,
@@ -77,46 +76,47 @@ __device__ __forceinline__ int ray_count(const int* count_dev, int count_terms, 
     return min(n, cap);
 }
 
-// PERSIST: waves pull 64-ray batches from `fetch` (else: static grid-stride assignment).
-// WW: while-while descent until every lane parked a leaf (else: one node step per iteration,
-// internal-node and leaf work interleaved).  Both are schedule choices: results are identical.
-template <bool COUNT, bool PERSIST, bool WW>
+// While-while schedule (Aila & Laine 2009): a lane descends until it parks a leaf, the wave
+// tests triangles once every active lane has one (r1 A/B, profiles/r1/trace_variants.txt: the
+// fastest of {grid-stride, persistent fetch} x {while-while, one step per iteration}).
+// SPILL: stack entries past kLdsStack go to a per-thread global region.  Without SPILL the
+// whole stack is in LDS (dynamic size = BVH depth + 2 entries per lane, chosen at launch):
+// every push/pop is a ds_write/ds_read instead of a flat access that must wait on vmcnt too.
+template <bool COUNT, bool SPILL>
 __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4* __restrict__ ro,
                                                        const float4* __restrict__ rd,
                                                        float4* __restrict__ hits,
                                                        const int* __restrict__ count_dev, int count_terms,
-                                                       int count_host, int cap, int* __restrict__ fetch,
-                                                       int* __restrict__ gstack,
-                                                       unsigned long long* __restrict__ counters) {
-    __shared__ int lstack[kLdsStack * kTraceBlock];
+                                                       int count_host, int cap, int* __restrict__ gstack,
+                                                       unsigned long long* __restrict__ counters, int rpw) {
+    extern __shared__ int lstack[];  // [entries][kTraceBlock]
     const int tid = threadIdx.x;
     const int lane = __lane_id();
     const int n = ray_count(count_dev, count_terms, count_host, cap);
     int* gst = gstack + (size_t)(blockIdx.x * kTraceBlock + tid) * kGlobalStack;
     unsigned long long nvis = 0, ntest = 0, mvis = 0, mtest = 0;
-#define PUSH(v)                                                  \
-    do {                                                         \
-        ++sp;                                                    \
-        if (sp < kLdsStack) lstack[sp * kTraceBlock + tid] = (v); \
-        else gst[sp - kLdsStack] = (v);                          \
+#define PUSH(v)                                                       \
+    do {                                                              \
+        ++sp;                                                         \
+        if (COUNT && sp > msp) msp = sp;                              \
+        if (!SPILL || sp < kLdsStack) lstack[sp * kTraceBlock + tid] = (v); \
+        else {                                                        \
+            if (COUNT) ++nspill;                                      \
+            gst[sp - kLdsStack] = (v);                                \
+        }                                                             \
     } while (0)
-#define POP() ((sp < kLdsStack) ? lstack[(sp--) * kTraceBlock + tid] : gst[(sp--) - kLdsStack])
-    int stride_i = blockIdx.x * kTraceBlock + tid - gridDim.x * kTraceBlock;
+#define POP() ((!SPILL || sp < kLdsStack) ? lstack[(sp--) * kTraceBlock + tid] : gst[(sp--) - kLdsStack])
+    // rpw rays per wave (lanes >= rpw idle): small queues spread over more waves
+    if (lane >= rpw) return;
+    const int wstride = gridDim.x * (kTraceBlock / 64) * rpw;
+    int stride_i = ((blockIdx.x * kTraceBlock + tid) >> 6) * rpw + lane - wstride;
+    unsigned long long witer = 0, nspill = 0, mclk = 0, mray[6] = {0, 0, 0, 0, 0, 0};
+    int msp = 0;
     for (;;) {
-        int i;
-        if constexpr (PERSIST) {
-            int base = 0;
-            if (lane == 0) base = atomicAdd(fetch, 64);
-            base = __shfl(base, 0, 64);
-            if (base >= n) break;
-            i = base + lane;
-            if (i >= n) continue;  // tail of the last batch (whole wave then fetches past n and exits)
-        } else {
-            stride_i += gridDim.x * kTraceBlock;
-            i = stride_i;
-            if (i >= n) break;
-        }
-        const float4 o4 = ro[i];
+        stride_i += wstride;
+        const int i = stride_i;
+        if (i >= n) break;
+    const float4 o4 = ro[i];
         const float4 d4 = rd[i];
         const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
         const float dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
@@ -129,6 +129,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
         float best_t = tfar, best_u = 0.0f, best_v = 0.0f;
         int best_prim = -1;
         unsigned rvis = 0, rtest = 0;
+        long long t_start = 0;
+        unsigned long long rcyc_node = 0, rcyc_leaf = 0, rleaf = 0, rcyc_load = 0;
+        if (COUNT) t_start = wall_clock64();
         int sp = 0;
         lstack[tid] = kSentinel;  // stack[0]
         int node = s.root;
@@ -143,11 +146,21 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
         }
         while (node != kSentinel || leaf < 0) {
             // ---- descend internal nodes until every active lane has parked a leaf ----
+            long long tn0 = 0;
+            if (COUNT) tn0 = clock64();
             while ((unsigned)node < (unsigned)kSentinel) {
+                if (COUNT) ++witer;
                 const BvhNode* nd = s.nodes + node;
+                long long tq0 = 0;
+                if (COUNT) tq0 = clock64();
                 const float4 a = nd->a, b = nd->b, c = nd->c;
                 const int4 d = nd->d;
-                if (COUNT) ++rvis;
+                if (COUNT) {
+                    ++rvis;
+                    // node-load round trip (instrumented variant only): wait for the data here
+                    asm volatile("" ::"v"(a.x), "v"(b.x), "v"(c.x), "v"(d.x));
+                    rcyc_load += (unsigned long long)(clock64() - tq0);
+                }
                 float t0, t1;
                 const bool h0 = box_hit(a.x, a.y, a.z, a.w, c.x, c.y, idx, idy, idz, oix, oiy, oiz, best_t, t0);
                 const bool h1 = box_hit(b.x, b.y, b.z, b.w, c.z, c.w, idx, idy, idz, oix, oiy, oiz, best_t, t1);
@@ -162,14 +175,19 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
                     leaf = node;
                     node = POP();
                 }
-                if constexpr (WW) {
-                    if (!__any(leaf == 0)) break;
-                } else {
-                    break;
-                }
+                if (!__any(leaf == 0)) break;
+            }
+            long long tl0 = 0;
+            if (COUNT) {
+                tl0 = clock64();
+                rcyc_node += (unsigned long long)(tl0 - tn0);
             }
             // ---- triangle tests for the parked leaves ----
             while (leaf < 0) {
+                if (COUNT) {
+                    ++witer;
+                    ++rleaf;
+                }
                 const int first = leaf_first(leaf), end = first + leaf_count(leaf);
                 // software-pipelined: the next triangle's loads are in flight while this one is
                 // tested, so a leaf costs about one memory latency instead of one per triangle
@@ -190,9 +208,20 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
                     node = POP();
                 }
             }
+            if (COUNT) rcyc_leaf += (unsigned long long)(clock64() - tl0);
         }
         hits[i] = make_float4(best_t, best_u, best_v, __int_as_float(best_prim));
         if (COUNT) {
+            const unsigned long long dt = (unsigned long long)(wall_clock64() - t_start);
+            if (dt > mclk) {  // the longest ray's profile
+                mclk = dt;
+                mray[0] = (dt << 24) | min(rvis, 0xffffffu);
+                mray[1] = (dt << 24) | min(rtest, 0xffffffu);
+                mray[2] = (dt << 24) | min(rleaf, 0xffffffull);
+                mray[3] = (dt << 24) | min(rcyc_node >> 6, 0xffffffull);
+                mray[4] = (dt << 24) | min(rcyc_leaf >> 6, 0xffffffull);
+                mray[5] = (dt << 24) | min(rcyc_load >> 6, 0xffffffull);
+            }
             nvis += rvis;
             ntest += rtest;
             mvis = rvis > mvis ? rvis : mvis;
@@ -206,6 +235,16 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
         atomicAdd(&counters[1], ntest);
         atomicMax(&counters[2], mvis);
         atomicMax(&counters[3], mtest);
+        // wave loop iterations (node steps + leaf rounds): every active lane counts the same
+        // iterations of its wave's loops only while it is inside them, so the max over lanes
+        // is a lower bound of the wave's iteration count
+        atomicMax(&counters[4], witer);
+        atomicMax(&counters[5], mclk);  // longest ray, wall_clock64 ticks (100 MHz)
+        atomicAdd(&counters[6], nspill);  // stack pushes past the LDS part
+        atomicMax(&counters[7], (unsigned long long)msp);
+        // the longest ray: (ticks << 24 | x) for x = visits, tests, leaf rounds, node-phase
+        // cycles / 64, leaf-phase cycles / 64 (max picks the longest ray's record)
+        for (int k = 0; k < 6; ++k) atomicMax(&counters[8 + k], mray[k]);
     }
 }
 
@@ -350,13 +389,7 @@ void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4
                   int count_host, int max_count, int* fetch, int* gstack, int gstack_threads,
                   unsigned long long* counters, bool count, hipStream_t stream, int expect, int count_terms) {
     if (max_count <= 0) return;
-    // schedule A/B switch (PGRT_TRACE_VARIANT = bit0 persistent fetch | bit1 while-while).
-    // Measured on the C2 frame (r1, profiles/r1/trace_variants.txt): 2 = grid-stride +
-    // while-while is fastest (1.31 ms vs 1.64-2.10 ms for the others), so it is the default.
-    static const int variant = [] {
-        const char* e = getenv("PGRT_TRACE_VARIANT");
-        return e ? atoi(e) : 2;
-    }();
+    static const bool force_spill = getenv("PGRT_FORCE_SPILL") != nullptr;  // A/B of the stack layout
     if (s.wide) {
         int grid = ceil_div(expect > 0 && expect < max_count ? expect : max_count, kTraceBlock);
         if (grid > gstack_threads / kTraceBlock) grid = gstack_threads / kTraceBlock;
@@ -368,21 +401,30 @@ void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4
                                count_dev, count_terms, count_host, max_count, gstack, counters);
         return;
     }
-    const bool persist = variant & 1, ww = variant & 2;
-    // size the grid to the expected count; persistent waves need no more than the machine
-    // keeps resident; never more than the global overflow stacks cover
-    int grid = ceil_div(expect > 0 && expect < max_count ? expect : max_count, kTraceBlock);
-    if (persist && grid > kResidentBlocks) grid = kResidentBlocks;
+    // rays per wave: full waves for big queues; small (tail) queues may spread thinner
+    static const int tail_rpw = [] {
+        const char* e = getenv("PGRT_TAIL_RPW");
+        return e ? atoi(e) : 64;
+    }();
+    static const int tail_max = [] {
+        const char* e = getenv("PGRT_TAIL_MAX");
+        return e ? atoi(e) : 131072;
+    }();
+    const int ex = expect > 0 && expect < max_count ? expect : max_count;
+    const int rpw = ex <= tail_max ? tail_rpw : 64;
+    int grid = ceil_div(ex, (kTraceBlock / 64) * rpw);
     if (grid > gstack_threads / kTraceBlock) grid = gstack_threads / kTraceBlock;
-#define PGRT_LAUNCH(C, P, W)                                                                               \
-    hipLaunchKernelGGL((k_trace<C, P, W>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits, count_dev, \
-                       count_terms, count_host, max_count, fetch, gstack, counters)
+    // all-LDS stack when the BVH depth fits (depth + 2 entries per lane, <= 64 KB per block)
+    const int entries = s.depth + 2;
+    const bool spill = force_spill || entries * kTraceBlock * 4 > 65536;
+    const size_t lds = (size_t)(spill ? kLdsStack : entries) * kTraceBlock * sizeof(int);
+#define PGRT_LAUNCH(C, S)                                                                                   \
+    hipLaunchKernelGGL((k_trace<C, S>), dim3(grid), dim3(kTraceBlock), lds, stream, s, ro, rd, hits, count_dev, \
+                       count_terms, count_host, max_count, gstack, counters, rpw)
     if (count) {
-        if (persist) { if (ww) PGRT_LAUNCH(true, true, true); else PGRT_LAUNCH(true, true, false); }
-        else { if (ww) PGRT_LAUNCH(true, false, true); else PGRT_LAUNCH(true, false, false); }
+        if (spill) PGRT_LAUNCH(true, true); else PGRT_LAUNCH(true, false);
     } else {
-        if (persist) { if (ww) PGRT_LAUNCH(false, true, true); else PGRT_LAUNCH(false, true, false); }
-        else { if (ww) PGRT_LAUNCH(false, false, true); else PGRT_LAUNCH(false, false, false); }
+        if (spill) PGRT_LAUNCH(false, true); else PGRT_LAUNCH(false, false);
     }
 #undef PGRT_LAUNCH
 }

@@ -23,7 +23,7 @@ struct FrameCounters {
     int fetch[2 * kMaxLevels];     // work counters of the closest-hit launches (level, shadow)
     // profile == 2: per closest-hit launch {sum node visits, sum triangle tests, max visits of
     // one ray, max tests of one ray}; [0, kMaxLevels) level queues, [kMaxLevels, 2k) shadows
-    unsigned long long trav[2 * kMaxLevels][4];
+    unsigned long long trav[2 * kMaxLevels][16];  // visits, tests, max visits, max tests, max wave iterations
 };
 
 struct FrameParams {
@@ -88,6 +88,7 @@ void launch_unpack_tiles(const float* gathered, float* rgba, int width, int heig
 // scene / BVH build
 constexpr int kBuilderLbvh = 0;  // Karras 2012 over 63-bit Morton codes
 constexpr int kBuilderPloc = 1;  // PLOC clustering over the same Morton order + SAH collapse
+constexpr float kDefaultSplitBeta = 0.0f;  // PGRT_SPLIT default (extra references / triangles)
 struct BuildOut {
     int builder;   // in: kBuilder*
     int leaf_max;  // in: triangles per binary leaf (<= kLeafMaxTris; kWideLeafMaxTris for BVH8)
@@ -95,9 +96,14 @@ struct BuildOut {
     int num_nodes;
     int max_depth;
     int iterations;  // PLOC merge iterations
+    int refs;        // leaf entries (triangle references; == triangles without splitting)
 };
-void build_ploc(const float* pos_dev, const int* order, int n, float4* tri_out, BvhNode* nodes_out, float pad,
-                BuildOut* out, int* iterations, hipStream_t stream);
+void build_ploc(const float* pos_dev, const float4* ref_lo, const float4* ref_hi, const int* order, int nref,
+                float4* tri_out, BvhNode* nodes_out, BuildOut* out, int* iterations, hipStream_t stream);
+// PLOC over triangle references (split.hip): beta > 0 adds up to beta * n split references
+// (early split clipping); sizes tri (3 float4 per reference) and nodes; returns the count
+int build_ploc_refs(const float* pos_dev, int ntri, float beta, float pad, float extent, DevBuf<float4>& tri,
+                    DevBuf<BvhNode>& nodes, BuildOut* out, hipStream_t stream);
 void build_lbvh(const float* pos_dev, int ntri, float4* tri_out, BvhNode* nodes_out, int* scratch_int,
                 void* sort_tmp, size_t sort_tmp_bytes, float pad, BuildOut* out, hipStream_t stream);
 // collapse the binary BVH (root: node index or leaf code; root box used for a leaf root) into

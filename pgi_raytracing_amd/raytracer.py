@@ -170,7 +170,8 @@ class Context:
         n = self.L.pgrt_frame_diag(self.h, arr, 16)
         if n < 0:
             raise PgrtError(n, "pgrt_frame_diag")
-        return [{k: int(getattr(arr[i], k)) for k, _ in abi.LevelDiag._fields_} for i in range(n)]
+        return [{k: (float if k.startswith("ms_") else int)(getattr(arr[i], k)) for k, _ in abi.LevelDiag._fields_}
+                for i in range(n)]
 
     def selftest_math(self, pairs: np.ndarray) -> np.ndarray:
         pairs = np.ascontiguousarray(pairs, np.float32).reshape(-1, 2)

@@ -177,16 +177,23 @@ def test_distributed_world1_equals_render(gpu_ctx, avenger_scene):
     assert (np.nan_to_num(a, nan=5) == np.nan_to_num(b, nan=5)).all()
 
 
-@pytest.mark.parametrize("builder,width", [("lbvh", "2"), ("ploc", "8"), ("lbvh", "8")])
-def test_bvh_layouts_bit_exact(gpu_ctx, avenger_scene, monkeypatch, builder, width):
-    """Every BVH builder / traversal layout gives the same closest hits and frames: the hit is
-    order-independent (ties to the smaller triangle index, conservative box tests)."""
+@pytest.mark.parametrize("builder,width,split", [("lbvh", "2", "0"), ("ploc", "8", "0"), ("lbvh", "8", "0"),
+                                                 ("ploc", "2", "0"), ("ploc", "2", "1.0"), ("ploc", "8", "0.5")])
+def test_bvh_layouts_bit_exact(gpu_ctx, avenger_scene, monkeypatch, builder, width, split):
+    """Every BVH builder / traversal layout / split budget gives the same closest hits and
+    frames: the hit is order-independent (ties to the smaller triangle index, conservative box
+    tests), and split references cover their triangle."""
     monkeypatch.setenv("PGRT_BVH", builder)
     monkeypatch.setenv("PGRT_BVH_WIDTH", width)
+    monkeypatch.setenv("PGRT_SPLIT", split)
     try:
         gpu_ctx.set_scene(avenger_scene)
         info = gpu_ctx.bvh_info()
         assert info.width == int(width) and info.builder == (0 if builder == "lbvh" else 1)
+        if builder == "ploc" and float(split) > 0:
+            assert info.num_references > info.num_triangles
+        else:
+            assert info.num_references == info.num_triangles
         rays = _random_rays(avenger_scene, 20000, 11)
         hg = gpu_ctx.intersect(rays)
         ho = _oracle(avenger_scene).intersect(rays)
@@ -202,4 +209,5 @@ def test_bvh_layouts_bit_exact(gpu_ctx, avenger_scene, monkeypatch, builder, wid
     finally:
         monkeypatch.delenv("PGRT_BVH")
         monkeypatch.delenv("PGRT_BVH_WIDTH")
+        monkeypatch.delenv("PGRT_SPLIT")
         gpu_ctx.set_scene(avenger_scene)

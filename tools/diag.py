@@ -26,7 +26,7 @@ def main():
     info = ctx.bvh_info()
     print(json.dumps({"bvh": {"builder": ["lbvh", "ploc"][info.builder], "iters": info.build_iterations,
                               "tris": info.num_triangles, "nodes": info.num_nodes, "depth": info.max_depth,
-                              "width": info.width, "build_ms": round(info.build_ms, 3), "set_scene_s": round(time.time() - t, 3)}}))
+                              "width": info.width, "refs": info.num_references, "split": round(info.split_beta, 3), "build_ms": round(info.build_ms, 3), "set_scene_s": round(time.time() - t, 3)}}))
     ctx.set_camera(abi.default_camera(W, H))
     p = abi.make_params(spp_side=S, max_level=d, dof=dof,
                         jitter=abi.PGRT_JITTER_HASH if S > 1 or dof else abi.PGRT_JITTER_NONE)
@@ -35,6 +35,7 @@ def main():
     _, st = ctx.render(p)
     print(json.dumps({"stage_ms": {k: round(v, 4) for k, v in st.as_dict().items() if k.startswith("ms_")},
                       "rays": st.rays(), "trace_launches": st.trace_launches}))
+    lv_ms = [(dd["ms_trace"], dd["ms_shade"]) for dd in ctx.frame_diag()]
     p.profile = 2
     ctx.render(p)
     for L, dd in enumerate(ctx.frame_diag()):
@@ -44,7 +45,12 @@ def main():
         s = max(1, dd["shadow_rays"])
         print(f"L{L}: rays {dd['rays']:9d} visits/ray {dd['visits'] / r:7.1f} max {dd['max_visits']:6d} "
               f"tests/ray {dd['tests'] / r:6.1f} max {dd['max_tests']:5d} | shadow {dd['shadow_rays']:8d} "
-              f"visits/ray {dd['shadow_visits'] / s:6.1f} max {dd['shadow_max_visits']:5d}")
+              f"visits/ray {dd['shadow_visits'] / s:6.1f} max {dd['shadow_max_visits']:5d} | wave iters "
+              f"{dd['max_wave_iterations']:5d} ray {dd['max_ray_ticks'] / 100:6.1f} us spills {dd['stack_spills']:6d} "
+              f"stack {dd['max_stack']:3d} | longest: vis {dd['lr_visits']} tests {dd['lr_tests']} leaves "
+              f"{dd['lr_leaves']} node cyc/vis {dd['lr_node_cyc64'] * 64 / max(1, dd['lr_visits']):.0f} leaf cyc/leaf "
+              f"{dd['lr_leaf_cyc64'] * 64 / max(1, dd['lr_leaves']):.0f} load cyc/vis "
+              f"{dd['lr_load_cyc64'] * 64 / max(1, dd['lr_visits']):.0f} | trace {lv_ms[L][0] * 1e3:7.1f} us shade {lv_ms[L][1] * 1e3:6.1f} us")
 
 
 if __name__ == "__main__":
