@@ -12,7 +12,8 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libpgrt.so")
+# PGRT_LIB: development override (A/B of two builds of the library in one session)
+LIB_PATH = os.environ.get("PGRT_LIB") or os.path.join(PKG_DIR, "lib", "libpgrt.so")
 
 PGRT_OK = 0
 PGRT_MATERIAL_DIELECTRIC = 4

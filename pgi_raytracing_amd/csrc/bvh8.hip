@@ -168,12 +168,12 @@ __global__ __launch_bounds__(kB) void k_collapse(const BvhNode* __restrict__ bin
         }
         if (c[k].code >= 0) {
             imask |= 1u << s;
-            meta[s] = (unsigned char)((1u << 5) | (24u + s));
+            meta[s] = 0x80u;  // any non-zero value: slot in use
             next_tasks[task_base + ci] = make_int2(c[k].code, child_base + ci);
             ++ci;
         } else {
             const int first = leaf_first(c[k].code), cnt = leaf_count(c[k].code);
-            meta[s] = (unsigned char)((((1u << cnt) - 1u) << 5) | (unsigned)to);
+            meta[s] = (unsigned char)(0x80u | ((unsigned)(cnt - 1) << 5) | (unsigned)to);
             for (int j = 0; j < cnt; ++j) {
                 const int src = 3 * (first + j), dst = 3 * (tri_base + to + j);
                 tri_out[dst] = tri_in[src];

@@ -104,20 +104,25 @@ __host__ __device__ inline int leaf_count(int c) { return (int)(((unsigned)c >> 
 //   m  = (child_base, tri_base, meta[0..3], meta[4..7])
 //   qx = (lo.x[0..3], lo.x[4..7], hi.x[0..3], hi.x[4..7]) bytes, likewise qy, qz
 // imask bit s: slot s is an internal node, stored at child_base + popc(imask below s).
-// meta[s] of a leaf: unary triangle count << 5 | offset from tri_base (count <= 3, <= 24
-// triangles per node); 0 = empty slot.
+// meta[s] of a leaf: 0x80 | (count - 1) << 5 | offset from tri_base (count <= 4, <= 32
+// triangles per node, so a node's triangles fit one 32-bit mask); 0 = empty slot.
 struct Bvh8Node {
     float4 p;
     uint4 m;
     uint4 qx, qy, qz;
 };
-constexpr int kWideLeafMaxTris = 3;
+__host__ __device__ inline unsigned wide_leaf_bits(unsigned meta) {  // the leaf's triangle mask
+    return ((2u << ((meta >> 5) & 3u)) - 1u) << (meta & 31u);
+}
 
 struct SceneView {  // kernel-argument view of the device scene
     const float4* tri;     // 3 x float4 per sorted triangle: (v0, orig id bits) (e1) (e2)
     const BvhNode* nodes;
     int root;              // node index, or a leaf code for tiny scenes
-    const Bvh8Node* nodes8;  // 8-wide BVH (root = node 0) when wide != 0; tri is then in its order
+    const Bvh8Node* nodes8;  // 8-wide BVH (root = node 0)
+    const float4* tri8;      // triangles in 8-wide leaf order (same records as tri)
+    int depth8;              // 8-wide BVH depth
+    int group_max;           // queues of <= group_max rays: 8 lanes per ray over the 8-wide BVH
     int wide;
     int ntri;
     int depth;             // binary BVH depth (bounds the traversal stack)

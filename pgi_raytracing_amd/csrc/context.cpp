@@ -85,6 +85,7 @@ struct pgrt_ctx {
     DevBuf<float4> tri;
     DevBuf<BvhNode> nodes;
     DevBuf<Bvh8Node> nodes8;
+    DevBuf<float4> tri8;  // triangles in 8-wide leaf order
     DevBuf<float> attr;
     DevBuf<DevMaterial> mats;
     DevBuf<DevTexture> texd;
@@ -282,7 +283,7 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
     const char* es = getenv("PGRT_SPLIT");
     const float beta = es ? std::max(0.0f, std::min(4.0f, (float)atof(es))) : kDefaultSplitBeta;
     bo.builder = builder;
-    bo.leaf_max = width == 8 ? kWideLeafMaxTris : kLeafMaxTris;
+    bo.leaf_max = kLeafMaxTris;
     auto tb = std::chrono::steady_clock::now();
     if (builder == kBuilderPloc) {
         build_ploc_refs(pos.p, n, beta, pad, ext, ctx->tri, ctx->nodes, &bo, st);
@@ -297,19 +298,16 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
         build_lbvh(pos.p, n, ctx->tri.p, ctx->nodes.p, scratch.p, sort_tmp.p, tmp_bytes, pad, &bo, st);
     }
     const int m = bo.refs;
+    // the 8-wide layout is always built: the multi-lane kernel traces small (deep-level) queues
+    // over it; PGRT_BVH_WIDTH=8 also sends the big queues to the one-lane 8-wide kernel
     int wide_nodes = 0, wide_depth = 0;
-    if (width == 8) {
+    {
         ctx->nodes8.alloc((size_t)std::max(1, m));
-        DevBuf<float4> tri8;
-        tri8.alloc((size_t)m * 3);
+        ctx->tri8.alloc((size_t)m * 3);
         const float4 rlo = make_float4(lo[0] - pad, lo[1] - pad, lo[2] - pad, 0.0f);
         const float4 rhi = make_float4(hi[0] + pad, hi[1] + pad, hi[2] + pad, 0.0f);
-        build_bvh8(ctx->nodes.p, ctx->tri.p, bo.root, m, rlo, rhi, ctx->nodes8.p, tri8.p, &wide_nodes, &wide_depth,
-                   st);
-        std::swap(ctx->tri.p, tri8.p);  // traversal reads the triangles in wide-leaf order
-        std::swap(ctx->tri.n, tri8.n);
-    } else {
-        ctx->nodes8.release();
+        build_bvh8(ctx->nodes.p, ctx->tri.p, bo.root, m, rlo, rhi, ctx->nodes8.p, ctx->tri8.p, &wide_nodes,
+                   &wide_depth, st);
     }
     auto te = std::chrono::steady_clock::now();
     PGRT_REQUIRE(bo.max_depth <= kLdsStack + kGlobalStack - 2, PGRT_ERR_INVALID_ARGUMENT,
@@ -319,7 +317,11 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
     v.tri = ctx->tri.p;
     v.nodes = ctx->nodes.p;
     v.root = bo.root;
-    v.nodes8 = width == 8 ? ctx->nodes8.p : nullptr;
+    v.nodes8 = ctx->nodes8.p;
+    v.tri8 = ctx->tri8.p;
+    v.depth8 = wide_depth;
+    const char* eg = getenv("PGRT_GROUP_MAX");  // read per set_scene (tests compare settings)
+    v.group_max = eg ? atoi(eg) : kDefaultGroupMax;
     v.wide = width == 8 ? 1 : 0;
     v.ntri = n;
     v.depth = bo.max_depth;
@@ -345,7 +347,7 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
         bi.scene_lo[k] = lo[k];
         bi.scene_hi[k] = hi[k];
     }
-    bi.device_bytes = ctx->tri.bytes() + (width == 8 ? ctx->nodes8.bytes() : ctx->nodes.bytes()) +
+    bi.device_bytes = ctx->tri.bytes() + ctx->tri8.bytes() + ctx->nodes8.bytes() + ctx->nodes.bytes() +
                       ctx->attr.bytes() + ctx->texels.bytes();
     (void)t0;
 }

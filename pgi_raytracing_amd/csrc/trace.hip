@@ -341,7 +341,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8(SceneView s, const float
                     const unsigned meta = ((k < 4 ? m.z : m.w) >> (8 * j)) & 0xffu;
                     if (meta != 0u && t0 <= t1 * 1.000001f) {
                         if ((imask >> k) & 1u) nbits |= 1u << (24 + (k ^ oct));
-                        else tb |= (meta >> 5) << (meta & 31u);
+                        else tb |= wide_leaf_bits(meta);
                     }
                 }
                 gbase = m.x;
@@ -353,16 +353,16 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8(SceneView s, const float
             // ---- triangle phase: loads of the next triangle overlap the current test ----
             int k = (int)tbase + __ffs((int)tbits) - 1;
             tbits &= tbits - 1u;
-            float4 p0 = s.tri[3 * k], p1 = s.tri[3 * k + 1], p2 = s.tri[3 * k + 2];
+            float4 p0 = s.tri8[3 * k], p1 = s.tri8[3 * k + 1], p2 = s.tri8[3 * k + 2];
             for (;;) {
                 const float4 q0 = p0, q1 = p1, q2 = p2;
                 const bool more = tbits != 0u;
                 if (more) {
                     k = (int)tbase + __ffs((int)tbits) - 1;
                     tbits &= tbits - 1u;
-                    p0 = s.tri[3 * k];
-                    p1 = s.tri[3 * k + 1];
-                    p2 = s.tri[3 * k + 2];
+                    p0 = s.tri8[3 * k];
+                    p1 = s.tri8[3 * k + 1];
+                    p2 = s.tri8[3 * k + 2];
                 }
                 if (COUNT) ++rtest;
                 tri_test(q0, q1, q2, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v, best_prim);
@@ -385,6 +385,176 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8(SceneView s, const float
     }
 }
 
+
+// ---------------------------------------------------------------- 8 lanes per ray, 8-wide BVH
+//
+// For small queues (the deep Whitted levels: tens of thousands of rays on 1024 SIMDs) a level
+// takes as long as its slowest ray, and a one-lane traversal of that ray is a chain of ~100
+// dependent node fetches.  Here 8 lanes trace one ray: every lane tests one child box of the
+// current 8-wide node (lane k takes slot k ^ octant, so the group's ballot byte is already in
+// near-to-far order), and the triangles of the node's hit leaves are tested 8 at a time.  The
+// chain shrinks to one fetch per 8-wide node (about a third of the binary depth) plus one per
+// leaf batch.  All 8 lanes hold identical traversal state (ballot / DPP reductions), so the
+// group's control flow is uniform; the node-group stack lives in LDS, one per group.
+constexpr int kGroupStack = 32;  // node groups per ray: >= 8-wide depth + 1
+
+// reduce over the 8 lanes of a group: xor 1, xor 2 (quad DPP), then lane i <-> 7 - i (row
+// half mirror), so every lane ends with the group value
+#ifdef PGRT_GROUP_SHFL  // debugging aid: the same reductions through ds_bpermute
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __shfl_xor(v, CTRL == 0xB1 ? 1 : (CTRL == 0x4E ? 2 : 7), 64);
+}
+#else
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+}
+#endif
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(dpp_i<CTRL>(__float_as_int(v)));
+}
+constexpr int kDppXor1 = 0xB1;        // quad_perm [1,0,3,2]
+constexpr int kDppXor2 = 0x4E;        // quad_perm [2,3,0,1]
+constexpr int kDppHalfMirror = 0x141;  // row_half_mirror
+
+template <int CTRL>
+__device__ __forceinline__ void merge_hit_step(float& t, float& u, float& v, int& prim) {
+    const float ot = dpp_f<CTRL>(t), ou = dpp_f<CTRL>(u), ov = dpp_f<CTRL>(v);
+    const int op = dpp_i<CTRL>(prim);
+    if (op >= 0 && (prim < 0 || ot < t || (ot == t && op < prim))) {
+        t = ot;
+        u = ou;
+        v = ov;
+        prim = op;
+    }
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(kTraceBlock) void k_trace8g(SceneView s, const float4* __restrict__ ro,
+                                                         const float4* __restrict__ rd, float4* __restrict__ hits,
+                                                         const int* __restrict__ count_dev, int count_terms,
+                                                         int count_host, int cap,
+                                                         unsigned long long* __restrict__ counters) {
+    constexpr int kGroups = kTraceBlock / 8;
+    __shared__ uint2 gstk[kGroupStack][kGroups];
+    const int tid = threadIdx.x;
+    const int k = tid & 7;     // lane within the group
+    const int gib = tid >> 3;  // group within the block
+    const int n = ray_count(count_dev, count_terms, count_host, cap);
+    unsigned long long nvis = 0, ntest = 0, mvis = 0, mtest = 0, mclk = 0;
+    for (int i = blockIdx.x * kGroups + gib; i < n; i += gridDim.x * kGroups) {
+        long long t_start = 0;
+        if (COUNT) t_start = wall_clock64();
+        const float4 o4 = ro[i];
+        const float4 d4 = rd[i];
+        const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
+        const float dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
+        const float sdx = fabsf(dx) < 1e-30f ? copysignf(1e-30f, dx) : dx;
+        const float sdy = fabsf(dy) < 1e-30f ? copysignf(1e-30f, dy) : dy;
+        const float sdz = fabsf(dz) < 1e-30f ? copysignf(1e-30f, dz) : dz;
+        const float idx = __builtin_amdgcn_rcpf(sdx), idy = __builtin_amdgcn_rcpf(sdy),
+                    idz = __builtin_amdgcn_rcpf(sdz);
+        const bool px = idx >= 0.0f, py = idy >= 0.0f, pz = idz >= 0.0f;
+        const unsigned oct = (dx > 0.0f ? 1u : 0u) | (dy > 0.0f ? 2u : 0u) | (dz > 0.0f ? 4u : 0u);
+        const unsigned my_slot = (unsigned)k ^ oct;
+        const int j = (int)(my_slot & 3u);
+        const bool hi_half = my_slot >= 4u;
+        float best_t = tfar, best_u = 0.0f, best_v = 0.0f;
+        int best_prim = -1;
+        unsigned rvis = 0, rtest = 0;
+        int sp = 0;
+        unsigned gbase = 0, gbits = (1u << (24 + oct)) | 1u;  // the root: slot 0 of a virtual parent
+        if (!(tfar >= 0.0f)) gbits = 0;
+        unsigned tbase = 0, tbits = 0;
+        for (;;) {
+            while (tbits == 0u) {  // ---- node phase (group-uniform) ----
+                if (gbits <= 0x00ffffffu) {
+                    if (sp == 0) break;
+                    --sp;
+                    const uint2 g = gstk[sp][gib];
+                    gbase = g.x;
+                    gbits = g.y;
+                }
+                const int pb = 31 - __clz((int)gbits);
+                gbits &= ~(1u << pb);
+                const unsigned slot = (unsigned)(pb - 24) ^ oct;
+                const int child = (int)gbase + __popc(gbits & 0xffu & ((1u << slot) - 1u));
+                if (gbits > 0x00ffffffu) {
+                    gstk[sp][gib] = make_uint2(gbase, gbits);  // same value from all 8 lanes
+                    ++sp;
+                }
+                const Bvh8Node* nd = s.nodes8 + child;
+                const float4 p = nd->p;
+                const uint4 m = nd->m, qx = nd->qx, qy = nd->qy, qz = nd->qz;
+                if (COUNT) ++rvis;
+                const unsigned eb = __float_as_uint(p.w);
+                const unsigned imask = eb >> 24;
+                const float ax = __uint_as_float((eb & 0xffu) << 23) * idx;
+                const float ay = __uint_as_float(((eb >> 8) & 0xffu) << 23) * idy;
+                const float az = __uint_as_float(((eb >> 16) & 0xffu) << 23) * idz;
+                const float bx = (p.x - ox) * idx, by = (p.y - oy) * idy, bz = (p.z - oz) * idz;
+                // this lane's slot: lo / hi bytes per axis, near / far by the ray's sign
+                const unsigned lxw = hi_half ? qx.y : qx.x, hxw = hi_half ? qx.w : qx.z;
+                const unsigned lyw = hi_half ? qy.y : qy.x, hyw = hi_half ? qy.w : qy.z;
+                const unsigned lzw = hi_half ? qz.y : qz.x, hzw = hi_half ? qz.w : qz.z;
+                const float lx = qb(lxw, j), hx = qb(hxw, j), ly = qb(lyw, j), hy = qb(hyw, j);
+                const float lz = qb(lzw, j), hz = qb(hzw, j);
+                const float t0 = fmaxf(fmaxf(fmaf(px ? lx : hx, ax, bx), fmaf(py ? ly : hy, ay, by)),
+                                       fmaxf(fmaf(pz ? lz : hz, az, bz), 0.0f));
+                const float t1 = fminf(fminf(fmaf(px ? hx : lx, ax, bx), fmaf(py ? hy : ly, ay, by)),
+                                       fminf(fmaf(pz ? hz : lz, az, bz), best_t));
+                const unsigned meta = ((hi_half ? m.w : m.z) >> (8 * j)) & 0xffu;
+                const bool hit = meta != 0u && t0 <= t1 * 1.000001f;
+                const bool inner = ((imask >> my_slot) & 1u) != 0u;
+                int tb = (hit && !inner) ? (int)wide_leaf_bits(meta) : 0;
+                const unsigned long long bal = __ballot(hit && inner);
+                const unsigned nb = (unsigned)(bal >> (__lane_id() & ~7)) & 0xffu;  // bit k = slot k ^ oct
+                tb |= dpp_i<kDppXor1>(tb);
+                tb |= dpp_i<kDppXor2>(tb);
+                tb |= dpp_i<kDppHalfMirror>(tb);
+                gbase = m.x;
+                gbits = (nb << 24) | imask;
+                tbase = m.y;
+                tbits = (unsigned)tb;
+            }
+            if (tbits == 0u) break;
+            // ---- triangle phase: 8 triangles per round, then the group's closest hit ----
+            while (tbits != 0u) {
+                unsigned mine = tbits;
+                for (int q = 0; q < k; ++q) mine &= mine - 1u;  // this lane's set bit
+                if (mine != 0u) {
+                    const int tr = (int)tbase + __ffs((int)mine) - 1;
+                    const float4 q0 = s.tri8[3 * tr], q1 = s.tri8[3 * tr + 1], q2 = s.tri8[3 * tr + 2];
+                    tri_test(q0, q1, q2, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v, best_prim);
+                }
+                if (COUNT) rtest += (unsigned)min(__popc(tbits), 8);
+                for (int q = 0; q < 8; ++q) tbits &= tbits - 1u;
+                merge_hit_step<kDppXor1>(best_t, best_u, best_v, best_prim);
+                merge_hit_step<kDppXor2>(best_t, best_u, best_v, best_prim);
+                merge_hit_step<kDppHalfMirror>(best_t, best_u, best_v, best_prim);
+            }
+        }
+        if (k == 0) hits[i] = make_float4(best_t, best_u, best_v, __int_as_float(best_prim));
+        if (COUNT && k == 0) {
+            const unsigned long long dt = (unsigned long long)(wall_clock64() - t_start);
+            mclk = dt > mclk ? dt : mclk;
+            nvis += rvis;
+            ntest += rtest;
+            mvis = rvis > mvis ? rvis : mvis;
+            mtest = rtest > mtest ? rtest : mtest;
+        }
+    }
+    if (COUNT && k == 0) {
+        atomicAdd(&counters[0], nvis);
+        atomicAdd(&counters[1], ntest);
+        atomicMax(&counters[2], mvis);
+        atomicMax(&counters[3], mtest);
+        atomicMax(&counters[5], mclk);
+    }
+}
+
 void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4* hits, const int* count_dev,
                   int count_host, int max_count, int* fetch, int* gstack, int gstack_threads,
                   unsigned long long* counters, bool count, hipStream_t stream, int expect, int count_terms) {
@@ -400,6 +570,23 @@ void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4
             hipLaunchKernelGGL((k_trace8<false>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
                                count_dev, count_terms, count_host, max_count, gstack, counters);
         return;
+    }
+    // small queues: 8 lanes per ray over the 8-wide BVH (PGRT_GROUP_MAX: largest queue, rays)
+    const int group_max = s.group_max;
+    {
+        const int exg = expect > 0 && expect < max_count ? expect : max_count;
+        if (exg <= group_max && s.depth8 + 1 <= kGroupStack) {
+            constexpr int kGroups = kTraceBlock / 8;
+            int grid = ceil_div(exg, kGroups);
+            if (grid > 16384) grid = 16384;
+            if (count)
+                hipLaunchKernelGGL((k_trace8g<true>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
+                                   count_dev, count_terms, count_host, max_count, counters);
+            else
+                hipLaunchKernelGGL((k_trace8g<false>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
+                                   count_dev, count_terms, count_host, max_count, counters);
+            return;
+        }
     }
     // rays per wave: full waves for big queues; small (tail) queues may spread thinner
     static const int tail_rpw = [] {

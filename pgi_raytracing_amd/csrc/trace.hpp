@@ -89,9 +89,11 @@ void launch_unpack_tiles(const float* gathered, float* rgba, int width, int heig
 constexpr int kBuilderLbvh = 0;  // Karras 2012 over 63-bit Morton codes
 constexpr int kBuilderPloc = 1;  // PLOC clustering over the same Morton order + SAH collapse
 constexpr float kDefaultSplitBeta = 0.0f;  // PGRT_SPLIT default (extra references / triangles)
+constexpr int kDefaultGroupMax = 400000;   // PGRT_GROUP_MAX default: queues up to this many rays use
+                                           // the 8-lanes-per-ray kernel (r1 A/B: tail levels -45 %)
 struct BuildOut {
     int builder;   // in: kBuilder*
-    int leaf_max;  // in: triangles per binary leaf (<= kLeafMaxTris; kWideLeafMaxTris for BVH8)
+    int leaf_max;  // in: triangles per binary leaf (<= kLeafMaxTris)
     int root;
     int num_nodes;
     int max_depth;

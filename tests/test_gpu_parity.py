@@ -177,15 +177,18 @@ def test_distributed_world1_equals_render(gpu_ctx, avenger_scene):
     assert (np.nan_to_num(a, nan=5) == np.nan_to_num(b, nan=5)).all()
 
 
-@pytest.mark.parametrize("builder,width,split", [("lbvh", "2", "0"), ("ploc", "8", "0"), ("lbvh", "8", "0"),
-                                                 ("ploc", "2", "0"), ("ploc", "2", "1.0"), ("ploc", "8", "0.5")])
-def test_bvh_layouts_bit_exact(gpu_ctx, avenger_scene, monkeypatch, builder, width, split):
+@pytest.mark.parametrize("builder,width,split,group", [
+    ("lbvh", "2", "0", "0"), ("ploc", "8", "0", "0"), ("lbvh", "8", "0", "0"), ("ploc", "2", "0", "0"),
+    ("ploc", "2", "1.0", "0"), ("ploc", "8", "0.5", "0"),
+    ("ploc", "2", "0", "1000000000"), ("lbvh", "2", "0.5", "1000000000"), ("ploc", "2", "0.5", "1000000000")])
+def test_bvh_layouts_bit_exact(gpu_ctx, avenger_scene, monkeypatch, builder, width, split, group):
     """Every BVH builder / traversal layout / split budget gives the same closest hits and
     frames: the hit is order-independent (ties to the smaller triangle index, conservative box
     tests), and split references cover their triangle."""
     monkeypatch.setenv("PGRT_BVH", builder)
     monkeypatch.setenv("PGRT_BVH_WIDTH", width)
     monkeypatch.setenv("PGRT_SPLIT", split)
+    monkeypatch.setenv("PGRT_GROUP_MAX", group)  # 8 lanes per ray over the 8-wide BVH for queues <= group
     try:
         gpu_ctx.set_scene(avenger_scene)
         info = gpu_ctx.bvh_info()
@@ -210,4 +213,5 @@ def test_bvh_layouts_bit_exact(gpu_ctx, avenger_scene, monkeypatch, builder, wid
         monkeypatch.delenv("PGRT_BVH")
         monkeypatch.delenv("PGRT_BVH_WIDTH")
         monkeypatch.delenv("PGRT_SPLIT")
+        monkeypatch.delenv("PGRT_GROUP_MAX")
         gpu_ctx.set_scene(avenger_scene)
