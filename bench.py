@@ -24,9 +24,10 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 METRIC = "Mrays/sec + ms/frame, avenger 1920x1080 Whitted d=5, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# algorithmic bytes: ray in 32 B + hit out 16 B per ray, 64 B per BVH node
-# visited, 48 B per triangle tested (our triangle record: v0|id, e1, e2)
-RAY_BYTES, NODE_BYTES, TRI_BYTES = 48, 64, 48
+# algorithmic bytes: ray in 32 B + hit out 16 B per ray, 64 B per binary BVH
+# node visited, 80 B per 8-wide node visited (small queues), 48 B per triangle tested (our
+# triangle record: v0|id, e1, e2)
+RAY_BYTES, NODE_BYTES, WIDE_NODE_BYTES, TRI_BYTES = 48, 64, 80, 48
 
 
 def parse():
@@ -124,7 +125,8 @@ def main():
         p1.profile = 2
         s2 = frame(p1)
         frame_rays = s2.rays()
-        alg_bytes = RAY_BYTES * frame_rays + NODE_BYTES * s2.node_visits + TRI_BYTES * s2.tri_tests
+        alg_bytes = (RAY_BYTES * frame_rays + NODE_BYTES * s2.node_visits + WIDE_NODE_BYTES * s2.wide_node_visits
+                     + TRI_BYTES * s2.tri_tests)
         avg_launch_ms = ms_trace / max(1, launches)
         per_launch_bytes = alg_bytes / max(1, launches / reps)
         achieved = per_launch_bytes / (avg_launch_ms * 1e-3) / 1e9
@@ -135,11 +137,12 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None,
-            "kernel": "k_trace<false> (closest hit)",
+            "kernel": "closest hit: k_trace (binary BVH, big queues) + k_trace8g (8 lanes/ray, small queues)",
             "avg_launch_ms": round(avg_launch_ms, 4),
             "launches_per_frame": launches // reps,
             "trace_ms_per_frame": round(ms_trace / reps, 4),
             "node_visits_per_ray": round(s2.node_visits / max(1, frame_rays), 2),
+            "wide_node_visits_per_ray": round(s2.wide_node_visits / max(1, frame_rays), 2),
             "tri_tests_per_ray": round(s2.tri_tests / max(1, frame_rays), 2),
             "bytes_per_ray": round(alg_bytes / max(1, frame_rays), 1),
         }

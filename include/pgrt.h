@@ -139,6 +139,8 @@ typedef struct pgrt_stats {
     int trace_launches;              /* launches of the closest-hit kernel in ms_trace */
     int levels;                      /* trace levels executed */
     int overflow_retries;            /* queue re-sizings this call */
+    uint64_t wide_node_visits;       /* profile == 2: 8-wide (80-B) node visits; node_visits
+                                        counts the binary (64-B) ones */
 } pgrt_stats;
 
 typedef struct pgrt_bvh_info {
@@ -229,6 +231,7 @@ typedef struct pgrt_level_diag {
     uint64_t max_stack;           /* deepest traversal stack of one ray */
     uint64_t longest_ray[6];      /* the longest ray: visits, tests, leaf rounds, node-phase,
                                      leaf-phase and node-load shader cycles / 64 */
+    uint64_t wide_visits;         /* the part of visits that were 8-wide nodes */
     double ms_trace, ms_shade;    /* this level's launches (profile >= 1 on the call; summed
                                      over sample batches) */
 } pgrt_level_diag;

@@ -127,6 +127,7 @@ class Stats(C.Structure):
         ("trace_launches", C.c_int),
         ("levels", C.c_int),
         ("overflow_retries", C.c_int),
+        ("wide_node_visits", C.c_uint64),
     ]
 
     def rays(self) -> int:
@@ -141,7 +142,7 @@ class LevelDiag(C.Structure):
                                           "shadow_visits", "shadow_tests", "shadow_max_visits", "shadow_max_tests",
                                           "max_wave_iterations", "max_ray_ticks", "stack_spills", "max_stack",
                                           "lr_visits", "lr_tests", "lr_leaves", "lr_node_cyc64", "lr_leaf_cyc64",
-                                          "lr_load_cyc64")] + [("ms_trace", C.c_double), ("ms_shade", C.c_double)]
+                                          "lr_load_cyc64", "wide_visits")] + [("ms_trace", C.c_double), ("ms_shade", C.c_double)]
 
 
 class BvhInfo(C.Structure):

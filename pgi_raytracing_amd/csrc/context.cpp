@@ -412,7 +412,7 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
     ctx->accum.alloc((size_t)npix);
     ctx->timer.on = p->profile > 0;
     double ms[CAT_N] = {0};
-    uint64_t rays_shadow = 0, rays_reflect = 0, rays_refract = 0, trav_nodes = 0, trav_tests = 0;
+    uint64_t rays_shadow = 0, rays_reflect = 0, rays_refract = 0, trav_nodes = 0, trav_tests = 0, trav_wide = 0;
     int retries = 0, trace_launches = 0;
     FrameParams fp{};
     fp.spp_side = p->spp_side;
@@ -464,7 +464,8 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
                 const int sid = ctx->timer.begin(s, CAT_SHADOW);
                 launch_trace(ctx->view, sq.ro, sq.rd, sq.hit, &fcd->shadow_count[0], 0, sq.cap,
                              &fcd->fetch[kMaxLevels], ctx->gstack.p, kTraceGridThreads, fcd->trav[kMaxLevels],
-                             p->profile >= 2, s, ctx->expect_shadow_total, levels);
+                             p->profile >= 2, s, ctx->expect_shadow_total, levels,
+                             false);  // shadow rays (from the light along H) mostly miss the root
                 ctx->timer.end(s, sid);
                 ctx->timer.end(s, id);
                 ++trace_launches;
@@ -547,6 +548,7 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
                 }
             }
             for (int k = 0; k < 2 * kMaxLevels; ++k) {
+                trav_wide += h.trav[k][14];
                 trav_nodes += h.trav[k][0];
                 trav_tests += h.trav[k][1];
             }
@@ -564,6 +566,7 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
         st->rays_reflect = rays_reflect;
         st->rays_refract = rays_refract;
         st->node_visits = trav_nodes;
+        st->wide_node_visits = trav_wide;
         st->tri_tests = trav_tests;
         st->ms_raygen = ms[CAT_RAYGEN];
         st->ms_trace = ms[CAT_TRACE];
@@ -882,7 +885,8 @@ int pgrt_frame_diag(const pgrt_ctx* ctx, pgrt_level_diag* out, int max_levels) {
             pgrt_level_diag& d = out[L];
             d.rays += (uint64_t)h.count[L];
             d.shadow_rays += (uint64_t)h.shadow_count[L];
-            d.visits += h.trav[L][0];
+            d.visits += h.trav[L][0] + h.trav[L][14];
+            d.wide_visits += h.trav[L][14];
             d.tests += h.trav[L][1];
             d.max_visits = std::max<uint64_t>(d.max_visits, h.trav[L][2]);
             d.max_tests = std::max<uint64_t>(d.max_tests, h.trav[L][3]);

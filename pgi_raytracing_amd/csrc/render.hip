@@ -24,20 +24,20 @@ static int grid_for(int max_count, int expect) {
     return g < 1 ? 1 : (g > 4096 ? 4096 : g);
 }
 
-// wave-level exclusive prefix allocation: every lane of the wave must call it (k = 0 allowed)
-__device__ __forceinline__ int wave_alloc(int* counter, int k) {
-    const int lane = __lane_id();
-    int x = k;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
+// Wave-level slot allocation for small per-lane counts (children <= 2, shadow rays <= lights):
+// the exclusive prefix is sum_b 2^b * (lanes below with bit b set), one ballot + mbcnt per bit,
+// and lane 0 issues the queue atomics together (one round trip).  Every lane of the wave must
+// be active (k_shade keeps whole waves in its loop).
+__device__ __forceinline__ void wave_prefix_small(int x, int bits, int& prefix, int& total) {
+    prefix = 0;
+    total = 0;
+    for (int b = 0; b < bits; ++b) {
+        const unsigned long long m = __ballot((x >> b) & 1);
+        const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+        prefix += below << b;
+        total += __popcll(m) << b;
     }
-    const int total = __shfl(x, 63, 64);
-    int base = 0;
-    if (lane == 63 && total > 0) base = atomicAdd(counter, total);
-    base = __shfl(base, 63, 64);
-    return base + x - k;
 }
 
 // ------------------------------------------------------------------ ray generation
@@ -129,6 +129,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(SceneView s, FrameParams fp, i
     // one shadow queue for the whole batch: level L's rays follow those of levels < L (final by now)
     int sq_base = 0;
     for (int l = 0; l < level; ++l) sq_base += fc->shadow_count[l];
+    const int sbits = s.nlight > 0 ? 32 - __clz(s.nlight) : 0;  // bits of a lane's shadow-ray count
     for (int base_i = blockIdx.x * kBlock; base_i < n; base_i += gridDim.x * kBlock) {
         const int i = base_i + tid;
         const bool active = i < n;
@@ -225,10 +226,19 @@ __global__ __launch_bounds__(kBlock) void k_shade(SceneView s, FrameParams fp, i
             }
         }
         // ---- queue allocation (wave-uniform control flow) ----
-        const int cbase = wave_alloc(&fc->count[level + 1 < kMaxLevels ? level + 1 : level], nchild);
-        const int sbase = sq_base + wave_alloc(&fc->shadow_count[level], nshadow);
-        const int nref = wave_alloc(&fc->refract[level + 1 < kMaxLevels ? level + 1 : level], nchild == 2 ? 1 : 0);
-        (void)nref;
+        int cpre, ctot, spre, stot;
+        wave_prefix_small(nchild, 2, cpre, ctot);
+        wave_prefix_small(nshadow, sbits, spre, stot);
+        const int rtot = (int)__popcll(__ballot(nchild == 2));
+        int cb = 0, sb = 0;
+        if (__lane_id() == 0) {
+            const int ln = level + 1 < kMaxLevels ? level + 1 : level;
+            if (ctot) cb = atomicAdd(&fc->count[ln], ctot);
+            if (stot) sb = atomicAdd(&fc->shadow_count[level], stot);
+            if (rtot) atomicAdd(&fc->refract[ln], rtot);  // statistics only: no return
+        }
+        const int cbase = __builtin_amdgcn_readfirstlane(cb) + cpre;
+        const int sbase = sq_base + __builtin_amdgcn_readfirstlane(sb) + spre;
         if (!active) continue;
         int4 link = make_int4(-1, -1, -1, 0);
         if (kind == 1) {

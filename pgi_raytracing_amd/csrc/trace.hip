@@ -378,7 +378,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8(SceneView s, const float
         }
     }
     if (COUNT) {
-        atomicAdd(&counters[0], nvis);
+        atomicAdd(&counters[14], nvis);  // 80-B wide-node visits
         atomicAdd(&counters[1], ntest);
         atomicMax(&counters[2], mvis);
         atomicMax(&counters[3], mtest);
@@ -547,7 +547,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8g(SceneView s, const floa
         }
     }
     if (COUNT && k == 0) {
-        atomicAdd(&counters[0], nvis);
+        atomicAdd(&counters[14], nvis);  // 80-B wide-node visits
         atomicAdd(&counters[1], ntest);
         atomicMax(&counters[2], mvis);
         atomicMax(&counters[3], mtest);
@@ -557,7 +557,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8g(SceneView s, const floa
 
 void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4* hits, const int* count_dev,
                   int count_host, int max_count, int* fetch, int* gstack, int gstack_threads,
-                  unsigned long long* counters, bool count, hipStream_t stream, int expect, int count_terms) {
+                  unsigned long long* counters, bool count, hipStream_t stream, int expect, int count_terms,
+                  bool allow_group) {
     if (max_count <= 0) return;
     static const bool force_spill = getenv("PGRT_FORCE_SPILL") != nullptr;  // A/B of the stack layout
     if (s.wide) {
@@ -575,7 +576,7 @@ void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4
     const int group_max = s.group_max;
     {
         const int exg = expect > 0 && expect < max_count ? expect : max_count;
-        if (exg <= group_max && s.depth8 + 1 <= kGroupStack) {
+        if (allow_group && exg <= group_max && s.depth8 + 1 <= kGroupStack) {
             constexpr int kGroups = kTraceBlock / 8;
             int grid = ceil_div(exg, kGroups);
             if (grid > 16384) grid = 16384;
