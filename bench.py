@@ -3,7 +3,8 @@
 1920x1080 Whitted d=5, 1/2/4/8 GPU).
 
 One step = one frame of BASELINE config C2 (avenger-proxy, 1920x1080, 1 spp pinhole, Whitted
-depth 5, spherical env map) rendered into an HBM-resident framebuffer.  N > 1: one process
+depth 5, spherical env map) rendered into an HBM-resident framebuffer (--config C3/C4/C5 select
+the other BASELINE configs for the records in DESIGN.md).  N > 1: one process
 per GPU (torch.distributed launcher env), 64x64 image tiles dealt round-robin to ranks, one
 ncclGather (RCCL over xGMI) to rank 0 and an unpack kernel there -- the total frame is fixed
 (strong scaling).  Rays = every closest-hit query (primary + shadow + reflect + refract).
@@ -30,20 +31,36 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 RAY_BYTES, NODE_BYTES, WIDE_NODE_BYTES, TRI_BYTES = 48, 64, 80, 48
 
 
+# BASELINE.json configs (SURVEY.md §8d "Concrete inputs"); C2 is the headline bench line, the
+# others are measured with --config and recorded in DESIGN.md / profiles/
+CONFIGS = {
+    "C2": dict(width=1920, height=1080, max_level=5, spp_side=1, dof=0, scene="avenger"),
+    "C3": dict(width=1920, height=1080, max_level=5, spp_side=8, dof=1, scene="avenger"),
+    "C4": dict(width=3840, height=2160, max_level=5, spp_side=8, dof=1, scene="avenger"),
+    "C5": dict(width=4096, height=4096, max_level=8, spp_side=1, dof=0, scene="random1m"),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--max-level", type=int, default=5)
-    ap.add_argument("--spp-side", type=int, default=1)
-    ap.add_argument("--dof", type=int, default=0)
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--max-level", type=int, default=None)
+    ap.add_argument("--spp-side", type=int, default=None)
+    ap.add_argument("--dof", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    return ap.parse_args()
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (multi-thread leg)")
+    a = ap.parse_args()
+    for k, v in CONFIGS[a.config].items():
+        if getattr(a, k, None) is None:
+            setattr(a, k, v)
+    return a
 
 
 def main():
@@ -60,13 +77,18 @@ def main():
     from pgi_raytracing_amd import abi
     from pgi_raytracing_amd.raytracer import Context, load_obj
 
-    if rank == 0 and not os.path.exists(scenes.AVENGER_OBJ):
-        scenes.write_avenger_proxy()
-    if dist:
-        dist.barrier()
-    scene = load_obj(scenes.AVENGER_OBJ)
-    scene.set_environment(os.path.join(ROOT, "assets", "spherical_map_windows.jpg"))
-    cam = abi.default_camera(args.width, args.height)
+    env = os.path.join(ROOT, "assets", "spherical_map_windows.jpg")
+    if args.scene == "avenger":
+        if rank == 0 and not os.path.exists(scenes.AVENGER_OBJ):
+            scenes.write_avenger_proxy()
+        if dist:
+            dist.barrier()
+        scene = load_obj(scenes.AVENGER_OBJ)
+        scene.set_environment(env)
+        cam = abi.default_camera(args.width, args.height)
+    else:  # C5: 10^6 random triangles, camera from (-140,-175,80) at the origin
+        scene = scenes.random_scene(1_000_000, 42, env)
+        cam = abi.make_camera(args.width, args.height, abi.deg2rad(42.185), (-140.0, -175.0, 80.0), (0.0, 0.0, 0.0))
     params = abi.make_params(spp_side=args.spp_side, max_level=args.max_level, dof=args.dof,
                              jitter=abi.PGRT_JITTER_HASH if (args.spp_side > 1 or args.dof) else abi.PGRT_JITTER_NONE)
     ctx = Context(local_rank)
@@ -147,26 +169,51 @@ def main():
             "bytes_per_ray": round(alg_bytes / max(1, frame_rays), 1),
         }
         tf = os.path.join(ROOT, "profiles", "traffic_c2.json")
-        if os.path.exists(tf):
+        if args.config == "C2" and os.path.exists(tf):
             try:
                 roof["traffic"] = json.load(open(tf)).get("bytes_per_launch")
             except Exception:  # noqa: BLE001
                 pass
 
+    host_fb = None
+    if world == 1 and not args.no_roofline:
+        # PCIe-inclusive rate: the same frame through pgrt_render into a host
+        # framebuffer (device -> host copy of W*H*16 B per frame); never the headline value
+        for _ in range(2):
+            ctx.render(params)
+        t1 = time.perf_counter()
+        nh = max(3, args.steps // 2)
+        for _ in range(nh):
+            ctx.render(params)
+        host_fb = round((time.perf_counter() - t1) / nh * 1e3, 4)
+
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.scene == "avenger":
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import pyoracle  # cpu_baseline leg only: the CPU restatement timed on the host cores
 
         osc = pyoracle.OracleScene(scene)
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        step = 4  # every 4th row of the same frame: ~1/4 of the C2 work
-        t1 = time.perf_counter()
-        _, sc = osc.render(cam, params, row_step=step, threads=threads)
-        dt = time.perf_counter() - t1
-        cpu = {"value": round(sc.rays() / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-               "sample": f"every {step}th row of the C2 frame ({sc.rays()} rays, {dt:.2f} s), "
-                         f"oracle/ CPU restatement with its own SAH BVH, OpenMP"}
+
+        def timed(nthreads, budget_s):  # whole C2 frames, repeated until the budget is spent
+            frames = rays_c = 0
+            t1 = time.perf_counter()
+            while True:
+                _, sc = osc.render(cam, params, row_step=1, threads=nthreads)
+                rays_c += sc.rays()
+                frames += 1
+                dt_c = time.perf_counter() - t1
+                if dt_c >= budget_s:
+                    return rays_c / dt_c / 1e6, frames, rays_c, dt_c
+
+        v_mt, f_mt, r_mt, t_mt = timed(threads, args.cpu_seconds)
+        v_st, f_st, r_st, t_st = timed(1, args.cpu_seconds / 2)
+        cpu = {"value": round(v_mt, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+               "sample": f"{f_mt} whole C2 frames ({r_mt} rays, {t_mt:.1f} s) on {threads} host threads "
+                         f"(OpenMP over rows); oracle/ CPU restatement with its own SAH BVH",
+               "single_thread_value": round(v_st, 3),
+               "single_thread_sample": f"{f_st} frames ({r_st} rays, {t_st:.1f} s), 1 thread (the reference's "
+                                       f"single Producer thread)"}
 
     if rank == 0:
         out = {
@@ -181,9 +228,11 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: avenger-proxy OBJ (reference OBJ absent) + spherical_map_windows.jpg",
+            "data": ("synthetic: avenger-proxy OBJ (reference OBJ absent) + spherical_map_windows.jpg"
+                     if args.scene == "avenger" else "synthetic: 10^6 random triangles (seed 42) + env map"),
             "config": {
-                "workload": f"C2 avenger-proxy {args.width}x{args.height} Whitted d={args.max_level} + env map, "
+                "workload": f"{args.config} {'avenger-proxy' if args.scene == 'avenger' else '1M random triangles'} "
+                            f"{args.width}x{args.height} Whitted d={args.max_level} + env map, "
                             f"{args.spp_side ** 2} spp {'DoF' if args.dof else 'pinhole'}",
                 "triangles": bvh.num_triangles,
                 "rays_per_frame": int(total_rays / args.steps),
@@ -191,6 +240,7 @@ def main():
                 else "1 GPU",
             },
             "roofline": roof,
+            "host_framebuffer_ms_per_step": host_fb,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -82,6 +82,11 @@ __device__ __forceinline__ int ray_count(const int* count_dev, int count_terms, 
 // SPILL: stack entries past kLdsStack go to a per-thread global region.  Without SPILL the
 // whole stack is in LDS (dynamic size = BVH depth + 2 entries per lane, chosen at launch):
 // every push/pop is a ds_write/ds_read instead of a flat access that must wait on vmcnt too.
+// the rare spill accesses as out-of-line calls, so the LDS push/pop stays a plain ds access
+// (a select between an LDS and a global pointer would become a flat access on every pop)
+__device__ __noinline__ void spill_store(int* p, int v) { *p = v; }
+__device__ __noinline__ int spill_load(const int* p) { return *p; }
+
 template <bool COUNT, bool SPILL>
 __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4* __restrict__ ro,
                                                        const float4* __restrict__ rd,
@@ -99,13 +104,20 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
     do {                                                              \
         ++sp;                                                         \
         if (COUNT && sp > msp) msp = sp;                              \
-        if (!SPILL || sp < kLdsStack) lstack[sp * kTraceBlock + tid] = (v); \
+        if (!SPILL || __builtin_expect(sp < kLdsStack, 1)) lstack[sp * kTraceBlock + tid] = (v); \
         else {                                                        \
             if (COUNT) ++nspill;                                      \
-            gst[sp - kLdsStack] = (v);                                \
+            spill_store(gst + (sp - kLdsStack), (v));                 \
         }                                                             \
     } while (0)
-#define POP() ((!SPILL || sp < kLdsStack) ? lstack[(sp--) * kTraceBlock + tid] : gst[(sp--) - kLdsStack])
+#define POP() pop_entry(sp)
+    auto pop_entry = [&](int& spr) -> int {
+        int v;
+        if (!SPILL || __builtin_expect(spr < kLdsStack, 1)) v = lstack[spr * kTraceBlock + tid];
+        else v = spill_load(gst + (spr - kLdsStack));
+        --spr;
+        return v;
+    };
     // rpw rays per wave (lanes >= rpw idle): small queues spread over more waves
     if (lane >= rpw) return;
     const int wstride = gridDim.x * (kTraceBlock / 64) * rpw;

@@ -26,4 +26,5 @@ run trace 400 --kernel-trace --stats
 run pmc_fetch 400 --kernel-trace --pmc FETCH_SIZE
 run pmc_write 400 --kernel-trace --pmc WRITE_SIZE
 run pmc_l2 400 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum
+python3 tools/traffic.py "$OUT" "$OUT/traffic_c2.json" "$TAG"
 find "$OUT" -name "*.csv" | head -20

@@ -415,6 +415,20 @@ def random_triangles(n: int = 1_000_000, seed: int = 42, n_materials: int = 100)
             np.ascontiguousarray(uv.reshape(-1)), mat_ids, mats)
 
 
+def random_scene(n: int = 1_000_000, seed: int = 42, env_map: str | None = None):
+    """C5 as a pgi_raytracing_amd Scene: the soup above, the reference light, optional env map."""
+    from pgi_raytracing_amd.scene import LightData, MaterialData, Scene
+
+    pos, nrm, uv, mids, mats = random_triangles(n, seed)
+    md = [MaterialData(name=f"m{i}", diffuse=tuple(float(x) for x in m["diffuse"]),
+                       specular=tuple(float(x) for x in m["specular"]), shininess=m["shininess"], ior=m["ior"],
+                       type=m["type"]) for i, m in enumerate(mats)]
+    sc = Scene(pos, nrm, uv, mids, md, [], -1, [LightData()])
+    if env_map:
+        sc.set_environment(env_map)
+    return sc
+
+
 if __name__ == "__main__":
     print(write_avenger_proxy())
     print(write_geosphere())
