@@ -16,6 +16,8 @@
 // through is tested with the same arithmetic as the oracle, and ties in t go to the smaller
 // original triangle index -- so the hit record is bit-identical to the CPU restatement.
 #include "shade_ops.hpp"
+#include <string>
+
 #include "trace.hpp"
 
 namespace pgrt {
@@ -443,22 +445,64 @@ __device__ __forceinline__ void merge_hit_step(float& t, float& u, float& v, int
     }
 }
 
-template <bool COUNT>
+// group reductions: G = 8 uses xor 1, xor 2 and the half-row mirror; G = 4 the two quad steps
+template <int G>
+__device__ __forceinline__ int group_or(int v) {
+    v |= dpp_i<kDppXor1>(v);
+    v |= dpp_i<kDppXor2>(v);
+    if constexpr (G == 8) v |= dpp_i<kDppHalfMirror>(v);
+    return v;
+}
+template <int G>
+__device__ __forceinline__ void group_merge_hit(float& t, float& u, float& v, int& prim) {
+    merge_hit_step<kDppXor1>(t, u, v, prim);
+    merge_hit_step<kDppXor2>(t, u, v, prim);
+    if constexpr (G == 8) merge_hit_step<kDppHalfMirror>(t, u, v, prim);
+}
+
+// one child slot of a wide node against the ray (conservative quantized slab test)
+struct SlotTest {
+    bool hit, inner;
+    unsigned meta;
+};
+__device__ __forceinline__ SlotTest test_slot(unsigned slot, const uint4& m, const uint4& qx, const uint4& qy,
+                                              const uint4& qz, unsigned imask, float ax, float ay, float az,
+                                              float bx, float by, float bz, bool px, bool py, bool pz,
+                                              float best_t) {
+    const int j = (int)(slot & 3u);
+    const bool hi_half = slot >= 4u;
+    const unsigned lxw = hi_half ? qx.y : qx.x, hxw = hi_half ? qx.w : qx.z;
+    const unsigned lyw = hi_half ? qy.y : qy.x, hyw = hi_half ? qy.w : qy.z;
+    const unsigned lzw = hi_half ? qz.y : qz.x, hzw = hi_half ? qz.w : qz.z;
+    const float lx = qb(lxw, j), hx = qb(hxw, j), ly = qb(lyw, j), hy = qb(hyw, j);
+    const float lz = qb(lzw, j), hz = qb(hzw, j);
+    const float t0 = fmaxf(fmaxf(fmaf(px ? lx : hx, ax, bx), fmaf(py ? ly : hy, ay, by)),
+                           fmaxf(fmaf(pz ? lz : hz, az, bz), 0.0f));
+    const float t1 = fminf(fminf(fmaf(px ? hx : lx, ax, bx), fmaf(py ? hy : ly, ay, by)),
+                           fminf(fmaf(pz ? hz : lz, az, bz), best_t));
+    SlotTest r;
+    r.meta = ((hi_half ? m.w : m.z) >> (8 * j)) & 0xffu;
+    r.hit = r.meta != 0u && t0 <= t1 * 1.000001f;
+    r.inner = ((imask >> slot) & 1u) != 0u;
+    return r;
+}
+
+template <bool COUNT, int G>
 __global__ __launch_bounds__(kTraceBlock) void k_trace8g(SceneView s, const float4* __restrict__ ro,
                                                          const float4* __restrict__ rd, float4* __restrict__ hits,
                                                          const int* __restrict__ count_dev, int count_terms,
                                                          int count_host, int cap,
                                                          unsigned long long* __restrict__ counters) {
-    constexpr int kGroups = kTraceBlock / 8;
+    static_assert(G == 4 || G == 8, "lanes per ray");
+    constexpr int kGroups = kTraceBlock / G;
     __shared__ uint2 gstk[kGroupStack][kGroups];
     const int tid = threadIdx.x;
-    const int k = tid & 7;     // lane within the group
-    const int gib = tid >> 3;  // group within the block
+    const int k = tid & (G - 1);  // lane within the group
+    const int gib = tid / G;      // group within the block
+    const int gshift = __lane_id() & ~(G - 1);
     const int n = ray_count(count_dev, count_terms, count_host, cap);
-    unsigned long long nvis = 0, ntest = 0, mvis = 0, mtest = 0, mclk = 0;
+    unsigned long long nvis = 0, ntest = 0, mvis = 0, mtest = 0;
     for (int i = blockIdx.x * kGroups + gib; i < n; i += gridDim.x * kGroups) {
-        long long t_start = 0;
-        if (COUNT) t_start = wall_clock64();
         const float4 o4 = ro[i];
         const float4 d4 = rd[i];
         const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
@@ -470,9 +514,6 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8g(SceneView s, const floa
                     idz = __builtin_amdgcn_rcpf(sdz);
         const bool px = idx >= 0.0f, py = idy >= 0.0f, pz = idz >= 0.0f;
         const unsigned oct = (dx > 0.0f ? 1u : 0u) | (dy > 0.0f ? 2u : 0u) | (dz > 0.0f ? 4u : 0u);
-        const unsigned my_slot = (unsigned)k ^ oct;
-        const int j = (int)(my_slot & 3u);
-        const bool hi_half = my_slot >= 4u;
         float best_t = tfar, best_u = 0.0f, best_v = 0.0f;
         int best_prim = -1;
         unsigned rvis = 0, rtest = 0;
@@ -494,7 +535,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8g(SceneView s, const floa
                 const unsigned slot = (unsigned)(pb - 24) ^ oct;
                 const int child = (int)gbase + __popc(gbits & 0xffu & ((1u << slot) - 1u));
                 if (gbits > 0x00ffffffu) {
-                    gstk[sp][gib] = make_uint2(gbase, gbits);  // same value from all 8 lanes
+                    gstk[sp][gib] = make_uint2(gbase, gbits);  // same value from all lanes of the group
                     ++sp;
                 }
                 const Bvh8Node* nd = s.nodes8 + child;
@@ -507,32 +548,26 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8g(SceneView s, const floa
                 const float ay = __uint_as_float(((eb >> 8) & 0xffu) << 23) * idy;
                 const float az = __uint_as_float(((eb >> 16) & 0xffu) << 23) * idz;
                 const float bx = (p.x - ox) * idx, by = (p.y - oy) * idy, bz = (p.z - oz) * idz;
-                // this lane's slot: lo / hi bytes per axis, near / far by the ray's sign
-                const unsigned lxw = hi_half ? qx.y : qx.x, hxw = hi_half ? qx.w : qx.z;
-                const unsigned lyw = hi_half ? qy.y : qy.x, hyw = hi_half ? qy.w : qy.z;
-                const unsigned lzw = hi_half ? qz.y : qz.x, hzw = hi_half ? qz.w : qz.z;
-                const float lx = qb(lxw, j), hx = qb(hxw, j), ly = qb(lyw, j), hy = qb(hyw, j);
-                const float lz = qb(lzw, j), hz = qb(hzw, j);
-                const float t0 = fmaxf(fmaxf(fmaf(px ? lx : hx, ax, bx), fmaf(py ? ly : hy, ay, by)),
-                                       fmaxf(fmaf(pz ? lz : hz, az, bz), 0.0f));
-                const float t1 = fminf(fminf(fmaf(px ? hx : lx, ax, bx), fmaf(py ? hy : ly, ay, by)),
-                                       fminf(fmaf(pz ? hz : lz, az, bz), best_t));
-                const unsigned meta = ((hi_half ? m.w : m.z) >> (8 * j)) & 0xffu;
-                const bool hit = meta != 0u && t0 <= t1 * 1.000001f;
-                const bool inner = ((imask >> my_slot) & 1u) != 0u;
-                int tb = (hit && !inner) ? (int)wide_leaf_bits(meta) : 0;
-                const unsigned long long bal = __ballot(hit && inner);
-                const unsigned nb = (unsigned)(bal >> (__lane_id() & ~7)) & 0xffu;  // bit k = slot k ^ oct
-                tb |= dpp_i<kDppXor1>(tb);
-                tb |= dpp_i<kDppXor2>(tb);
-                tb |= dpp_i<kDppHalfMirror>(tb);
+                // lane k tests the slot at near-to-far position k (slot k ^ oct) and, for G = 4,
+                // also position k + 4; the ballots then give the group's near-to-far hit byte
+                const SlotTest s0 = test_slot((unsigned)k ^ oct, m, qx, qy, qz, imask, ax, ay, az, bx, by, bz, px,
+                                              py, pz, best_t);
+                int tb = (s0.hit && !s0.inner) ? (int)wide_leaf_bits(s0.meta) : 0;
+                unsigned nb = (unsigned)(__ballot(s0.hit && s0.inner) >> gshift) & ((1u << G) - 1u);
+                if constexpr (G == 4) {
+                    const SlotTest s1 = test_slot((unsigned)(k + 4) ^ oct, m, qx, qy, qz, imask, ax, ay, az, bx, by,
+                                                  bz, px, py, pz, best_t);
+                    if (s1.hit && !s1.inner) tb |= (int)wide_leaf_bits(s1.meta);
+                    nb |= ((unsigned)(__ballot(s1.hit && s1.inner) >> gshift) & 0xfu) << 4;
+                }
+                tb = group_or<G>(tb);
                 gbase = m.x;
                 gbits = (nb << 24) | imask;
                 tbase = m.y;
                 tbits = (unsigned)tb;
             }
             if (tbits == 0u) break;
-            // ---- triangle phase: 8 triangles per round, then the group's closest hit ----
+            // ---- triangle phase: G triangles per round, then the group's closest hit ----
             while (tbits != 0u) {
                 unsigned mine = tbits;
                 for (int q = 0; q < k; ++q) mine &= mine - 1u;  // this lane's set bit
@@ -541,17 +576,13 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8g(SceneView s, const floa
                     const float4 q0 = s.tri8[3 * tr], q1 = s.tri8[3 * tr + 1], q2 = s.tri8[3 * tr + 2];
                     tri_test(q0, q1, q2, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v, best_prim);
                 }
-                if (COUNT) rtest += (unsigned)min(__popc(tbits), 8);
-                for (int q = 0; q < 8; ++q) tbits &= tbits - 1u;
-                merge_hit_step<kDppXor1>(best_t, best_u, best_v, best_prim);
-                merge_hit_step<kDppXor2>(best_t, best_u, best_v, best_prim);
-                merge_hit_step<kDppHalfMirror>(best_t, best_u, best_v, best_prim);
+                if (COUNT) rtest += (unsigned)min(__popc(tbits), G);
+                for (int q = 0; q < G; ++q) tbits &= tbits - 1u;
+                group_merge_hit<G>(best_t, best_u, best_v, best_prim);
             }
         }
         if (k == 0) hits[i] = make_float4(best_t, best_u, best_v, __int_as_float(best_prim));
         if (COUNT && k == 0) {
-            const unsigned long long dt = (unsigned long long)(wall_clock64() - t_start);
-            mclk = dt > mclk ? dt : mclk;
             nvis += rvis;
             ntest += rtest;
             mvis = rvis > mvis ? rvis : mvis;
@@ -563,7 +594,6 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8g(SceneView s, const floa
         atomicAdd(&counters[1], ntest);
         atomicMax(&counters[2], mvis);
         atomicMax(&counters[3], mtest);
-        atomicMax(&counters[5], mclk);
     }
 }
 
@@ -586,18 +616,25 @@ void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4
     }
     // small queues: 8 lanes per ray over the 8-wide BVH (PGRT_GROUP_MAX: largest queue, rays)
     const int group_max = s.group_max;
+    static const int group8_max = [] {
+        const char* e = getenv("PGRT_GROUP8_MAX");  // r1 A/B: 4 lanes on level 1, 8 below
+        return e ? atoi(e) : 150000;
+    }();
     {
         const int exg = expect > 0 && expect < max_count ? expect : max_count;
         if (allow_group && exg <= group_max && s.depth8 + 1 <= kGroupStack) {
-            constexpr int kGroups = kTraceBlock / 8;
-            int grid = ceil_div(exg, kGroups);
-            if (grid > 16384) grid = 16384;
-            if (count)
-                hipLaunchKernelGGL((k_trace8g<true>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
-                                   count_dev, count_terms, count_host, max_count, counters);
-            else
-                hipLaunchKernelGGL((k_trace8g<false>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
-                                   count_dev, count_terms, count_host, max_count, counters);
+            // 8 lanes per ray for the smallest queues (the latency floor of the slowest ray),
+            // 4 lanes (two child slots each) when there are enough rays to fill the machine
+            const bool g4 = exg > group8_max;
+#define PGRT_LAUNCH_G(C, G)                                                                                        \
+    hipLaunchKernelGGL((k_trace8g<C, G>), dim3(ceil_div(exg, kTraceBlock / G) > 16384 ? 16384 : ceil_div(exg, kTraceBlock / G)), \
+                       dim3(kTraceBlock), 0, stream, s, ro, rd, hits, count_dev, count_terms, count_host, max_count, counters)
+            if (count) {
+                if (g4) PGRT_LAUNCH_G(true, 4); else PGRT_LAUNCH_G(true, 8);
+            } else {
+                if (g4) PGRT_LAUNCH_G(false, 4); else PGRT_LAUNCH_G(false, 8);
+            }
+#undef PGRT_LAUNCH_G
             return;
         }
     }

@@ -32,10 +32,16 @@ def main():
                         jitter=abi.PGRT_JITTER_HASH if S > 1 or dof else abi.PGRT_JITTER_NONE)
     ctx.render(p)
     p.profile = 1
-    _, st = ctx.render(p)
-    print(json.dumps({"stage_ms": {k: round(v, 4) for k, v in st.as_dict().items() if k.startswith("ms_")},
-                      "rays": st.rays(), "trace_launches": st.trace_launches}))
-    lv_ms = [(dd["ms_trace"], dd["ms_shade"]) for dd in ctx.frame_diag()]
+    reps = int(os.environ.get("DIAG_REPS", "9"))  # medians over repeated profiled frames
+    stats, lvs = [], []
+    for _ in range(reps):
+        _, st = ctx.render(p)
+        stats.append(st.as_dict())
+        lvs.append([(dd["ms_trace"], dd["ms_shade"]) for dd in ctx.frame_diag()])
+    med = lambda xs: sorted(xs)[len(xs) // 2]  # noqa: E731
+    print(json.dumps({"stage_ms": {k: round(med([x[k] for x in stats]), 4) for k in stats[0] if k.startswith("ms_")},
+                      "rays": st.rays(), "trace_launches": st.trace_launches, "reps": reps}))
+    lv_ms = [(med([lv[L][0] for lv in lvs]), med([lv[L][1] for lv in lvs])) for L in range(len(lvs[0]))]
     p.profile = 2
     ctx.render(p)
     for L, dd in enumerate(ctx.frame_diag()):
