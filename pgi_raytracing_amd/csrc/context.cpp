@@ -76,6 +76,63 @@ enum { CAT_RAYGEN, CAT_TRACE, CAT_SHADE, CAT_SHADOW, CAT_COMBINE, CAT_LTRACE, CA
 
 }  // namespace
 
+namespace pgrt {
+// One pipeline instance: queues, level nodes, shadow queue and counters for a subset of the
+// frame's tiles, enqueued on its own stream.  Two slots run concurrently: each launch of one
+// slot fills the CUs the other slot's latency-bound launches leave idle (the tail of every
+// level, the deep Whitted levels).  r1 A/B on C2 (tools/ab_slots.sh): 1 slot 0.87 ms, 2 slots
+// 0.79-0.80, 3 slots 0.80, 4+ slots slower (more streams than the 4 hardware queues); a stagger
+// (slot k+1 waits for slot k's level 0, PGRT_STAGGER_LEVEL) was slower (0.90).
+struct FrameSlot {
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_stagger = nullptr, ev_done = nullptr;
+    DevBuf<int4> tiles;
+    DevBuf<float4> q_ro[2], q_rd[2], q_hit[2];
+    DevBuf<float> q_time[2];
+    int q_cap = 0;
+    std::vector<std::unique_ptr<DevBuf<float4>>> n_color, n_att;
+    std::vector<std::unique_ptr<DevBuf<int4>>> n_link;
+    std::vector<int> level_cap;
+    DevBuf<float4> s_ro, s_rd, s_hit, s_contrib;
+    int s_cap = 0;
+    DevBuf<FrameCounters> fc;  // one per sample batch
+    std::vector<FrameCounters> host_fc;
+    // pinned staging (async copies from pageable memory would block the enqueue of the next slot)
+    FrameCounters* pinned_fc = nullptr;
+    int pinned_fc_n = 0;
+    int4* pinned_tiles = nullptr;
+    int pinned_tiles_n = 0;
+    void ensure_pinned(int batches, int ntiles) {
+        if (pinned_fc_n < batches) {
+            if (pinned_fc) (void)hipHostFree(pinned_fc);
+            PGRT_HIP(hipHostMalloc((void**)&pinned_fc, sizeof(FrameCounters) * batches, hipHostMallocDefault));
+            pinned_fc_n = batches;
+        }
+        if (pinned_tiles_n < ntiles) {
+            if (pinned_tiles) (void)hipHostFree(pinned_tiles);
+            PGRT_HIP(hipHostMalloc((void**)&pinned_tiles, sizeof(int4) * ntiles, hipHostMallocDefault));
+            pinned_tiles_n = ntiles;
+        }
+    }
+    DevBuf<float4> accum;
+    DevBuf<int> gstack;
+    int expect_count[kMaxLevels] = {0};  // grid hints from the previous frame (0 = unknown)
+    int expect_shadow_total = 0;
+    FrameSlot() {
+        PGRT_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        PGRT_HIP(hipEventCreateWithFlags(&ev_stagger, hipEventDisableTiming));
+        PGRT_HIP(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
+    }
+    ~FrameSlot() {
+        if (pinned_fc) (void)hipHostFree(pinned_fc);
+        if (pinned_tiles) (void)hipHostFree(pinned_tiles);
+        if (ev_stagger) (void)hipEventDestroy(ev_stagger);
+        if (ev_done) (void)hipEventDestroy(ev_done);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+}  // namespace pgrt
+
 struct pgrt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -98,25 +155,14 @@ struct pgrt_ctx {
     CameraView cam{};
     bool has_cam = false;
 
-    // frame state
-    DevBuf<int4> tiles;
-    DevBuf<float4> q_ro[2], q_rd[2], q_hit[2];
-    DevBuf<float> q_time[2];
-    int q_cap = 0;
-    std::vector<std::unique_ptr<DevBuf<float4>>> n_color, n_att;
-    std::vector<std::unique_ptr<DevBuf<int4>>> n_link;
-    std::vector<int> level_cap;
-    DevBuf<float4> s_ro, s_rd, s_hit, s_contrib;
-    int s_cap = 0;
-    DevBuf<FrameCounters> fc;
-    DevBuf<float4> accum;
-    DevBuf<int> gstack;
+    // frame state: independent pipeline slots (tile subsets), each on its own stream
+    std::vector<std::unique_ptr<FrameSlot>> slots;
+    DevBuf<FrameCounters> fc;  // pgrt_intersect_closest
+    DevBuf<int> gstack;        // pgrt_intersect_closest
     DevBuf<float> out_tmp;
     StageTimer timer;
-    std::vector<FrameCounters> last_fc;  // per batch, for pgrt_frame_diag
+    std::vector<FrameCounters> last_fc;  // per slot and batch, for pgrt_frame_diag
     double level_ms[kMaxLevels][2] = {};  // per-level trace / shade ms of the last profiled call
-    int expect_count[kMaxLevels] = {0};   // grid hints from the previous frame (0 = unknown)
-    int expect_shadow_total = 0;
 
     // multi-GPU
     ncclComm_t comm = nullptr;
@@ -352,42 +398,79 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
     (void)t0;
 }
 
-void ensure_frame_buffers(pgrt_ctx* ctx, int n0, int levels) {
-    if (ctx->q_cap < n0) {
+void ensure_frame_buffers(FrameSlot* sl, int n0, int levels, int nlight, int batches) {
+    if (sl->q_cap < n0) {
         for (int b = 0; b < 2; ++b) {
-            ctx->q_ro[b].alloc(n0);
-            ctx->q_rd[b].alloc(n0);
-            ctx->q_hit[b].alloc(n0);
-            ctx->q_time[b].alloc(n0);
+            sl->q_ro[b].alloc(n0);
+            sl->q_rd[b].alloc(n0);
+            sl->q_hit[b].alloc(n0);
+            sl->q_time[b].alloc(n0);
         }
-        ctx->q_cap = n0;
+        sl->q_cap = n0;
     }
-    if ((int)ctx->level_cap.size() < levels) ctx->level_cap.resize(levels, 0);
-    while ((int)ctx->n_color.size() < levels) {
-        ctx->n_color.emplace_back(new DevBuf<float4>());
-        ctx->n_att.emplace_back(new DevBuf<float4>());
-        ctx->n_link.emplace_back(new DevBuf<int4>());
+    if ((int)sl->level_cap.size() < levels) sl->level_cap.resize(levels, 0);
+    while ((int)sl->n_color.size() < levels) {
+        sl->n_color.emplace_back(new DevBuf<float4>());
+        sl->n_att.emplace_back(new DevBuf<float4>());
+        sl->n_link.emplace_back(new DevBuf<int4>());
     }
     for (int L = 0; L < levels; ++L) {
-        const int cap = std::max(L == 0 ? n0 : std::min(ctx->q_cap, std::max(ctx->level_cap[L], n0)), 1);
-        if (ctx->level_cap[L] < cap || (int)ctx->n_color[L]->n < cap) {
-            ctx->n_color[L]->alloc(cap);
-            ctx->n_att[L]->alloc(cap);
-            ctx->n_link[L]->alloc(cap);
-            ctx->level_cap[L] = cap;
+        const int cap = std::max(L == 0 ? n0 : std::min(sl->q_cap, std::max(sl->level_cap[L], n0)), 1);
+        if (sl->level_cap[L] < cap || (int)sl->n_color[L]->n < cap) {
+            sl->n_color[L]->alloc(cap);
+            sl->n_att[L]->alloc(cap);
+            sl->n_link[L]->alloc(cap);
+            sl->level_cap[L] = cap;
         }
     }
-    const int nl = std::max(1, ctx->view.nlight);
-    if (ctx->s_cap < n0 * nl) {
+    const int nl = std::max(1, nlight);
+    if (sl->s_cap < n0 * nl) {
         const int sc = n0 * nl;
-        ctx->s_ro.alloc(sc);
-        ctx->s_rd.alloc(sc);
-        ctx->s_hit.alloc(sc);
-        ctx->s_contrib.alloc(sc);
-        ctx->s_cap = sc;
+        sl->s_ro.alloc(sc);
+        sl->s_rd.alloc(sc);
+        sl->s_hit.alloc(sc);
+        sl->s_contrib.alloc(sc);
+        sl->s_cap = sc;
     }
-    ctx->fc.alloc(1);
-    if (ctx->gstack.n == 0) ctx->gstack.alloc((size_t)kTraceGridThreads * kGlobalStack);
+    sl->fc.alloc((size_t)batches);
+    if (sl->gstack.n == 0) sl->gstack.alloc((size_t)kTraceGridThreads * kGlobalStack);
+}
+
+// grow a slot's level queues / shadow queue after an overflow (2x what was requested)
+void grow_after_overflow(FrameSlot* sl, int levels) {
+    int shadow_need = 0;
+    for (auto& h : sl->host_fc) {
+        int sc = 0;
+        for (int L = 0; L < kMaxLevels; ++L) sc += h.shadow_count[L];
+        shadow_need = std::max(shadow_need, sc);
+        for (int L = 1; L < levels; ++L) {
+            const int need = h.count[L] * 2;
+            if (need > sl->level_cap[L]) sl->level_cap[L] = need;
+            if (need > sl->q_cap) {
+                for (int b = 0; b < 2; ++b) {
+                    sl->q_ro[b].alloc(need);
+                    sl->q_rd[b].alloc(need);
+                    sl->q_hit[b].alloc(need);
+                    sl->q_time[b].alloc(need);
+                }
+                sl->q_cap = need;
+            }
+        }
+    }
+    for (int L = 1; L < levels; ++L)
+        if ((int)sl->n_color[L]->n < sl->level_cap[L]) {
+            sl->n_color[L]->alloc(sl->level_cap[L]);
+            sl->n_att[L]->alloc(sl->level_cap[L]);
+            sl->n_link[L]->alloc(sl->level_cap[L]);
+        }
+    if (shadow_need * 2 > sl->s_cap) {
+        const int sh = shadow_need * 2;
+        sl->s_ro.alloc(sh);
+        sl->s_rd.alloc(sh);
+        sl->s_hit.alloc(sh);
+        sl->s_contrib.alloc(sh);
+        sl->s_cap = sh;
+    }
 }
 
 // Render the pixels of `tiles` (each <= kTile x kTile); out_mode 0 writes a framebuffer
@@ -399,139 +482,157 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
     PGRT_REQUIRE(p->spp_side >= 1 && p->spp_side <= 64, PGRT_ERR_INVALID_ARGUMENT, "spp_side must be in [1, 64]");
     PGRT_REQUIRE(p->max_level >= 0 && p->max_level <= kMaxLevels - 2, PGRT_ERR_INVALID_ARGUMENT,
                  "max_level must be in [0, 14]");
-    hipStream_t s = ctx->stream;
     const int ntiles = (int)tiles.size();
-    const long long npix = (long long)ntiles * kTile * kTile;
     const int spp = p->spp_side * p->spp_side;
     if (ntiles == 0) return;
-    PGRT_REQUIRE(npix <= kMaxBatchRays * 8, PGRT_ERR_INVALID_ARGUMENT, "frame too large");
-    int nsb = (int)std::max(1ll, std::min<long long>(spp, kMaxBatchRays / npix));
     const int levels = p->max_level + 1;
-    ctx->tiles.alloc(ntiles);
-    PGRT_HIP(hipMemcpyAsync(ctx->tiles.p, tiles.data(), sizeof(int4) * ntiles, hipMemcpyHostToDevice, s));
-    ctx->accum.alloc((size_t)npix);
+    // pipeline slots: tiles dealt round-robin (slot j gets tiles j, j+K, ...)
+    static const int want_slots = [] {
+        const char* e = getenv("PGRT_SLOTS");
+        return e ? std::max(1, std::min(3, atoi(e))) : kDefaultSlots;
+    }();
+    static const int stagger_level = [] {  // slot k+1 starts after slot k's level-L shade (-1: no stagger)
+        const char* e = getenv("PGRT_STAGGER_LEVEL");
+        return e ? atoi(e) : -1;
+    }();
+    const int K = std::max(1, std::min(want_slots, ntiles));
+    while ((int)ctx->slots.size() < K) ctx->slots.emplace_back(new FrameSlot());
     ctx->timer.on = p->profile > 0;
     double ms[CAT_N] = {0};
     uint64_t rays_shadow = 0, rays_reflect = 0, rays_refract = 0, trav_nodes = 0, trav_tests = 0, trav_wide = 0;
     int retries = 0, trace_launches = 0;
-    FrameParams fp{};
-    fp.spp_side = p->spp_side;
-    fp.max_level = p->max_level;
-    fp.dof = p->dof;
-    fp.focal = p->focal_distance;
-    fp.aperture = p->aperture;
-    fp.gamma = p->gamma_level;
-    fp.jitter = p->jitter;
-    fp.seed = p->seed;
-    fp.frame = p->frame;
-    fp.ntiles = ntiles;
+    FrameParams fp0{};
+    fp0.spp_side = p->spp_side;
+    fp0.max_level = p->max_level;
+    fp0.dof = p->dof;
+    fp0.focal = p->focal_distance;
+    fp0.aperture = p->aperture;
+    fp0.gamma = p->gamma_level;
+    fp0.jitter = p->jitter;
+    fp0.seed = p->seed;
+    fp0.frame = p->frame;
+    // the main stream's prior work (scene upload, camera) happens before any slot starts
+    hipEvent_t ev_start;
+    PGRT_HIP(hipEventCreateWithFlags(&ev_start, hipEventDisableTiming));
+    struct EvGuard {
+        hipEvent_t e;
+        ~EvGuard() { (void)hipEventDestroy(e); }
+    } evg{ev_start};
     for (;;) {  // whole-frame retry if any queue overflowed
-        const int n0max = (int)(npix * nsb);
-        ensure_frame_buffers(ctx, n0max, levels);
-        std::vector<FrameCounters> host_fc;
-        for (int s0 = 0; s0 < spp; s0 += nsb) {
-            fp.s0 = s0;
-            fp.nsb = std::min(nsb, spp - s0);
-            const int n0 = (int)(npix * fp.nsb);
-            FrameCounters* fcd = ctx->fc.p;
-            PGRT_HIP(hipMemsetAsync(fcd, 0, sizeof(FrameCounters), s));
-            Queue q[2];
-            for (int b = 0; b < 2; ++b)
-                q[b] = Queue{ctx->q_ro[b].p, ctx->q_rd[b].p, ctx->q_time[b].p, ctx->q_hit[b].p, ctx->q_cap};
-            ShadowQueue sq{ctx->s_ro.p, ctx->s_rd.p, ctx->s_hit.p, ctx->s_contrib.p, ctx->s_cap};
-            int id = ctx->timer.begin(s, CAT_RAYGEN);
-            launch_raygen(ctx->cam, fp, ctx->tiles.p, q[0], n0, fcd, s);
-            ctx->timer.end(s, id);
-            for (int L = 0; L < levels; ++L) {
-                Queue qc = q[L & 1], qn = q[(L + 1) & 1];
-                const int maxc = L == 0 ? n0 : std::min(ctx->q_cap, ctx->level_cap[L]);
-                qc.cap = maxc;
-                qn.cap = std::min(ctx->q_cap, L + 1 < levels ? ctx->level_cap[L + 1] : ctx->q_cap);
-                LevelNodes ln{ctx->n_color[L]->p, ctx->n_link[L]->p, ctx->n_att[L]->p};
-                // grid hints: last frame's per-level counts (+25 %); level 0 is exact
-                const int ex = L == 0 ? n0 : ctx->expect_count[L];
-                id = ctx->timer.begin(s, CAT_TRACE, CAT_LTRACE + L);
-                launch_trace(ctx->view, qc.ro, qc.rd, qc.hit, &fcd->count[L], 0, maxc, &fcd->fetch[L],
-                             ctx->gstack.p, kTraceGridThreads, fcd->trav[L], p->profile >= 2, s, ex);
+        PGRT_HIP(hipEventRecord(ev_start, ctx->stream));
+        for (int j = 0; j < K; ++j) {
+            FrameSlot* sl = ctx->slots[j].get();
+            hipStream_t s = sl->stream;
+            const int nt = (ntiles - j + K - 1) / K;
+            const long long npix = (long long)nt * kTile * kTile;
+            PGRT_REQUIRE(npix <= kMaxBatchRays * 8, PGRT_ERR_INVALID_ARGUMENT, "frame too large");
+            const int nsb = (int)std::max(1ll, std::min<long long>(spp, kMaxBatchRays / npix));
+            const int batches = (spp + nsb - 1) / nsb;
+            ensure_frame_buffers(sl, (int)(npix * nsb), levels, ctx->view.nlight, batches);
+            sl->ensure_pinned(batches, nt);
+            for (int t = j, q = 0; t < ntiles; t += K, ++q) sl->pinned_tiles[q] = tiles[t];
+            PGRT_HIP(hipStreamWaitEvent(s, ev_start, 0));
+            if (j > 0 && stagger_level >= 0) PGRT_HIP(hipStreamWaitEvent(s, ctx->slots[j - 1]->ev_stagger, 0));
+            sl->tiles.alloc(nt);
+            PGRT_HIP(hipMemcpyAsync(sl->tiles.p, sl->pinned_tiles, sizeof(int4) * nt, hipMemcpyHostToDevice, s));
+            sl->accum.alloc((size_t)npix);
+            PGRT_HIP(hipMemsetAsync(sl->fc.p, 0, sizeof(FrameCounters) * batches, s));
+            FrameParams fp = fp0;
+            fp.ntiles = nt;
+            bool staggered = false;
+            for (int bi = 0; bi < batches; ++bi) {
+                const int s0 = bi * nsb;
+                fp.s0 = s0;
+                fp.nsb = std::min(nsb, spp - s0);
+                const int n0 = (int)(npix * fp.nsb);
+                FrameCounters* fcd = sl->fc.p + bi;
+                Queue q[2];
+                for (int b = 0; b < 2; ++b)
+                    q[b] = Queue{sl->q_ro[b].p, sl->q_rd[b].p, sl->q_time[b].p, sl->q_hit[b].p, sl->q_cap};
+                ShadowQueue sq{sl->s_ro.p, sl->s_rd.p, sl->s_hit.p, sl->s_contrib.p, sl->s_cap};
+                int id = ctx->timer.begin(s, CAT_RAYGEN);
+                launch_raygen(ctx->cam, fp, sl->tiles.p, q[0], n0, fcd, s);
                 ctx->timer.end(s, id);
-                ++trace_launches;
-                id = ctx->timer.begin(s, CAT_SHADE, CAT_LSHADE + L);
-                launch_shade(ctx->view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex);
+                for (int L = 0; L < levels; ++L) {
+                    Queue qc = q[L & 1], qn = q[(L + 1) & 1];
+                    const int maxc = L == 0 ? n0 : std::min(sl->q_cap, sl->level_cap[L]);
+                    qc.cap = maxc;
+                    qn.cap = std::min(sl->q_cap, L + 1 < levels ? sl->level_cap[L + 1] : sl->q_cap);
+                    LevelNodes ln{sl->n_color[L]->p, sl->n_link[L]->p, sl->n_att[L]->p};
+                    // grid hints: last frame's per-level counts (+25 %); level 0 is exact
+                    const int ex = L == 0 ? n0 : sl->expect_count[L];
+                    id = ctx->timer.begin(s, CAT_TRACE, CAT_LTRACE + L);
+                    launch_trace(ctx->view, qc.ro, qc.rd, qc.hit, &fcd->count[L], 0, maxc, &fcd->fetch[L],
+                                 sl->gstack.p, kTraceGridThreads, fcd->trav[L], p->profile >= 2, s, ex);
+                    ctx->timer.end(s, id);
+                    ++trace_launches;
+                    id = ctx->timer.begin(s, CAT_SHADE, CAT_LSHADE + L);
+                    launch_shade(ctx->view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex);
+                    ctx->timer.end(s, id);
+                    if (!staggered && (L == std::min(stagger_level, levels - 1))) {
+                        PGRT_HIP(hipEventRecord(sl->ev_stagger, s));
+                        staggered = true;
+                    }
+                }
+                if (ctx->view.nlight > 0 && p->max_level > 0) {  // every level's shadow rays, one launch
+                    id = ctx->timer.begin(s, CAT_TRACE);
+                    const int sid = ctx->timer.begin(s, CAT_SHADOW);
+                    launch_trace(ctx->view, sq.ro, sq.rd, sq.hit, &fcd->shadow_count[0], 0, sq.cap,
+                                 &fcd->fetch[kMaxLevels], sl->gstack.p, kTraceGridThreads, fcd->trav[kMaxLevels],
+                                 p->profile >= 2, s, sl->expect_shadow_total, levels,
+                                 false);  // shadow rays (from the light along H) mostly miss the root
+                    ctx->timer.end(s, sid);
+                    ctx->timer.end(s, id);
+                    ++trace_launches;
+                }
+                id = ctx->timer.begin(s, CAT_COMBINE);
+                for (int L = p->max_level - 1; L >= 1; --L) {
+                    LevelNodes ln{sl->n_color[L]->p, sl->n_link[L]->p, sl->n_att[L]->p};
+                    launch_combine(ctx->view, L, ln, sl->n_color[L + 1]->p, sq, fcd,
+                                   std::min(sl->q_cap, sl->level_cap[L]), s, sl->expect_count[L]);
+                }
+                LevelNodes l0{sl->n_color[0]->p, sl->n_link[0]->p, sl->n_att[0]->p};
+                launch_finish(ctx->view, fp, sl->tiles.p, l0, levels > 1 ? sl->n_color[1]->p : sl->n_color[0]->p,
+                              sq, sl->accum.p, out, out_mode, ox, oy, pitch, (int)npix, s0 == 0,
+                              s0 + fp.nsb >= spp, K, j, s);
                 ctx->timer.end(s, id);
             }
-            if (ctx->view.nlight > 0 && p->max_level > 0) {  // every level's shadow rays, one launch
-                id = ctx->timer.begin(s, CAT_TRACE);
-                const int sid = ctx->timer.begin(s, CAT_SHADOW);
-                launch_trace(ctx->view, sq.ro, sq.rd, sq.hit, &fcd->shadow_count[0], 0, sq.cap,
-                             &fcd->fetch[kMaxLevels], ctx->gstack.p, kTraceGridThreads, fcd->trav[kMaxLevels],
-                             p->profile >= 2, s, ctx->expect_shadow_total, levels,
-                             false);  // shadow rays (from the light along H) mostly miss the root
-                ctx->timer.end(s, sid);
-                ctx->timer.end(s, id);
-                ++trace_launches;
-            }
-            id = ctx->timer.begin(s, CAT_COMBINE);
-            for (int L = p->max_level - 1; L >= 1; --L) {
-                LevelNodes ln{ctx->n_color[L]->p, ctx->n_link[L]->p, ctx->n_att[L]->p};
-                launch_combine(ctx->view, L, ln, ctx->n_color[L + 1]->p, sq, fcd,
-                               std::min(ctx->q_cap, ctx->level_cap[L]), s, ctx->expect_count[L]);
-            }
-            LevelNodes l0{ctx->n_color[0]->p, ctx->n_link[0]->p, ctx->n_att[0]->p};
-            launch_finish(ctx->view, fp, ctx->tiles.p, l0, levels > 1 ? ctx->n_color[1]->p : ctx->n_color[0]->p, sq,
-                          ctx->accum.p, out, out_mode, ox, oy, pitch, (int)npix, s0 == 0, s0 + fp.nsb >= spp, s);
-            ctx->timer.end(s, id);
-            FrameCounters hfc;
-            PGRT_HIP(hipMemcpyAsync(&hfc, fcd, sizeof(FrameCounters), hipMemcpyDeviceToHost, s));
-            PGRT_HIP(hipStreamSynchronize(s));
-            host_fc.push_back(hfc);
-            if (hfc.overflow) break;
+            if (!staggered) PGRT_HIP(hipEventRecord(sl->ev_stagger, s));
+            sl->host_fc.resize(batches);
+            PGRT_HIP(hipMemcpyAsync(sl->pinned_fc, sl->fc.p, sizeof(FrameCounters) * batches, hipMemcpyDeviceToHost,
+                                    s));
+            PGRT_HIP(hipEventRecord(sl->ev_done, s));
+        }
+        for (int j = 0; j < K; ++j) PGRT_HIP(hipStreamWaitEvent(ctx->stream, ctx->slots[j]->ev_done, 0));
+        for (int j = 0; j < K; ++j) {
+            FrameSlot* sl = ctx->slots[j].get();
+            PGRT_HIP(hipEventSynchronize(sl->ev_done));
+            std::copy(sl->pinned_fc, sl->pinned_fc + sl->host_fc.size(), sl->host_fc.begin());
         }
         PGRT_HIP(hipGetLastError());
         bool overflow = false;
-        for (auto& h : host_fc) overflow |= h.overflow != 0;
-        ctx->last_fc = host_fc;
-        int shadow_need = 0;  // largest batch-wide shadow queue requested
-        for (auto& h : host_fc) {
-            int sc = 0;
-            for (int L = 0; L < kMaxLevels; ++L) sc += h.shadow_count[L];
-            shadow_need = std::max(shadow_need, sc);
-        }
-        for (int L = 0; L < kMaxLevels; ++L) {  // grid hints for the next frame
-            int c = 0;
-            for (auto& h : host_fc) c = std::max(c, h.count[L]);
-            ctx->expect_count[L] = c + c / 4 + 1024;
-        }
-        ctx->expect_shadow_total = shadow_need + shadow_need / 4 + 1024;
-        if (overflow) {
-            // grow every level queue to what was requested (2x margin) and redo the frame
-            for (auto& h : host_fc)
-                for (int L = 1; L < levels; ++L) {
-                    const int need = h.count[L] * 2;
-                    if (need > ctx->level_cap[L]) ctx->level_cap[L] = need;
-                    if (need > ctx->q_cap) {
-                        for (int b = 0; b < 2; ++b) {
-                            ctx->q_ro[b].alloc(need);
-                            ctx->q_rd[b].alloc(need);
-                            ctx->q_hit[b].alloc(need);
-                            ctx->q_time[b].alloc(need);
-                        }
-                        ctx->q_cap = need;
-                    }
-                    for (int L2 = 1; L2 < levels; ++L2)
-                        if ((int)ctx->n_color[L2]->n < ctx->level_cap[L2]) {
-                            ctx->n_color[L2]->alloc(ctx->level_cap[L2]);
-                            ctx->n_att[L2]->alloc(ctx->level_cap[L2]);
-                            ctx->n_link[L2]->alloc(ctx->level_cap[L2]);
-                        }
-                }
-            if (shadow_need * 2 > ctx->s_cap) {
-                const int sh = shadow_need * 2;
-                ctx->s_ro.alloc(sh);
-                ctx->s_rd.alloc(sh);
-                ctx->s_hit.alloc(sh);
-                ctx->s_contrib.alloc(sh);
-                ctx->s_cap = sh;
+        ctx->last_fc.clear();
+        for (int j = 0; j < K; ++j) {
+            FrameSlot* sl = ctx->slots[j].get();
+            for (auto& h : sl->host_fc) {
+                overflow |= h.overflow != 0;
+                ctx->last_fc.push_back(h);
             }
+            int shadow_need = 0;
+            for (auto& h : sl->host_fc) {
+                int sc = 0;
+                for (int L = 0; L < kMaxLevels; ++L) sc += h.shadow_count[L];
+                shadow_need = std::max(shadow_need, sc);
+            }
+            for (int L = 0; L < kMaxLevels; ++L) {  // grid hints for the next frame
+                int c = 0;
+                for (auto& h : sl->host_fc) c = std::max(c, h.count[L]);
+                sl->expect_count[L] = c + c / 4 + 1024;
+            }
+            sl->expect_shadow_total = shadow_need + shadow_need / 4 + 1024;
+        }
+        if (overflow) {
+            for (int j = 0; j < K; ++j) grow_after_overflow(ctx->slots[j].get(), levels);
             ctx->timer.collect(ms);
             std::fill(ms, ms + CAT_N, 0.0);
             ++retries;
@@ -539,7 +640,7 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
             trace_launches = 0;
             continue;
         }
-        for (auto& h : host_fc) {
+        for (auto& h : ctx->last_fc) {
             for (int L = 0; L < levels; ++L) {
                 rays_shadow += (uint64_t)h.shadow_count[L];
                 if (L >= 1) {
@@ -556,9 +657,8 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
         break;
     }
     PGRT_HIP(hipGetLastError());
+    ctx->timer.collect(ms);
     if (st) {
-        PGRT_HIP(hipStreamSynchronize(s));
-        ctx->timer.collect(ms);
         long long real_pix = 0;
         for (auto& t : tiles) real_pix += (long long)t.z * t.w;
         st->rays_primary = (uint64_t)(real_pix * spp);
@@ -580,8 +680,6 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
         st->trace_launches = trace_launches;
         st->levels = levels;
         st->overflow_retries = retries;
-    } else {
-        ctx->timer.collect(ms);
     }
 }
 

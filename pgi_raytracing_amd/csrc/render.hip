@@ -370,7 +370,8 @@ void launch_combine(const SceneView& s, int level, LevelNodes nodes, const float
 __global__ __launch_bounds__(kBlock) void k_finish(SceneView s, FrameParams fp, const int4* __restrict__ tiles,
                                                    LevelNodes l0, const float4* __restrict__ child, ShadowQueue sq,
                                                    float4* __restrict__ accum, float* __restrict__ out, int out_mode,
-                                                   int ox, int oy, int pitch, int npix, int first, int last) {
+                                                   int ox, int oy, int pitch, int npix, int first, int last, int K,
+                                                   int j) {
     const int p = blockIdx.x * kBlock + threadIdx.x;
     if (p >= npix) return;
     float4 acc = first ? make_float4(0.0f, 0.0f, 0.0f, 1.0f) : accum[p];
@@ -397,17 +398,18 @@ __global__ __launch_bounds__(kBlock) void k_finish(SceneView s, FrameParams fp, 
     } else {
         const int tile = p / (kTile * kTile);
         const int4 tr = tiles[tile];
-        dst = out + ((size_t)tile * kTile * kTile + (size_t)(py - tr.y) * kTile + (size_t)(px - tr.x)) * 4;
+        const size_t gtile = (size_t)tile * K + j;  // position in the caller's tile list
+        dst = out + (gtile * kTile * kTile + (size_t)(py - tr.y) * kTile + (size_t)(px - tr.x)) * 4;
     }
     *reinterpret_cast<float4*>(dst) = o;
 }
 
 void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles, LevelNodes l0, const float4* child,
                    ShadowQueue sq, float4* accum, float* out, int out_mode, int ox, int oy, int pitch, int npix,
-                   bool first, bool last, hipStream_t stream) {
+                   bool first, bool last, int K, int j, hipStream_t stream) {
     if (npix <= 0) return;
     hipLaunchKernelGGL(k_finish, dim3(ceil_div(npix, kBlock)), dim3(kBlock), 0, stream, s, fp, tiles, l0, child, sq,
-                       accum, out, out_mode, ox, oy, pitch, npix, first ? 1 : 0, last ? 1 : 0);
+                       accum, out, out_mode, ox, oy, pitch, npix, first ? 1 : 0, last ? 1 : 0, K, j);
 }
 
 // ------------------------------------------------------------------ multi-GPU unpack

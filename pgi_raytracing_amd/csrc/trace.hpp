@@ -79,9 +79,11 @@ void launch_combine(const SceneView& s, int level, LevelNodes nodes, const float
                     const FrameCounters* fc, int max_count, hipStream_t stream, int expect = 0);
 // level-0 combine + sample accumulation (+ gamma and framebuffer write on the last batch).
 // out_mode 0: framebuffer (rect origin ox,oy, row pitch in pixels); 1: tile-compact
+// tiles of this launch are tiles j, j + K, ... of the caller's list (pipeline slot j of K):
+// out_mode 1 writes local tile t at tile-compact position t * K + j
 void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles, LevelNodes l0, const float4* child,
                    ShadowQueue sq, float4* accum, float* out, int out_mode, int ox, int oy, int pitch, int npix,
-                   bool first, bool last, hipStream_t stream);
+                   bool first, bool last, int K, int j, hipStream_t stream);
 void launch_unpack_tiles(const float* gathered, float* rgba, int width, int height, int world, int tiles_per_rank,
                          hipStream_t stream);
 
@@ -89,6 +91,7 @@ void launch_unpack_tiles(const float* gathered, float* rgba, int width, int heig
 constexpr int kBuilderLbvh = 0;  // Karras 2012 over 63-bit Morton codes
 constexpr int kBuilderPloc = 1;  // PLOC clustering over the same Morton order + SAH collapse
 constexpr float kDefaultSplitBeta = 0.0f;  // PGRT_SPLIT default (extra references / triangles)
+constexpr int kDefaultSlots = 2;           // PGRT_SLOTS default: staggered pipeline slots per frame
 constexpr int kDefaultGroupMax = 400000;   // PGRT_GROUP_MAX default: queues up to this many rays use
                                            // the 8-lanes-per-ray kernel (r1 A/B: tail levels -45 %)
 struct BuildOut {
