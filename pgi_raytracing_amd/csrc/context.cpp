@@ -563,7 +563,8 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
                     const int ex = L == 0 ? n0 : sl->expect_count[L];
                     id = ctx->timer.begin(s, CAT_TRACE, CAT_LTRACE + L);
                     launch_trace(ctx->view, qc.ro, qc.rd, qc.hit, &fcd->count[L], 0, maxc, &fcd->fetch[L],
-                                 sl->gstack.p, kTraceGridThreads, fcd->trav[L], p->profile >= 2, s, ex);
+                                 sl->gstack.p, kTraceGridThreads, fcd->trav[L], p->profile >= 2, s, ex, 1, true,
+                                 L == 0);  // level 0: coherent 8x8-pixel waves -> packet traversal
                     ctx->timer.end(s, id);
                     ++trace_launches;
                     id = ctx->timer.begin(s, CAT_SHADE, CAT_LSHADE + L);

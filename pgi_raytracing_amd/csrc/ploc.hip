@@ -23,9 +23,9 @@ namespace pgrt {
 namespace {
 
 constexpr int kB = 256;
-constexpr int kRadius = 16;
-constexpr float kCostNode = 1.0f;  // SAH constants: one traversal step vs one triangle test
-constexpr float kCostTri = 1.0f;
+constexpr int kMaxRadius = 64;     // LDS window bound; the search radius is a runtime knob
+constexpr int kDefaultRadius = 16;
+constexpr float kDefaultCostTri = 1.0f;  // SAH: one triangle test relative to one node step
 
 __device__ __forceinline__ float half_area(float4 lo, float4 hi) {
     const float dx = hi.x - lo.x, dy = hi.y - lo.y, dz = hi.z - lo.z;
@@ -50,8 +50,8 @@ __global__ __launch_bounds__(kB) void k_ploc_init(const float4* __restrict__ rlo
 }
 
 __global__ __launch_bounds__(kB) void k_ploc_nn(int m, const float4* __restrict__ cl_lo,
-                                                const float4* __restrict__ cl_hi, int* __restrict__ nn) {
-    __shared__ float4 slo[kB + 2 * kRadius], shi[kB + 2 * kRadius];
+                                                const float4* __restrict__ cl_hi, int* __restrict__ nn, int kRadius) {
+    __shared__ float4 slo[kB + 2 * kMaxRadius], shi[kB + 2 * kMaxRadius];
     const int b0 = blockIdx.x * kB;
     for (int k = threadIdx.x; k < kB + 2 * kRadius; k += kB) {
         const int j = b0 - kRadius + k;
@@ -134,7 +134,8 @@ __global__ __launch_bounds__(kB) void k_ploc_compact(int m, const int* __restric
 __global__ __launch_bounds__(kB) void k_ploc_cost(int n, const float4* __restrict__ nlo,
                                                   const float4* __restrict__ nhi, const int2* __restrict__ kids,
                                                   const int* __restrict__ parent, int* count, float* cost,
-                                                  int* collapse, int* flags, int leaf_max) {
+                                                  int* collapse, int* flags, int leaf_max, float kCostTri) {
+    constexpr float kCostNode = 1.0f;
     const int i = blockIdx.x * kB + threadIdx.x;
     if (i >= n) return;
     count[i] = 1;
@@ -221,6 +222,11 @@ __global__ __launch_bounds__(kB) void k_ploc_tris(const float* __restrict__ pos,
 void build_ploc(const float* pos, const float4* rlo, const float4* rhi, const int* order, int n, float4* tri,
                 BvhNode* nodes, BuildOut* out, int* iterations, hipStream_t stream) {
     const int total = 2 * n - 1;
+    // build knobs (A/B): PGRT_PLOC_RADIUS (<= 64), PGRT_SAH_TRI (triangle-test cost / node step)
+    const char* er = getenv("PGRT_PLOC_RADIUS");
+    const int radius = er ? std::max(1, std::min(kMaxRadius, atoi(er))) : kDefaultRadius;
+    const char* ec = getenv("PGRT_SAH_TRI");
+    const float cost_tri = ec ? (float)atof(ec) : kDefaultCostTri;
     DevBuf<float4> nlo, nhi, cl_lo[2], cl_hi[2];
     DevBuf<int2> kids;
     DevBuf<int> parent, cl_node[2], nn, count, collapse, flags, offset, misc;
@@ -250,7 +256,7 @@ void build_ploc(const float* pos, const float4* rlo, const float4* rhi, const in
     unsigned long long tail[2];
     while (m > 1) {
         const int g = ceil_div(m, kB);
-        hipLaunchKernelGGL(k_ploc_nn, dim3(g), dim3(kB), 0, stream, m, cl_lo[cur].p, cl_hi[cur].p, nn.p);
+        hipLaunchKernelGGL(k_ploc_nn, dim3(g), dim3(kB), 0, stream, m, cl_lo[cur].p, cl_hi[cur].p, nn.p, radius);
         hipLaunchKernelGGL(k_ploc_flags, dim3(g), dim3(kB), 0, stream, m, nn.p, packed.p);
         size_t sb = scan_bytes;
         PGRT_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp.p, sb, packed.p, scanned.p, m, stream));
@@ -278,7 +284,7 @@ void build_ploc(const float* pos, const float4* rlo, const float4* rhi, const in
     PGRT_HIP(hipMemsetAsync(flags.p, 0, sizeof(int) * total, stream));
     PGRT_HIP(hipMemsetAsync(misc.p, 0, sizeof(int) * 4, stream));
     hipLaunchKernelGGL(k_ploc_cost, dim3(grid), dim3(kB), 0, stream, n, nlo.p, nhi.p, kids.p, parent.p, count.p,
-                       cost.p, collapse.p, flags.p, out->leaf_max);
+                       cost.p, collapse.p, flags.p, out->leaf_max, cost_tri);
     hipLaunchKernelGGL(k_ploc_offsets, dim3(ceil_div(total, kB)), dim3(kB), 0, stream, total, kids.p, parent.p,
                        count.p, offset.p, misc.p);
     if (n >= 2)

@@ -178,12 +178,23 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
                 float t0, t1;
                 const bool h0 = box_hit(a.x, a.y, a.z, a.w, c.x, c.y, idx, idy, idz, oix, oiy, oiz, best_t, t0);
                 const bool h1 = box_hit(b.x, b.y, b.z, b.w, c.z, c.w, idx, idy, idz, oix, oiy, oiz, best_t, t1);
-                if (!h0 && !h1) {
-                    node = POP();
-                } else {
+                if constexpr (!SPILL) {
+                    // branch-light form: the stack top is read unconditionally (it is the pop
+                    // target when neither child is hit), the far child pushed under exec mask
+                    const int top = lstack[sp * kTraceBlock + tid];
+                    const bool any = h0 || h1;
                     const bool first0 = h0 && (!h1 || t0 <= t1);
-                    node = first0 ? d.x : d.y;
                     if (h0 && h1) PUSH(first0 ? d.y : d.x);
+                    node = any ? (first0 ? d.x : d.y) : top;
+                    sp -= any ? 0 : 1;
+                } else {
+                    if (!h0 && !h1) {
+                        node = POP();
+                    } else {
+                        const bool first0 = h0 && (!h1 || t0 <= t1);
+                        node = first0 ? d.x : d.y;
+                        if (h0 && h1) PUSH(first0 ? d.y : d.x);
+                    }
                 }
                 if (node < 0 && leaf == 0) {  // first leaf: park it and keep descending
                     leaf = node;
@@ -597,10 +608,110 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8g(SceneView s, const floa
     }
 }
 
+
+// ---------------------------------------------------------------- wave packets (primary rays)
+//
+// Level 0 holds coherent rays: one wave = one 8x8 pixel block (or one pixel's samples).  Here the
+// wave traverses the binary BVH as one packet: a single wave-uniform node stream (the union of
+// its rays' paths), every node and triangle fetched ONCE per wave by scalar loads into SGPRs
+// (constant address space), each lane testing its own ray against them.  A child is entered
+// when any lane's ray hits it (ballot), nearer-first by majority vote; each lane keeps its own
+// closest hit, so results are the one-lane kernel's.  No per-lane gathers go through the
+// texture path, and the per-lane state is small (no node data in VGPRs).
+typedef const __attribute__((address_space(4))) float* cfloat_ptr;
+__device__ __forceinline__ float4 cload4(cfloat_ptr p) { return make_float4(p[0], p[1], p[2], p[3]); }
+constexpr int kPktStack = 64;  // wave-uniform stack entries (>= BVH depth + 2)
+
+template <bool COUNT>
+__global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const float4* __restrict__ ro,
+                                                           const float4* __restrict__ rd, float4* __restrict__ hits,
+                                                           const int* __restrict__ count_dev, int count_terms,
+                                                           int count_host, int cap,
+                                                           unsigned long long* __restrict__ counters) {
+    __shared__ int wstack[kTraceBlock / 64][kPktStack];
+    const int wib = threadIdx.x >> 6;
+    const int lane = __lane_id();
+    const int n = ray_count(count_dev, count_terms, count_host, cap);
+    const cfloat_ptr nodes = (cfloat_ptr)(const void*)s.nodes;  // 16 floats per node
+    const cfloat_ptr tris = (cfloat_ptr)(const void*)s.tri;     // 12 floats per triangle
+    unsigned long long nvis = 0, ntest = 0;
+    for (int base = (blockIdx.x * (kTraceBlock / 64) + wib) * 64; base < n;
+         base += gridDim.x * kTraceBlock) {
+        const int i = base + lane;
+        const bool valid = i < n;
+        float4 o4 = make_float4(0, 0, 0, 0), d4 = make_float4(0, 0, 1, -1.0f);
+        if (valid) {
+            o4 = ro[i];
+            d4 = rd[i];
+        }
+        const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
+        const float dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
+        const float sdx = fabsf(dx) < 1e-30f ? copysignf(1e-30f, dx) : dx;
+        const float sdy = fabsf(dy) < 1e-30f ? copysignf(1e-30f, dy) : dy;
+        const float sdz = fabsf(dz) < 1e-30f ? copysignf(1e-30f, dz) : dz;
+        const float idx = __builtin_amdgcn_rcpf(sdx), idy = __builtin_amdgcn_rcpf(sdy),
+                    idz = __builtin_amdgcn_rcpf(sdz);
+        const float oix = ox * idx, oiy = oy * idy, oiz = oz * idz;
+        const bool live = valid && tfar >= 0.0f;  // padding slots / empty segments never hit
+        float best_t = live ? tfar : -1.0f;       // a dead lane's boxes all miss (t1 < 0 <= t0)
+        float best_u = 0.0f, best_v = 0.0f;
+        int best_prim = -1;
+        int sp = 0;
+        int node = s.root;
+        if (__ballot(live) == 0ull) node = kSentinel;
+        unsigned rvis = 0, rtest = 0;
+        for (;;) {
+            node = __builtin_amdgcn_readfirstlane(node);  // wave-uniform by construction
+            if (node == kSentinel) break;
+            if (node >= 0) {  // internal node (wave-uniform)
+                const cfloat_ptr nd = nodes + 16 * node;
+                const float4 a = cload4(nd), b = cload4(nd + 4), c = cload4(nd + 8);
+                const int4 d = make_int4(__float_as_int(nd[12]), __float_as_int(nd[13]), __float_as_int(nd[14]),
+                                         __float_as_int(nd[15]));
+                if (COUNT) ++rvis;
+                float t0, t1;
+                const bool h0 = box_hit(a.x, a.y, a.z, a.w, c.x, c.y, idx, idy, idz, oix, oiy, oiz, best_t, t0);
+                const bool h1 = box_hit(b.x, b.y, b.z, b.w, c.z, c.w, idx, idy, idz, oix, oiy, oiz, best_t, t1);
+                const unsigned long long b0 = __ballot(h0), b1 = __ballot(h1);
+                if (b0 == 0ull && b1 == 0ull) {
+                    node = sp > 0 ? wstack[wib][--sp] : kSentinel;
+                } else if (b0 != 0ull && b1 != 0ull) {
+                    // nearer first, by majority of the lanes that hit both
+                    const unsigned long long near0 = __ballot(h0 && h1 && t0 <= t1);
+                    const unsigned long long both = b0 & b1;
+                    const bool first0 = 2 * __popcll(near0) >= __popcll(both);
+                    wstack[wib][sp++] = first0 ? d.y : d.x;
+                    node = first0 ? d.x : d.y;
+                } else {
+                    node = b0 != 0ull ? d.x : d.y;
+                }
+            } else {  // leaf: its triangles against every lane's ray
+                const int first = leaf_first(node), end = first + leaf_count(node);
+                for (int k = first; k < end; ++k) {
+                    const cfloat_ptr q = tris + 12 * k;
+                    const float4 q0 = cload4(q), q1 = cload4(q + 4), q2 = cload4(q + 8);
+                    if (COUNT) ++rtest;
+                    if (live) tri_test(q0, q1, q2, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v, best_prim);
+                }
+                node = sp > 0 ? wstack[wib][--sp] : kSentinel;
+            }
+        }
+        if (valid) hits[i] = make_float4(live ? best_t : tfar, best_u, best_v, __int_as_float(best_prim));
+        if (COUNT && lane == 0) {
+            nvis += rvis;
+            ntest += rtest;
+        }
+    }
+    if (COUNT && lane == 0) {  // per-wave counts (one packet step = one node visit)
+        atomicAdd(&counters[0], nvis);
+        atomicAdd(&counters[1], ntest);
+    }
+}
+
 void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4* hits, const int* count_dev,
                   int count_host, int max_count, int* fetch, int* gstack, int gstack_threads,
                   unsigned long long* counters, bool count, hipStream_t stream, int expect, int count_terms,
-                  bool allow_group) {
+                  bool allow_group, bool coherent) {
     if (max_count <= 0) return;
     static const bool force_spill = getenv("PGRT_FORCE_SPILL") != nullptr;  // A/B of the stack layout
     if (s.wide) {
@@ -615,6 +726,22 @@ void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4
         return;
     }
     // small queues: 8 lanes per ray over the 8-wide BVH (PGRT_GROUP_MAX: largest queue, rays)
+    static const bool packets = [] {  // PGRT_PACKETS=0: level 0 on the one-lane kernel too
+        const char* e = getenv("PGRT_PACKETS");
+        return !(e && atoi(e) == 0);
+    }();
+    if (coherent && packets && !s.wide && s.root >= 0 && s.depth + 2 <= kPktStack) {
+        const int exg = expect > 0 && expect < max_count ? expect : max_count;
+        int grid = ceil_div(exg, kTraceBlock);
+        if (grid > 16384) grid = 16384;
+        if (count)
+            hipLaunchKernelGGL((k_trace_pkt<true>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
+                               count_dev, count_terms, count_host, max_count, counters);
+        else
+            hipLaunchKernelGGL((k_trace_pkt<false>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
+                               count_dev, count_terms, count_host, max_count, counters);
+        return;
+    }
     const int group_max = s.group_max;
     static const int group8_max = [] {
         const char* e = getenv("PGRT_GROUP8_MAX");  // r1 A/B: 4 lanes on level 1, 8 below

@@ -65,7 +65,7 @@ struct ShadowQueue {  // one per batch: the shadow rays of every level, level-ma
 void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4* hits, const int* count_dev,
                   int count_host, int max_count, int* fetch, int* gstack, int gstack_threads,
                   unsigned long long* counters, bool count, hipStream_t stream, int expect = 0,
-                  int count_terms = 1, bool allow_group = true);
+                  int count_terms = 1, bool allow_group = true, bool coherent = false);
 int trace_block_size();
 
 // `expect` sizes the grid of a grid-stride kernel (counts live on the device; any value is

@@ -18,8 +18,13 @@ from pgi_raytracing_amd.raytracer import Context, load_obj  # noqa: E402
 def main():
     a = [int(x) for x in sys.argv[1:]] + [1920, 1080, 5, 1, 0][len(sys.argv) - 1:]
     W, H, d, S, dof = a[:5]
-    sc = load_obj(scenes.AVENGER_OBJ)
-    sc.set_environment(os.path.join(ROOT, "assets", "spherical_map_windows.jpg"))
+    env = os.path.join(ROOT, "assets", "spherical_map_windows.jpg")
+    c5 = os.environ.get("DIAG_SCENE") == "c5"  # BASELINE C5: 10^6 random triangles
+    if c5:
+        sc = scenes.random_scene(1_000_000, 42, env)
+    else:
+        sc = load_obj(scenes.AVENGER_OBJ)
+        sc.set_environment(env)
     ctx = Context(0)
     t = time.time()
     ctx.set_scene(sc)
@@ -27,7 +32,10 @@ def main():
     print(json.dumps({"bvh": {"builder": ["lbvh", "ploc"][info.builder], "iters": info.build_iterations,
                               "tris": info.num_triangles, "nodes": info.num_nodes, "depth": info.max_depth,
                               "width": info.width, "refs": info.num_references, "split": round(info.split_beta, 3), "build_ms": round(info.build_ms, 3), "set_scene_s": round(time.time() - t, 3)}}))
-    ctx.set_camera(abi.default_camera(W, H))
+    if c5:
+        ctx.set_camera(abi.make_camera(W, H, abi.deg2rad(42.185), (-140.0, -175.0, 80.0), (0.0, 0.0, 0.0)))
+    else:
+        ctx.set_camera(abi.default_camera(W, H))
     p = abi.make_params(spp_side=S, max_level=d, dof=dof,
                         jitter=abi.PGRT_JITTER_HASH if S > 1 or dof else abi.PGRT_JITTER_NONE)
     ctx.render(p)
