@@ -184,6 +184,12 @@ int pgrt_synchronize(pgrt_ctx* ctx);
  * is the global triangle index stored as int32 bits, -1 on a miss (t = tfar, u = v = 0). */
 int pgrt_intersect_closest(pgrt_ctx* ctx, const float* rays, int n, float* hits);
 
+/* ---- batched occlusion query with rtcOccluded1 semantics (rtcore_scene.h:120; Embree marks an
+ * occluded ray by setting tfar = -inf): occluded[i] = 1 when ANY triangle is hit with t in
+ * (tnear, tfar], else 0.  Same ray layout as pgrt_intersect_closest; the traversal stops at the
+ * first accepted triangle. */
+int pgrt_occluded(pgrt_ctx* ctx, const float* rays, int n, int* occluded);
+
 /* ---- multi-GPU image tiles (one process per GPU, RCCL over xGMI) ----
  * Tiles are tile_size x tile_size, numbered row-major; tile t belongs to rank t % world. */
 int pgrt_tile_count(int width, int height, int tile_size, int rank, int world);

@@ -122,12 +122,25 @@ PGRT_HD double pg_pow_pos(double x, double y)
     return pg_exp(y * pg_log_pos(x));
 }
 
+/* x^n for 0 < n <= 64 by squaring (each product rounded once, IEEE double) */
+PGRT_HD double pg_ipow_d(double x, int n)
+{
+    double acc = 1.0;
+    while (n) {
+        if (n & 1) acc *= x;
+        n >>= 1;
+        if (n) x *= x;
+    }
+    return acc;
+}
+
 /* pow(double, double) for finite arguments with an integer or positive-base case split
  * (the Fresnel-like R of raytracer.cpp:316 raises 1 - |cos| to the 5th power in double). */
 PGRT_HD double pg_pow_d(double x, double y)
 {
     if (y == 0.0 || x == 1.0) return 1.0;
     if (x != x || y != y) return x + y;
+    if (x > 0.0 && y >= 1.0 && y <= 64.0 && pg_floor_d(y) == y) return pg_ipow_d(x, (int)y); /* (1-cos)^5 */
     if (x > 0.0) return pg_exp(y * pg_log_pos(x));
     double fy = pg_floor_d(y);
     int odd = (fy == y) && (pg_fabs_d(y) < 9007199254740992.0) &&
@@ -177,6 +190,15 @@ PGRT_HD float pg_powf(float x, float y)
     /* y = 1/2 (the gamma slider default): the correctly rounded sqrtf, identical on both
      * targets; exp(log/2) in double misrounds 48 of the 2^31 positive floats (checked) */
     if (y == 0.5f) return sqrtf(x);
+    if (yint != 0 && ay <= 64.0f) {
+        /* small integer exponent (Phong's Ns, raytracer.cpp:374-382): exponentiation by
+         * squaring in double, <= 63 roundings of 2^-53 -> within 1 ulp after the final rounding,
+         * and ~20x cheaper than exp(y log x) in double on both targets */
+        double r = pg_ipow_d((double)ax, (int)ay);
+        if (y < 0) r = 1.0 / r;
+        float rf = (float)r;
+        return (neg && yint == 2) ? -rf : rf;
+    }
     double r = pg_exp((double)y * pg_log_pos((double)ax));
     float rf = (float)r;
     return (neg && yint == 2) ? -rf : rf;

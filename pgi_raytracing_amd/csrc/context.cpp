@@ -495,6 +495,10 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
         const char* e = getenv("PGRT_STAGGER_LEVEL");
         return e ? atoi(e) : -1;
     }();
+    static const int packet_levels = [] {  // levels traced as wave packets (A/B knob)
+        const char* e = getenv("PGRT_PACKET_LEVELS");
+        return e ? atoi(e) : 0;
+    }();
     const int K = std::max(1, std::min(want_slots, ntiles));
     while ((int)ctx->slots.size() < K) ctx->slots.emplace_back(new FrameSlot());
     ctx->timer.on = p->profile > 0;
@@ -564,7 +568,7 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
                     id = ctx->timer.begin(s, CAT_TRACE, CAT_LTRACE + L);
                     launch_trace(ctx->view, qc.ro, qc.rd, qc.hit, &fcd->count[L], 0, maxc, &fcd->fetch[L],
                                  sl->gstack.p, kTraceGridThreads, fcd->trav[L], p->profile >= 2, s, ex, 1, true,
-                                 L == 0);  // level 0: coherent 8x8-pixel waves -> packet traversal
+                                 L <= packet_levels);  // coherent 8x8-pixel waves -> packet traversal
                     ctx->timer.end(s, id);
                     ++trace_launches;
                     id = ctx->timer.begin(s, CAT_SHADE, CAT_LSHADE + L);
@@ -857,6 +861,31 @@ int pgrt_intersect_closest(pgrt_ctx* ctx, const float* rays, int n, float* hits)
                      kTraceGridThreads, nullptr, false, ctx->stream);
         PGRT_HIP(hipGetLastError());
         PGRT_HIP(hipMemcpyAsync(hits, h.p, sizeof(float4) * n, hipMemcpyDeviceToHost, ctx->stream));
+        PGRT_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int pgrt_occluded(pgrt_ctx* ctx, const float* rays, int n, int* occluded) {
+    if (!ctx || n < 0 || (n > 0 && (!rays || !occluded))) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        PGRT_REQUIRE(ctx->has_scene, PGRT_ERR_NO_SCENE, "pgrt_set_scene has not been called");
+        if (n == 0) return;
+        DevBuf<float4> ro, rd;
+        DevBuf<int> occ;
+        ro.alloc(n);
+        rd.alloc(n);
+        occ.alloc(n);
+        std::vector<float4> a(n), b(n);
+        for (int i = 0; i < n; ++i) {
+            const float* r = rays + 8 * (size_t)i;
+            a[i] = make_float4(r[0], r[1], r[2], r[3]);
+            b[i] = make_float4(r[4], r[5], r[6], r[7]);
+        }
+        PGRT_HIP(hipMemcpyAsync(ro.p, a.data(), sizeof(float4) * n, hipMemcpyHostToDevice, ctx->stream));
+        PGRT_HIP(hipMemcpyAsync(rd.p, b.data(), sizeof(float4) * n, hipMemcpyHostToDevice, ctx->stream));
+        launch_occluded(ctx->view, ro.p, rd.p, n, occ.p, ctx->stream);
+        PGRT_HIP(hipGetLastError());
+        PGRT_HIP(hipMemcpyAsync(occluded, occ.p, sizeof(int) * n, hipMemcpyDeviceToHost, ctx->stream));
         PGRT_HIP(hipStreamSynchronize(ctx->stream));
     });
 }

@@ -793,6 +793,76 @@ void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4
 #undef PGRT_LAUNCH
 }
 
+
+// ---------------------------------------------------------------- any hit (rtcOccluded1)
+//
+// Embree's occlusion query (rtcore_scene.h: rtcOccluded1): is there ANY triangle hit with t in
+// (tnear, tfar]?  One lane per ray over the binary BVH, LDS stack sized to the tree depth,
+// nearer child first, and the traversal stops at the first accepted triangle.  The per-triangle
+// acceptance is the closest-hit kernel's (tri_test), so occluded == (closest hit exists).
+__global__ __launch_bounds__(kTraceBlock) void k_occluded(SceneView s, const float4* __restrict__ ro,
+                                                          const float4* __restrict__ rd, int n,
+                                                          int* __restrict__ occluded) {
+    extern __shared__ int lstack[];  // [depth + 2][kTraceBlock]
+    const int tid = threadIdx.x;
+    for (int i = blockIdx.x * kTraceBlock + tid; i < n; i += gridDim.x * kTraceBlock) {
+        const float4 o4 = ro[i];
+        const float4 d4 = rd[i];
+        const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
+        const float dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
+        const float sdx = fabsf(dx) < 1e-30f ? copysignf(1e-30f, dx) : dx;
+        const float sdy = fabsf(dy) < 1e-30f ? copysignf(1e-30f, dy) : dy;
+        const float sdz = fabsf(dz) < 1e-30f ? copysignf(1e-30f, dz) : dz;
+        const float idx = __builtin_amdgcn_rcpf(sdx), idy = __builtin_amdgcn_rcpf(sdy),
+                    idz = __builtin_amdgcn_rcpf(sdz);
+        const float oix = ox * idx, oiy = oy * idy, oiz = oz * idz;
+        int hit = 0;
+        int sp = 0;
+        lstack[tid] = kSentinel;
+        int node = (tfar >= 0.0f) ? s.root : kSentinel;
+        while (node != kSentinel && !hit) {
+            if (node >= 0) {
+                const BvhNode* nd = s.nodes + node;
+                const float4 a = nd->a, b = nd->b, c = nd->c;
+                const int4 d = nd->d;
+                float t0, t1;
+                const bool h0 = box_hit(a.x, a.y, a.z, a.w, c.x, c.y, idx, idy, idz, oix, oiy, oiz, tfar, t0);
+                const bool h1 = box_hit(b.x, b.y, b.z, b.w, c.z, c.w, idx, idy, idz, oix, oiy, oiz, tfar, t1);
+                if (h0 && h1) {
+                    const bool first0 = t0 <= t1;
+                    lstack[++sp * kTraceBlock + tid] = first0 ? d.y : d.x;
+                    node = first0 ? d.x : d.y;
+                } else if (h0 || h1) {
+                    node = h0 ? d.x : d.y;
+                } else {
+                    node = lstack[(sp--) * kTraceBlock + tid];
+                }
+            } else {
+                const int first = leaf_first(node), end = first + leaf_count(node);
+                for (int k = first; k < end && !hit; ++k) {
+                    float bt = tfar, bu = 0.0f, bv = 0.0f;
+                    int bp = -1;
+                    tri_test(s.tri[3 * k], s.tri[3 * k + 1], s.tri[3 * k + 2], ox, oy, oz, dx, dy, dz, tnear, tfar,
+                             bt, bu, bv, bp);
+                    hit = bp >= 0;
+                }
+                node = lstack[(sp--) * kTraceBlock + tid];
+            }
+        }
+        occluded[i] = hit;
+    }
+}
+
+void launch_occluded(const SceneView& s, const float4* ro, const float4* rd, int n, int* occluded,
+                     hipStream_t stream) {
+    if (n <= 0) return;
+    PGRT_REQUIRE(s.depth + 2 <= 64, PGRT_ERR_INVALID_ARGUMENT, "BVH too deep for the any-hit stack");
+    int grid = ceil_div(n, kTraceBlock);
+    if (grid > 16384) grid = 16384;
+    const size_t lds = (size_t)(s.depth + 2) * kTraceBlock * sizeof(int);
+    hipLaunchKernelGGL(k_occluded, dim3(grid), dim3(kTraceBlock), lds, stream, s, ro, rd, n, occluded);
+}
+
 int trace_block_size() { return kTraceBlock; }
 
 }  // namespace pgrt

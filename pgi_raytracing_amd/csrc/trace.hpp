@@ -67,6 +67,9 @@ void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4
                   unsigned long long* counters, bool count, hipStream_t stream, int expect = 0,
                   int count_terms = 1, bool allow_group = true, bool coherent = false);
 int trace_block_size();
+// any-hit query (rtcOccluded1 semantics): occluded[i] = 1 when some triangle is hit in (tnear, tfar]
+void launch_occluded(const SceneView& s, const float4* ro, const float4* rd, int n, int* occluded,
+                     hipStream_t stream);
 
 // `expect` sizes the grid of a grid-stride kernel (counts live on the device; any value is
 // correct, a good guess -- last frame's count -- avoids dispatching empty workgroups)

@@ -53,6 +53,7 @@ def lib():
         "pgrt_copy_to_host": (ip, [vp, vp, vp, C.c_size_t]),
         "pgrt_synchronize": (ip, [vp]),
         "pgrt_intersect_closest": (ip, [vp, fp, ip, fp]),
+        "pgrt_occluded": (ip, [vp, fp, ip, C.POINTER(C.c_int)]),
         "pgrt_tile_count": (ip, [ip, ip, ip, ip, ip]),
         "pgrt_tile_rect": (ip, [ip, ip, ip, ip, C.POINTER(C.c_int)]),
         "pgrt_unpack_tiles_host": (ip, [ip, ip, ip, ip, fp, fp]),
@@ -163,6 +164,14 @@ class Context:
         hits = np.zeros((rays.shape[0], 4), np.float32)
         _check(self.h, self.L.pgrt_intersect_closest(self.h, abi.fptr(rays), rays.shape[0], abi.fptr(hits)))
         return hits
+
+    def occluded(self, rays: np.ndarray) -> np.ndarray:
+        """rtcOccluded1 over a batch: rays (n, 8) -> (n,) bool, any hit in (tnear, tfar]."""
+        rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+        occ = np.zeros(rays.shape[0], np.int32)
+        _check(self.h, self.L.pgrt_occluded(self.h, abi.fptr(rays), rays.shape[0],
+                                            occ.ctypes.data_as(C.POINTER(C.c_int))))
+        return occ.astype(bool)
 
     def frame_diag(self) -> list:
         """Per-level counters of the last frame (traversal counts need params.profile == 2)."""
@@ -275,3 +284,6 @@ class Raytracer:
 
     def intersect(self, rays):
         return self.ctx.intersect(rays)
+
+    def occluded(self, rays):
+        return self.ctx.occluded(rays)

@@ -65,3 +65,19 @@ def test_double_pow_for_srgb():
     out = _eval(u, np.full_like(u, 1 / 2.4))
     ref = np.power(u.astype(np.float64), np.float64(np.float32(1 / 2.4)))
     assert np.max(np.abs(out[:, 7] - ref) / ref) < 1.2e-7
+
+
+def test_integer_exponent_fast_path():
+    """pg_powf / pg_pow_d with small integer exponents (Phong Ns = 32, Fresnel (1-cos)^5) use
+    exponentiation by squaring in double: still within 1 ulp of the float64 reference."""
+    rng = np.random.default_rng(5)
+    a = np.concatenate([rng.uniform(-1, 1, 20000), rng.uniform(0, 1.5, 5000), [0.0, -0.0, 1.0, -1.0]])
+    a = a.astype(np.float32)
+    for e in (1, 2, 3, 5, 32, 63, 64, -3):
+        out = _eval(a, np.full_like(a, e))
+        with np.errstate(all="ignore"):
+            ref = np.power(a.astype(np.float64), float(e))
+        ok = np.isfinite(ref) & (np.abs(ref) < 3e38) & ((np.abs(ref) > 1.2e-38) | (ref == 0))
+        assert (_ulps(out[ok, 2], ref[ok]) <= 1).all(), e
+        pos = ok & (a > 0)
+        assert (_ulps(out[pos, 7], ref[pos]) <= 1).all(), e

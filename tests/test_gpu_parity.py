@@ -215,3 +215,18 @@ def test_bvh_layouts_bit_exact(gpu_ctx, avenger_scene, monkeypatch, builder, wid
         monkeypatch.delenv("PGRT_SPLIT")
         monkeypatch.delenv("PGRT_GROUP_MAX")
         gpu_ctx.set_scene(avenger_scene)
+
+
+def test_occluded_matches_closest_hit(gpu_ctx, avenger_scene):
+    """rtcOccluded1 analogue: any hit in (tnear, tfar] exactly when the closest-hit query (oracle)
+    finds one -- including finite-tfar shadow-style rays that stop short of the geometry."""
+    gpu_ctx.set_scene(avenger_scene)
+    rays = _random_rays(avenger_scene, 20000, 21)
+    short = rays.copy()
+    short[:, 7] = np.float32(5.0)  # tfar 5: most rays stop before any triangle
+    rays = np.concatenate([rays, short])
+    occ = gpu_ctx.occluded(rays)
+    ho = _oracle(avenger_scene).intersect(rays)
+    expect = ho[:, 3].view(np.int32) >= 0
+    assert (occ == expect).all(), f"{(occ != expect).sum()} differ"
+    assert 1000 < occ.sum() < len(occ) - 1000
