@@ -179,6 +179,15 @@ int pgrt_device_free(pgrt_ctx* ctx, void* ptr);
 int pgrt_copy_to_host(pgrt_ctx* ctx, void* dst_host, const void* src_device, size_t bytes);
 int pgrt_synchronize(pgrt_ctx* ctx);
 
+/* ---- frame sink (replaces the Producer's endless re-render, simpleguidx11.cpp:86-128, with a
+ *      progressive average): each call renders one frame (use a new params.frame per call so the
+ *      jitter / lens samples differ), adds it to a device running sum in call order and writes
+ *      the running mean (W*H*4 floats, or the rect) to mean_host when not NULL.  *frames receives
+ *      the number of frames in the sum.  A different frame size or pgrt_accumulate_reset restarts. */
+int pgrt_accumulate_reset(pgrt_ctx* ctx);
+int pgrt_render_accumulate(pgrt_ctx* ctx, const pgrt_render_params* p, float* mean_host, int* frames,
+                           pgrt_stats* st);
+
 /* ---- batched closest-hit query with rtcIntersect1 semantics ----
  * rays: n x 8 floats {org.xyz, tnear, dir.xyz, tfar}; hits: n x 4 {t, u, v, prim} where prim
  * is the global triangle index stored as int32 bits, -1 on a miss (t = tfar, u = v = 0). */

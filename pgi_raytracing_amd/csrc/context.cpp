@@ -169,6 +169,10 @@ struct pgrt_ctx {
     int world = 1, rank = 0;
     DevBuf<float> tilebuf, gathered, fb_dev;
 
+    // frame sink (progressive accumulation)
+    DevBuf<float> acc_frame, acc_sum, acc_mean;
+    int acc_count = 0, acc_w = 0, acc_h = 0;
+
     ~pgrt_ctx() {
         if (comm) (void)ncclCommDestroy(comm);
         if (stream) (void)hipStreamDestroy(stream);
@@ -887,6 +891,43 @@ int pgrt_occluded(pgrt_ctx* ctx, const float* rays, int n, int* occluded) {
         PGRT_HIP(hipGetLastError());
         PGRT_HIP(hipMemcpyAsync(occluded, occ.p, sizeof(int) * n, hipMemcpyDeviceToHost, ctx->stream));
         PGRT_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+// ---- frame sink: progressive accumulation ----------------------------------------------------
+
+int pgrt_accumulate_reset(pgrt_ctx* ctx) {
+    if (!ctx) return PGRT_ERR_INVALID_ARGUMENT;
+    ctx->acc_count = 0;
+    return PGRT_OK;
+}
+
+int pgrt_render_accumulate(pgrt_ctx* ctx, const pgrt_render_params* p, float* mean_host, int* frames,
+                           pgrt_stats* st) {
+    if (!ctx || !p) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        PGRT_REQUIRE(ctx->has_cam, PGRT_ERR_NO_CAMERA, "pgrt_set_camera has not been called");
+        auto t0 = std::chrono::steady_clock::now();
+        int x, y, w, h;
+        frame_rect(ctx, p, x, y, w, h);
+        if (w != ctx->acc_w || h != ctx->acc_h) ctx->acc_count = 0;  // a new frame size restarts the sum
+        const size_t px = (size_t)w * h;
+        ctx->acc_frame.alloc(px * 4);
+        ctx->acc_sum.alloc(px * 4);
+        ctx->acc_mean.alloc(px * 4);
+        render_tiles(ctx, p, rect_tiles(x, y, w, h), ctx->acc_frame.p, 0, x, y, w, st);
+        ctx->acc_w = w;
+        ctx->acc_h = h;
+        ++ctx->acc_count;
+        launch_accumulate_frame(ctx->acc_frame.p, ctx->acc_sum.p, ctx->acc_mean.p, (long long)px, ctx->acc_count,
+                                ctx->stream);
+        PGRT_HIP(hipGetLastError());
+        if (mean_host)
+            PGRT_HIP(hipMemcpyAsync(mean_host, ctx->acc_mean.p, px * 4 * sizeof(float), hipMemcpyDeviceToHost,
+                                    ctx->stream));
+        PGRT_HIP(hipStreamSynchronize(ctx->stream));
+        if (frames) *frames = ctx->acc_count;
+        if (st) st->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     });
 }
 

@@ -442,6 +442,37 @@ void launch_unpack_tiles(const float* gathered, float* rgba, int width, int heig
                        world, tiles_per_rank);
 }
 
+// ------------------------------------------------------------------ progressive accumulation
+//
+// The reference's Producer re-renders forever (simpleguidx11.cpp:86-128) and shows the latest
+// frame; with jitter / DoF every frame is a new noisy estimate.  The frame sink keeps a running
+// sum of the resolved frames (accumulated in frame order, one add per frame) and its mean.
+__global__ __launch_bounds__(kBlock) void k_accumulate_frame(const float4* __restrict__ frame,
+                                                            float4* __restrict__ sum, float4* __restrict__ mean,
+                                                            long long n, int count) {
+    const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float4 f = frame[i];
+    float4 a = count == 1 ? f : sum[i];
+    if (count > 1) {
+        a.x += f.x;
+        a.y += f.y;
+        a.z += f.z;
+        a.w += f.w;
+    }
+    sum[i] = a;
+    const float c = (float)count;
+    mean[i] = make_float4(a.x / c, a.y / c, a.z / c, a.w / c);
+}
+
+void launch_accumulate_frame(const float* frame, float* sum, float* mean, long long pixels, int count,
+                             hipStream_t stream) {
+    if (pixels <= 0) return;
+    hipLaunchKernelGGL(k_accumulate_frame, dim3((unsigned)((pixels + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
+                       reinterpret_cast<const float4*>(frame), reinterpret_cast<float4*>(sum),
+                       reinterpret_cast<float4*>(mean), pixels, count);
+}
+
 // ------------------------------------------------------------------ math self-test
 
 __global__ void k_selftest(const float* in, int n, float* out) {

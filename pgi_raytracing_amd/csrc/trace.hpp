@@ -87,6 +87,9 @@ void launch_combine(const SceneView& s, int level, LevelNodes nodes, const float
 void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles, LevelNodes l0, const float4* child,
                    ShadowQueue sq, float4* accum, float* out, int out_mode, int ox, int oy, int pitch, int npix,
                    bool first, bool last, int K, int j, hipStream_t stream);
+// frame sink: sum += frame (count-th frame; count == 1 resets), mean = sum / count
+void launch_accumulate_frame(const float* frame, float* sum, float* mean, long long pixels, int count,
+                             hipStream_t stream);
 void launch_unpack_tiles(const float* gathered, float* rgba, int width, int height, int world, int tiles_per_rank,
                          hipStream_t stream);
 

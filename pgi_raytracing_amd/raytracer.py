@@ -54,6 +54,9 @@ def lib():
         "pgrt_synchronize": (ip, [vp]),
         "pgrt_intersect_closest": (ip, [vp, fp, ip, fp]),
         "pgrt_occluded": (ip, [vp, fp, ip, C.POINTER(C.c_int)]),
+        "pgrt_accumulate_reset": (ip, [vp]),
+        "pgrt_render_accumulate": (ip, [vp, C.POINTER(abi.RenderParams), fp, C.POINTER(C.c_int),
+                                        C.POINTER(abi.Stats)]),
         "pgrt_tile_count": (ip, [ip, ip, ip, ip, ip]),
         "pgrt_tile_rect": (ip, [ip, ip, ip, ip, C.POINTER(C.c_int)]),
         "pgrt_unpack_tiles_host": (ip, [ip, ip, ip, ip, fp, fp]),
@@ -164,6 +167,20 @@ class Context:
         hits = np.zeros((rays.shape[0], 4), np.float32)
         _check(self.h, self.L.pgrt_intersect_closest(self.h, abi.fptr(rays), rays.shape[0], abi.fptr(hits)))
         return hits
+
+    def accumulate_reset(self) -> None:
+        _check(self.h, self.L.pgrt_accumulate_reset(self.h))
+
+    def render_accumulate(self, params: abi.RenderParams):
+        """One more frame into the progressive average; returns (mean image, frames in the sum)."""
+        w = params.rect_w if params.rect_w > 0 else self.camera.width
+        h = params.rect_h if params.rect_h > 0 else self.camera.height
+        out = np.empty((h, w, 4), np.float32)
+        frames = C.c_int(0)
+        st = abi.Stats()
+        _check(self.h, self.L.pgrt_render_accumulate(self.h, C.byref(params), abi.fptr(out), C.byref(frames),
+                                                     C.byref(st)))
+        return out, frames.value
 
     def occluded(self, rays: np.ndarray) -> np.ndarray:
         """rtcOccluded1 over a batch: rays (n, 8) -> (n,) bool, any hit in (tnear, tfar]."""
@@ -276,6 +293,17 @@ class Raytracer:
             params = abi.make_params(**kw)
         self.frame, st = self.ctx.render(params)
         return self.frame, st
+
+    def render_progressive(self, frames: int, first_frame: int = 0, **kw):
+        """Producer loop as a frame sink (simpleguidx11.cpp:86-128): `frames` renders with
+        params.frame = first_frame, first_frame+1, ... averaged on the device; returns the mean."""
+        kw.setdefault("gamma_level", self.gamma_level)
+        self.ctx.accumulate_reset()
+        mean, n = None, 0
+        for f in range(first_frame, first_frame + frames):
+            mean, n = self.ctx.render_accumulate(abi.make_params(frame=f, **kw))
+        self.frame = mean
+        return mean, n
 
     def get_pixel(self, x: int, y: int, t: float = 0.0):  # noqa: ARG002 (t is unused, as in the reference)
         if self.frame is None:

@@ -230,3 +230,32 @@ def test_occluded_matches_closest_hit(gpu_ctx, avenger_scene):
     expect = ho[:, 3].view(np.int32) >= 0
     assert (occ == expect).all(), f"{(occ != expect).sum()} differ"
     assert 1000 < occ.sum() < len(occ) - 1000
+
+
+def test_progressive_accumulation_is_mean_of_frames(gpu_ctx, avenger_scene):
+    """Frame sink: the device running mean of 4 jittered DoF frames equals the float32 mean of
+    the same frames rendered one by one (same summation order), and a reset restarts it."""
+    gpu_ctx.set_scene(avenger_scene)
+    cam = abi.default_camera(96, 64)
+    gpu_ctx.set_camera(cam)
+    frames = []
+    for f in range(4):
+        p = abi.make_params(spp_side=1, max_level=3, dof=1, jitter=abi.PGRT_JITTER_HASH, frame=f)
+        img, _ = gpu_ctx.render(p)
+        frames.append(img)
+    gpu_ctx.accumulate_reset()
+    for f in range(4):
+        mean, n = gpu_ctx.render_accumulate(abi.make_params(spp_side=1, max_level=3, dof=1,
+                                                             jitter=abi.PGRT_JITTER_HASH, frame=f))
+    assert n == 4
+    acc = frames[0].copy()
+    for fr in frames[1:]:
+        acc = acc + fr
+    ref = acc / np.float32(4)
+    same = (mean == ref) | (np.isnan(mean) & np.isnan(ref))
+    assert same.all()
+    assert not (frames[0] == frames[1]).all()  # the jitter differs per frame
+    gpu_ctx.accumulate_reset()
+    m1, n1 = gpu_ctx.render_accumulate(abi.make_params(spp_side=1, max_level=3, dof=1, jitter=abi.PGRT_JITTER_HASH,
+                                                       frame=0))
+    assert n1 == 1 and ((m1 == frames[0]) | (np.isnan(m1) & np.isnan(frames[0]))).all()
