@@ -193,6 +193,19 @@ public:
         return st;
     }
 
+    // The Producer loop as a frame sink: one more frame (next jitter / lens sample set) into
+    // the device-side progressive mean, which becomes the frame get_pixel reads.
+    int RenderProgressive(bool restart = false) {
+        if (restart) check(ctx_, pgrt_accumulate_reset(ctx_), "pgrt_accumulate_reset");
+        params_.gamma_level = gamma_level;
+        frame_.resize((size_t)camera_.width_ * camera_.height_ * 4);
+        int frames = 0;
+        check(ctx_, pgrt_render_accumulate(ctx_, &params_, frame_.data(), &frames, nullptr),
+              "pgrt_render_accumulate");
+        ++params_.frame;
+        return frames;
+    }
+
     // get_pixel(x, y, t) (raytracer.cpp:396-437): reads the last rendered frame.
     Color4f get_pixel(const int x, const int y, const float /*t*/ = 0.0f) {
         if (frame_.empty()) Render();
@@ -212,6 +225,13 @@ public:
         check(ctx_, pgrt_intersect_closest(ctx_, rays.data(), (int)(rays.size() / 8), hits.data()),
               "pgrt_intersect_closest");
         return hits;
+    }
+
+    // rtcOccluded1 for a batch (any hit in (tnear, tfar])
+    std::vector<int> Occluded(const std::vector<float>& rays) {
+        std::vector<int> occ(rays.size() / 8);
+        check(ctx_, pgrt_occluded(ctx_, rays.data(), (int)(rays.size() / 8), occ.data()), "pgrt_occluded");
+        return occ;
     }
 
 private:
