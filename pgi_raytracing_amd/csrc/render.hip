@@ -124,6 +124,8 @@ void launch_raygen(const CameraView& cam, const FrameParams& fp, const int4* til
 
 __global__ __launch_bounds__(kBlock) void k_shade(SceneView s, FrameParams fp, int level, Queue q, Queue next,
                                                   LevelNodes nodes, ShadowQueue sq, FrameCounters* fc) {
+    __shared__ float lut255[256];
+    fill_byte_lut(lut255);
     const int n = min(fc->count[level], q.cap);
     const int tid = threadIdx.x;
     // one shadow queue for the whole batch: level L's rays follow those of levels < L (final by now)
@@ -155,7 +157,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(SceneView s, FrameParams fp, i
                 d = normalize(dirraw);
                 const int prim = __float_as_int(h.w);
                 if (prim < 0) {
-                    color = env_texel(s, d);  // miss (raytracer.cpp:390-393)
+                    color = env_texel(s, lut255, d);  // miss (raytracer.cpp:390-393)
                 } else {
                     t = h.x;
                     const float* a = s.attr + 16 * (size_t)prim;
@@ -211,7 +213,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(SceneView s, FrameParams fp, i
                         } else {
                             const float tu = interp1(a[9], a[11], a[13], u, v);
                             const float tv = interp1(a[10], a[12], a[14], u, v);
-                            const V3 tx = tex_texel(s.tex[m.tex], s.texels, tu, 1.0f - tv);
+                            const V3 tx = tex_texel(s.tex[m.tex], s.texels, lut255, tu, 1.0f - tv);
                             m_d_r = tx.x;
                             m_d_g = tx.y;
                             m_d_b = tx.z;

@@ -49,17 +49,25 @@ __device__ __forceinline__ float interp1(float a0, float a1, float a2, float u, 
     return fmaf(w, a0, fmaf(u, a1, v * a2));
 }
 
+// byte / 255.0f for every byte value, filled per block (k_shade) with the same correctly
+// rounded division the reference performs per channel: a table read instead of a division
+__device__ __forceinline__ void fill_byte_lut(float* lut) {
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) lut[i] = (float)i / 255.0f;
+    __syncthreads();
+}
+
 // Texture::get_pixel (APP/texture.cpp:56-62): Color3f{B,G,R}/255; bytes outside the decoded
-// buffer read as 0 (the reference reads out of bounds there).
-__device__ __forceinline__ V3 tex_pixel(const DevTexture& t, const unsigned char* pool, int x, int y) {
+// buffer read as 0 (the reference reads out of bounds there).  lut[b] == b / 255.0f.
+__device__ __forceinline__ V3 tex_pixel(const DevTexture& t, const unsigned char* pool, const float* lut, int x,
+                                        int y) {
     long long off = (long long)y * t.pitch + (long long)x * t.bpp;
     if (off < 0 || off + 2 >= t.size) return v3(0, 0, 0);
     const unsigned char* p = pool + t.offset + off;
-    return v3(p[0] / 255.0f, p[1] / 255.0f, p[2] / 255.0f);
+    return v3(lut[p[0]], lut[p[1]], lut[p[2]]);
 }
 
 // Texture::get_texel (APP/texture.cpp:77-130): bilinear with the reference's edge quirks.
-__device__ inline V3 tex_texel(const DevTexture& t, const unsigned char* pool, float u, float v) {
+__device__ inline V3 tex_texel(const DevTexture& t, const unsigned char* pool, const float* lut, float u, float v) {
     const float x = u * (float)t.width;
     const float y = v * (float)t.height;
     if (!(fabsf(x) < 16777216.0f) || !(fabsf(y) < 16777216.0f)) return v3(0, 0, 0);
@@ -70,25 +78,28 @@ __device__ inline V3 tex_texel(const DevTexture& t, const unsigned char* pool, f
     const int y1 = (tmp_y1 < 1) ? tmp_y1 + 1 : tmp_y1;
     const int y2 = (tmp_y2 == t.height) ? tmp_y1 : tmp_y2;
     if (x1 == x2 || y1 == y2) return v3(0, 0, 0);
-    const V3 x1y1 = tex_pixel(t, pool, x1, y1), x2y1 = tex_pixel(t, pool, x2, y1);
-    const V3 x1y2 = tex_pixel(t, pool, x1, y2), x2y2 = tex_pixel(t, pool, x2, y2);
-    const float Q11 = ((float)x2 - x) / (float)(x2 - x1);
-    const float Q21 = (x - (float)x1) / (float)(x2 - x1);
+    const V3 x1y1 = tex_pixel(t, pool, lut, x1, y1), x2y1 = tex_pixel(t, pool, lut, x2, y1);
+    const V3 x1y2 = tex_pixel(t, pool, lut, x1, y2), x2y2 = tex_pixel(t, pool, lut, x2, y2);
+    // the denominators are 1 except at the wrap / clamp quirks: q / 1 == q exactly, so the
+    // (correctly rounded, ~10-instruction) division only runs where it can change the value
+    const float dx = (float)(x2 - x1), dy = (float)(y2 - y1);
+    const float Q11 = dx == 1.0f ? (float)x2 - x : ((float)x2 - x) / dx;
+    const float Q21 = dx == 1.0f ? x - (float)x1 : (x - (float)x1) / dx;
     const float Q12 = Q11, Q22 = Q21;
     const V3 f1 = v3(x1y1.x * Q11 + x2y1.x * Q21, x1y1.y * Q11 + x2y1.y * Q21, x1y1.z * Q11 + x2y1.z * Q21);
     const V3 f2 = v3(x1y2.x * Q12 + x2y2.x * Q22, x1y2.y * Q12 + x2y2.y * Q22, x1y2.z * Q12 + x2y2.z * Q22);
-    const float wy2 = ((float)y2 - y) / (float)(y2 - y1);
-    const float wy1 = (y - (float)y1) / (float)(y2 - y1);
+    const float wy2 = dy == 1.0f ? (float)y2 - y : ((float)y2 - y) / dy;
+    const float wy1 = dy == 1.0f ? y - (float)y1 : (y - (float)y1) / dy;
     return v3(f1.x * wy2 + f2.x * wy1, f1.y * wy2 + f2.y * wy1, f1.z * wy2 + f2.z * wy1);
 }
 
 // SphericalMap::get_texel (APP/SphericalMap.cpp:17-29): returns RGBA with a = 1.
-__device__ inline float4 env_texel(const SceneView& s, V3 d) {
+__device__ inline float4 env_texel(const SceneView& s, const float* lut, V3 d) {
     if (s.env < 0) return make_float4(0, 0, 0, 1);
     const V3 vec = normalize(v3(d.x, d.z, d.y));
     const float u = (float)(0.5 + (double)pg_atan2f(vec.x, vec.z) / (2 * 3.14159265358979323846));
     const float v = (float)(0.5 - (double)pg_asinf(vec.y) / 3.14159265358979323846);
-    const V3 c = tex_texel(s.tex[s.env], s.texels, u, v);
+    const V3 c = tex_texel(s.tex[s.env], s.texels, lut, u, v);
     return make_float4(c.z, c.y, c.x, 1.0f);
 }
 

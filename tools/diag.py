@@ -24,7 +24,8 @@ def main():
         sc = scenes.random_scene(1_000_000, 42, env)
     else:
         sc = load_obj(scenes.AVENGER_OBJ)
-        sc.set_environment(env)
+        if not os.environ.get("DIAG_NOENV"):
+            sc.set_environment(env)
     ctx = Context(0)
     t = time.time()
     ctx.set_scene(sc)
