@@ -129,6 +129,7 @@ struct SceneView {  // kernel-argument view of the device scene
     const float* attr;     // 16 floats per ORIGINAL triangle: n0 n1 n2 uv0 uv1 uv2, mat (bits)
     const DevMaterial* mats;
     const DevTexture* tex;
+    int nmat, ntex;
     const unsigned char* texels;
     int env;
     int nlight;

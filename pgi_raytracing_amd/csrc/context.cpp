@@ -378,6 +378,8 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
     v.attr = ctx->attr.p;
     v.mats = ctx->mats.p;
     v.tex = ctx->texd.p;
+    v.nmat = (int)mats.size();
+    v.ntex = (int)texs.size();
     v.texels = ctx->texels.p;
     v.env = d->env_texture;
     v.nlight = d->num_lights;

@@ -122,10 +122,23 @@ void launch_raygen(const CameraView& cam, const FrameParams& fp, const int4* til
 
 // ------------------------------------------------------------------ shading (trace body)
 
+// LDS_TABLES: the material and texture-descriptor tables are copied to LDS per block, so the
+// hit -> attributes -> material -> texture chain has one global round trip fewer per hop
+constexpr int kLdsMats = 64, kLdsTex = 32;
+
+template <bool LDS_TABLES>
 __global__ __launch_bounds__(kBlock) void k_shade(SceneView s, FrameParams fp, int level, Queue q, Queue next,
                                                   LevelNodes nodes, ShadowQueue sq, FrameCounters* fc) {
     __shared__ float lut255[256];
-    fill_byte_lut(lut255);
+    __shared__ DevMaterial smat[LDS_TABLES ? kLdsMats : 1];
+    __shared__ DevTexture stex[LDS_TABLES ? kLdsTex : 1];
+    if constexpr (LDS_TABLES) {
+        for (int k = threadIdx.x; k < s.nmat; k += kBlock) smat[k] = s.mats[k];
+        for (int k = threadIdx.x; k < s.ntex; k += kBlock) stex[k] = s.tex[k];
+        s.tex = stex;  // env_texel / tex_texel read descriptors through s.tex
+    }
+    const DevMaterial* mats = LDS_TABLES ? smat : s.mats;
+    fill_byte_lut(lut255);  // ends with __syncthreads: the tables above are visible too
     const int n = min(fc->count[level], q.cap);
     const int tid = threadIdx.x;
     // one shadow queue for the whole batch: level L's rays follow those of levels < L (final by now)
@@ -165,7 +178,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(SceneView s, FrameParams fp, i
                     V3 nn = v3(interp1(a[0], a[3], a[6], u, v), interp1(a[1], a[4], a[7], u, v),
                                interp1(a[2], a[5], a[8], u, v));
                     mid = __float_as_int(a[15]);
-                    const DevMaterial& m = s.mats[mid];
+                    const DevMaterial& m = mats[mid];
                     nn = normalize(nn);
                     hitp = org + scale(t, dirraw);
                     if (rtime == PGRT_IOR_AIR) {
@@ -263,7 +276,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(SceneView s, FrameParams fp, i
             if (sbase + nshadow > sq.cap) {
                 atomicOr(&fc->overflow, 1);
             } else {
-                const DevMaterial& m = s.mats[mid];
+                const DevMaterial& m = mats[mid];
                 int k = sbase;
                 for (int li = 0; li < s.nlight; ++li) {
                     const DevLight& L = s.lights[li];
@@ -303,7 +316,10 @@ void launch_shade(const SceneView& s, const FrameParams& fp, int level, Queue q,
                   ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect) {
     if (max_count <= 0) return;
     const int grid = grid_for(max_count, expect);
-    hipLaunchKernelGGL(k_shade, dim3(grid), dim3(kBlock), 0, stream, s, fp, level, q, next, nodes, sq, fc);
+    if (s.nmat <= kLdsMats && s.ntex <= kLdsTex)
+        hipLaunchKernelGGL(k_shade<true>, dim3(grid), dim3(kBlock), 0, stream, s, fp, level, q, next, nodes, sq, fc);
+    else
+        hipLaunchKernelGGL(k_shade<false>, dim3(grid), dim3(kBlock), 0, stream, s, fp, level, q, next, nodes, sq, fc);
 }
 
 // ------------------------------------------------------------------ combine + finish
