@@ -603,9 +603,13 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
                                    std::min(sl->q_cap, sl->level_cap[L]), s, sl->expect_count[L]);
                 }
                 LevelNodes l0{sl->n_color[0]->p, sl->n_link[0]->p, sl->n_att[0]->p};
+                const bool resolve_l0 = fp.nsb > 1;  // several samples per pixel: trees in parallel
+                if (resolve_l0)
+                    launch_combine(ctx->view, 0, l0, levels > 1 ? sl->n_color[1]->p : sl->n_color[0]->p, sq, fcd,
+                                   n0, s, n0);
                 launch_finish(ctx->view, fp, sl->tiles.p, l0, levels > 1 ? sl->n_color[1]->p : sl->n_color[0]->p,
                               sq, sl->accum.p, out, out_mode, ox, oy, pitch, (int)npix, s0 == 0,
-                              s0 + fp.nsb >= spp, K, j, s);
+                              s0 + fp.nsb >= spp, K, j, resolve_l0, s);
                 ctx->timer.end(s, id);
             }
             if (!staggered) PGRT_HIP(hipEventRecord(sl->ev_stagger, s));

@@ -389,12 +389,14 @@ __global__ __launch_bounds__(kBlock) void k_finish(SceneView s, FrameParams fp, 
                                                    LevelNodes l0, const float4* __restrict__ child, ShadowQueue sq,
                                                    float4* __restrict__ accum, float* __restrict__ out, int out_mode,
                                                    int ox, int oy, int pitch, int npix, int first, int last, int K,
-                                                   int j) {
+                                                   int j, int resolved) {
     const int p = blockIdx.x * kBlock + threadIdx.x;
     if (p >= npix) return;
     float4 acc = first ? make_float4(0.0f, 0.0f, 0.0f, 1.0f) : accum[p];
     for (int k = 0; k < fp.nsb; ++k) {  // final_color += result_colors[x][y] (raytracer.cpp:422-429)
-        const float4 v = node_color(s, sq, l0, child, p * fp.nsb + k);
+        // resolved: a k_combine pass over level 0 already wrote every sample's final colour (many
+        // samples per pixel: their trees are evaluated in parallel, only the ordered sum is here)
+        const float4 v = resolved ? l0.color[p * fp.nsb + k] : node_color(s, sq, l0, child, p * fp.nsb + k);
         acc.x += v.x;
         acc.y += v.y;
         acc.z += v.z;
@@ -424,10 +426,10 @@ __global__ __launch_bounds__(kBlock) void k_finish(SceneView s, FrameParams fp, 
 
 void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles, LevelNodes l0, const float4* child,
                    ShadowQueue sq, float4* accum, float* out, int out_mode, int ox, int oy, int pitch, int npix,
-                   bool first, bool last, int K, int j, hipStream_t stream) {
+                   bool first, bool last, int K, int j, bool resolved, hipStream_t stream) {
     if (npix <= 0) return;
     hipLaunchKernelGGL(k_finish, dim3(ceil_div(npix, kBlock)), dim3(kBlock), 0, stream, s, fp, tiles, l0, child, sq,
-                       accum, out, out_mode, ox, oy, pitch, npix, first ? 1 : 0, last ? 1 : 0, K, j);
+                       accum, out, out_mode, ox, oy, pitch, npix, first ? 1 : 0, last ? 1 : 0, K, j, resolved ? 1 : 0);
 }
 
 // ------------------------------------------------------------------ multi-GPU unpack

@@ -83,10 +83,11 @@ void launch_combine(const SceneView& s, int level, LevelNodes nodes, const float
 // level-0 combine + sample accumulation (+ gamma and framebuffer write on the last batch).
 // out_mode 0: framebuffer (rect origin ox,oy, row pitch in pixels); 1: tile-compact
 // tiles of this launch are tiles j, j + K, ... of the caller's list (pipeline slot j of K):
-// out_mode 1 writes local tile t at tile-compact position t * K + j
+// out_mode 1 writes local tile t at tile-compact position t * K + j.  resolved: level 0's final
+// colours were written by launch_combine(level 0) (several samples per pixel)
 void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles, LevelNodes l0, const float4* child,
                    ShadowQueue sq, float4* accum, float* out, int out_mode, int ox, int oy, int pitch, int npix,
-                   bool first, bool last, int K, int j, hipStream_t stream);
+                   bool first, bool last, int K, int j, bool resolved, hipStream_t stream);
 // frame sink: sum += frame (count-th frame; count == 1 resets), mean = sum / count
 void launch_accumulate_frame(const float* frame, float* sum, float* mean, long long pixels, int count,
                              hipStream_t stream);
