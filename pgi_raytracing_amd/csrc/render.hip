@@ -145,9 +145,31 @@ __global__ __launch_bounds__(kBlock) void k_shade(SceneView s, FrameParams fp, i
     int sq_base = 0;
     for (int l = 0; l < level; ++l) sq_base += fc->shadow_count[l];
     const int sbits = s.nlight > 0 ? 32 - __clz(s.nlight) : 0;  // bits of a lane's shadow-ray count
-    for (int base_i = blockIdx.x * kBlock; base_i < n; base_i += gridDim.x * kBlock) {
+    // software pipeline over the grid-stride loop: the next ray's record and hit are loaded
+    // while this one is shaded (big queues give every thread several rays)
+    const int stride = gridDim.x * kBlock;
+    float4 nx_o = make_float4(0, 0, 0, 0), nx_d = make_float4(0, 0, 0, 0), nx_h = make_float4(0, 0, 0, 0);
+    float nx_t = 0.0f;
+    {
+        const int i0 = blockIdx.x * kBlock + tid;
+        if (i0 < n) {
+            nx_o = q.ro[i0];
+            nx_d = q.rd[i0];
+            nx_t = q.time[i0];
+            nx_h = q.hit[i0];
+        }
+    }
+    for (int base_i = blockIdx.x * kBlock; base_i < n; base_i += stride) {
         const int i = base_i + tid;
         const bool active = i < n;
+        const float4 cur_o = nx_o, cur_d = nx_d, cur_h = nx_h;
+        const float cur_t = nx_t;
+        if (i + stride < n) {
+            nx_o = q.ro[i + stride];
+            nx_d = q.rd[i + stride];
+            nx_t = q.time[i + stride];
+            nx_h = q.hit[i + stride];
+        }
         int kind = 0;  // 0 final colour, 1 dielectric, 2 opaque (shadow rays pending)
         float4 color = make_float4(0, 0, 0, 1);
         int nshadow = 0, nchild = 0;
@@ -158,10 +180,10 @@ __global__ __launch_bounds__(kBlock) void k_shade(SceneView s, FrameParams fp, i
         float m_d_r = 0, m_d_g = 0, m_d_b = 0;
         int mid = 0;
         if (active) {
-            const float4 o4 = q.ro[i];
-            const float4 d4 = q.rd[i];
-            const float rtime = q.time[i];
-            const float4 h = q.hit[i];
+            const float4 o4 = cur_o;
+            const float4 d4 = cur_d;
+            const float rtime = cur_t;
+            const float4 h = cur_h;
             org = v3(o4.x, o4.y, o4.z);
             dirraw = v3(d4.x, d4.y, d4.z);
             if (d4.w < 0.0f) {
