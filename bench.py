@@ -8,6 +8,8 @@ the other BASELINE configs for the records in DESIGN.md).  N > 1: one process
 per GPU (torch.distributed launcher env), 64x64 image tiles dealt round-robin to ranks, one
 ncclGather (RCCL over xGMI) to rank 0 and an unpack kernel there -- the total frame is fixed
 (strong scaling).  Rays = every closest-hit query (primary + shadow + reflect + refract).
+Frames run asynchronously with up to --in-flight frames overlapping on the device (throughput =
+ms_per_step); the latency of one synchronous frame is reported beside it (frame_latency_ms).
 """
 from __future__ import annotations
 
@@ -16,11 +18,15 @@ import json
 import os
 import sys
 import time
+from collections import deque
 
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# one hardware queue per frame in flight (+ the context stream): HIP's default of 4 would make
+# frames share queues; read by the HIP runtime at its initialisation, i.e. before libpgrt loads
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 METRIC = "Mrays/sec + ms/frame, avenger 1920x1080 Whitted d=5, 1/2/4/8 GPU"
@@ -54,6 +60,8 @@ def parse():
     ap.add_argument("--dof", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--in-flight", type=int, default=None,
+                    help="frames in flight (pgrt_set_frames_in_flight); default 6 (r1 scan, tools/inflight_scan.py)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (multi-thread leg)")
     a = ap.parse_args()
@@ -101,25 +109,51 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(world, rank, uid[0])
 
-    def frame(p):
+    def frame(p):  # synchronous frame (latency, profiled frames)
         if world > 1:
             return ctx.render_distributed_device(p, fb)
         return ctx.render_device(p, fb)
 
-    for _ in range(args.warmup):
-        frame(params)
+    # frames in flight: a step is one whole frame (every rank's tiles rendered, gathered and
+    # unpacked on rank 0); up to `in_flight` consecutive frames overlap on the device, so one
+    # frame's latency-bound deep levels share the CUs with the next frame's wide levels
+    in_flight = args.in_flight or 6
+    ctx.set_frames_in_flight(in_flight)
+
+    def run_frames(n):
+        pending, rays_n = deque(), 0
+        for _ in range(n):
+            pending.append(ctx.render_distributed_device_async(params, fb) if world > 1
+                           else ctx.render_device_async(params, fb))
+            if len(pending) >= in_flight:
+                rays_n += ctx.render_wait(pending.popleft()).rays()
+        while pending:
+            rays_n += ctx.render_wait(pending.popleft()).rays()
+        return rays_n
+
+    run_frames(args.warmup)
     ctx.synchronize()
     if dist:
         dist.barrier()
-    rays = 0
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        st = frame(params)
-        rays += st.rays()
+    rays = run_frames(args.steps)
     ctx.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # frame latency (one synchronous frame at a time), reported beside the throughput
+    lat = []
+    for _ in range(min(args.steps, 30)):
+        t1 = time.perf_counter()
+        frame(params)
+        lat.append(time.perf_counter() - t1)
+    latency_ms = sorted(lat)[len(lat) // 2] * 1e3
+    if dist:
+        import torch
+
+        lt = torch.tensor([latency_ms], dtype=torch.float64)
+        dist.all_reduce(lt, op=dist.ReduceOp.MAX)
+        latency_ms = float(lt.item())
     total_rays = rays
     if dist:
         import torch
@@ -224,6 +258,8 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "frames_in_flight": in_flight,
+            "frame_latency_ms": round(latency_ms, 4),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,

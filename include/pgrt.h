@@ -188,6 +188,21 @@ int pgrt_accumulate_reset(pgrt_ctx* ctx);
 int pgrt_render_accumulate(pgrt_ctx* ctx, const pgrt_render_params* p, float* mean_host, int* frames,
                            pgrt_stats* st);
 
+/* ---- frames in flight (asynchronous frames) ----
+ * pgrt_render_device_async enqueues a frame and returns at once with a ticket; up to n frames
+ * (pgrt_set_frames_in_flight, 1..8, default 1) run concurrently, each on its own pipeline
+ * streams, so one frame's latency-bound deep Whitted levels overlap the next frame's wide levels.
+ * Submitting when n frames are pending first completes the oldest.  pgrt_render_wait(ticket)
+ * completes every frame up to that ticket and returns its statistics (ms_total = submit to
+ * completion); a ticket stays valid until its frame set is reused n submissions later.  The
+ * framebuffer of a pending frame must not be read or reused.  Frames are bit-identical to
+ * pgrt_render_device.  The synchronous entry points complete pending frames first.  profile must
+ * be 0 for asynchronous frames. */
+int pgrt_set_frames_in_flight(pgrt_ctx* ctx, int n);
+int pgrt_render_device_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device,
+                             unsigned long long* ticket);
+int pgrt_render_wait(pgrt_ctx* ctx, unsigned long long ticket, pgrt_stats* st);
+
 /* ---- batched closest-hit query with rtcIntersect1 semantics ----
  * rays: n x 8 floats {org.xyz, tnear, dir.xyz, tfar}; hits: n x 4 {t, u, v, prim} where prim
  * is the global triangle index stored as int32 bits, -1 on a miss (t = tfar, u = v = 0). */
@@ -209,6 +224,12 @@ int pgrt_unpack_tiles_host(int width, int height, int tile_size, int world,
                            const float* gathered, float* rgba);
 int pgrt_comm_unique_id(char id[128]);
 int pgrt_comm_init(pgrt_ctx* ctx, int world, int rank, const char id[128]);
+/* Rank-local half of the distributed render, for callers that gather with their own
+ * communicator: render the tiles of `rank` (of `world`) of the camera image into a tile-compact
+ * device buffer of pgrt_tile_count(W, H, 64, rank, world) * 64 * 64 * 4 floats (local tile j is
+ * global tile j * world + rank; edge tiles are padded). */
+int pgrt_render_tiles_device(pgrt_ctx* ctx, const pgrt_render_params* p, int rank, int world,
+                             void* tiles_device, pgrt_stats* st);
 /* Render this rank's tiles, gather them on rank 0 with one ncclGather, unpack on device.
  * rgba_host (rank 0 only, may be NULL elsewhere): W*H*4 floats. */
 int pgrt_render_distributed(pgrt_ctx* ctx, const pgrt_render_params* p, float* rgba_host,
@@ -216,6 +237,11 @@ int pgrt_render_distributed(pgrt_ctx* ctx, const pgrt_render_params* p, float* r
 /* Same, framebuffer left on rank 0's device (W*H*4 floats). */
 int pgrt_render_distributed_device(pgrt_ctx* ctx, const pgrt_render_params* p,
                                    void* rgba_device, pgrt_stats* st);
+/* Asynchronous form (frames in flight, see pgrt_render_device_async): the gather of a frame is
+ * enqueued when it completes (pgrt_render_wait or a later submission) and overlaps the frames
+ * still in flight.  Every rank must submit and wait in the same order. */
+int pgrt_render_distributed_device_async(pgrt_ctx* ctx, const pgrt_render_params* p,
+                                         void* rgba_device, unsigned long long* ticket);
 
 /* ---- scene ingest (LoadOBJ / LoadMTL, objloader.cpp:53-507; host only) ----
  * Texture files named by map_Kd are NOT decoded here: their paths are reported so the caller

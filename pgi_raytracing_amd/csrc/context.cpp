@@ -22,6 +22,7 @@ namespace {
 
 constexpr long long kMaxBatchRays = 16ll << 20;  // level-0 rays per sample batch
 constexpr int kTraceGridThreads = 2048 * 256;    // persistent trace grid (global overflow stacks)
+constexpr int kMaxFramesInFlight = 8;
 
 struct StageTimer {
     struct Rec {
@@ -77,6 +78,19 @@ enum { CAT_RAYGEN, CAT_TRACE, CAT_SHADE, CAT_SHADOW, CAT_COMBINE, CAT_LTRACE, CA
 }  // namespace
 
 namespace pgrt {
+// byte signature of the host-side arguments of a captured launch sequence
+struct Signature {
+    std::vector<unsigned char> v;
+    void add_bytes(const void* p, size_t n) {
+        const unsigned char* b = static_cast<const unsigned char*>(p);
+        v.insert(v.end(), b, b + n);
+    }
+    template <class T>
+    void add(const T& x) {
+        add_bytes(&x, sizeof(T));
+    }
+};
+
 // One pipeline instance: queues, level nodes, shadow queue and counters for a subset of the
 // frame's tiles, enqueued on its own stream.  Two slots run concurrently: each launch of one
 // slot fills the CUs the other slot's latency-bound launches leave idle (the tail of every
@@ -105,7 +119,9 @@ struct FrameSlot {
     void ensure_pinned(int batches, int ntiles) {
         if (pinned_fc_n < batches) {
             if (pinned_fc) (void)hipHostFree(pinned_fc);
-            PGRT_HIP(hipHostMalloc((void**)&pinned_fc, sizeof(FrameCounters) * batches, hipHostMallocDefault));
+            // written by the export kernel (coherent: no host-side cache maintenance)
+            PGRT_HIP(hipHostMalloc((void**)&pinned_fc, sizeof(FrameCounters) * batches,
+                                   hipHostMallocMapped | hipHostMallocCoherent));
             pinned_fc_n = batches;
         }
         if (pinned_tiles_n < ntiles) {
@@ -116,19 +132,84 @@ struct FrameSlot {
     }
     DevBuf<float4> accum;
     DevBuf<int> gstack;
+    std::vector<int4> tiles_dev;  // host copy of the device tile list
     int expect_count[kMaxLevels] = {0};  // grid hints from the previous frame (0 = unknown)
     int expect_shadow_total = 0;
+    // captured launch sequence of this slot and the host arguments it was captured with
+    hipGraphExec_t gexec = nullptr;
+    std::vector<unsigned char> gsig;
+    int graph_trace_launches = 0;
+    void add_buffers(Signature& g) const {
+        for (int b = 0; b < 2; ++b) {
+            g.add(q_ro[b].p);
+            g.add(q_rd[b].p);
+            g.add(q_hit[b].p);
+            g.add(q_time[b].p);
+        }
+        g.add(q_cap);
+        for (size_t L = 0; L < n_color.size(); ++L) {
+            g.add(n_color[L]->p);
+            g.add(n_att[L]->p);
+            g.add(n_link[L]->p);
+            g.add(level_cap[L]);
+        }
+        g.add(s_ro.p);
+        g.add(s_rd.p);
+        g.add(s_hit.p);
+        g.add(s_contrib.p);
+        g.add(s_cap);
+        g.add(fc.p);
+        g.add(pinned_fc);
+        g.add(pinned_tiles);
+        g.add(tiles.p);
+        g.add(accum.p);
+        g.add(gstack.p);
+        g.add_bytes(expect_count, sizeof(expect_count));
+        g.add(expect_shadow_total);
+    }
     FrameSlot() {
         PGRT_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         PGRT_HIP(hipEventCreateWithFlags(&ev_stagger, hipEventDisableTiming));
         PGRT_HIP(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
     }
     ~FrameSlot() {
+        if (gexec) (void)hipGraphExecDestroy(gexec);
         if (pinned_fc) (void)hipHostFree(pinned_fc);
         if (pinned_tiles) (void)hipHostFree(pinned_tiles);
         if (ev_stagger) (void)hipEventDestroy(ev_stagger);
         if (ev_done) (void)hipEventDestroy(ev_done);
         if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+// One frame in flight: its pipeline slots, the frame's arguments (kept for an overflow re-render)
+// and, for a distributed frame, this rank's tile-compact buffer.  Frames in flight run
+// concurrently on their own slot streams: the deep Whitted levels of one frame are chains of
+// dependent launches over a few thousand rays (latency floors), and the next
+// frame's wide levels fill the CUs they leave idle.
+struct FrameSet {
+    std::vector<std::unique_ptr<FrameSlot>> slots;
+    // recorded on the context stream after the last reader of this set's output (gather/unpack):
+    // the set's next frame waits for it before overwriting its buffers
+    hipEvent_t ev_ready = nullptr;
+    bool pending = false, has_result = false;
+    unsigned long long ticket = 0;
+    pgrt_render_params params{};
+    std::vector<int4> tiles;
+    float* out = nullptr;
+    int out_mode = 0, ox = 0, oy = 0, pitch = 0;
+    int K = 0;             // slots of the pending frame
+    bool distributed = false;
+    float* dist_fb = nullptr;
+    DevBuf<float> tilebuf;  // distributed: this rank's tiles, tile-compact
+    int cam_w = 0, cam_h = 0;  // image size at submission (the gather's layout)
+    pgrt_stats stats{};
+    std::chrono::steady_clock::time_point t0;
+    FrameSet() { PGRT_HIP(hipEventCreateWithFlags(&ev_ready, hipEventDisableTiming)); }
+    ~FrameSet() {
+        for (auto& s : slots)
+            if (s->stream) (void)hipStreamSynchronize(s->stream);
+        if (ev_ready) (void)hipEventDestroy(ev_ready);
     }
 };
 }  // namespace pgrt
@@ -150,13 +231,17 @@ struct pgrt_ctx {
     DevBuf<DevLight> lights;
     SceneView view{};
     bool has_scene = false;
+    unsigned long long scene_gen = 0;  // bumped by every pgrt_set_scene
     pgrt_bvh_info info{};
 
     CameraView cam{};
     bool has_cam = false;
 
-    // frame state: independent pipeline slots (tile subsets), each on its own stream
-    std::vector<std::unique_ptr<FrameSlot>> slots;
+    // frame state: frames in flight (set 0 serves the synchronous entry points), each with its
+    // independent pipeline slots (tile subsets) on their own streams
+    std::vector<std::unique_ptr<FrameSet>> sets;
+    int frames_in_flight = 1;
+    unsigned long long next_ticket = 1;
     DevBuf<FrameCounters> fc;  // pgrt_intersect_closest
     DevBuf<int> gstack;        // pgrt_intersect_closest
     DevBuf<float> out_tmp;
@@ -438,7 +523,10 @@ void ensure_frame_buffers(FrameSlot* sl, int n0, int levels, int nlight, int bat
         sl->s_contrib.alloc(sc);
         sl->s_cap = sc;
     }
-    sl->fc.alloc((size_t)batches);
+    if (sl->fc.n < (size_t)batches) {  // zeroed once; every frame's export kernel re-zeroes them
+        sl->fc.alloc((size_t)batches);
+        PGRT_HIP(hipMemset(sl->fc.p, 0, sizeof(FrameCounters) * batches));
+    }
     if (sl->gstack.n == 0) sl->gstack.alloc((size_t)kTraceGridThreads * kGlobalStack);
 }
 
@@ -479,24 +567,31 @@ void grow_after_overflow(FrameSlot* sl, int levels) {
     }
 }
 
-// Render the pixels of `tiles` (each <= kTile x kTile); out_mode 0 writes a framebuffer
-// (origin ox,oy, pitch in pixels), 1 writes tile-compact buffers.  Device pointer output.
-void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<int4>& tiles, float* out,
-                  int out_mode, int ox, int oy, int pitch, pgrt_stats* st) {
-    PGRT_REQUIRE(ctx->has_scene, PGRT_ERR_NO_SCENE, "pgrt_set_scene has not been called");
-    PGRT_REQUIRE(ctx->has_cam, PGRT_ERR_NO_CAMERA, "pgrt_set_camera has not been called");
-    PGRT_REQUIRE(p->spp_side >= 1 && p->spp_side <= 64, PGRT_ERR_INVALID_ARGUMENT, "spp_side must be in [1, 64]");
-    PGRT_REQUIRE(p->max_level >= 0 && p->max_level <= kMaxLevels - 2, PGRT_ERR_INVALID_ARGUMENT,
-                 "max_level must be in [0, 14]");
+FrameSet* frame_set(pgrt_ctx* ctx, int i) {
+    while ((int)ctx->sets.size() <= i) {
+        ctx->sets.emplace_back(new FrameSet());
+        PGRT_HIP(hipEventRecord(ctx->sets.back()->ev_ready, ctx->stream));
+    }
+    return ctx->sets[i].get();
+}
+
+// Enqueue the frame described by fs (params, tiles, output) on fs's slot streams after
+// fs->ev_ready.  Tiles are <= kTile x kTile; out_mode 0 writes a framebuffer (origin ox,oy, pitch
+// in pixels), 1 tile-compact buffers.  No host synchronisation.
+void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
+    const pgrt_render_params* p = &fs->params;
+    const std::vector<int4>& tiles = fs->tiles;
     const int ntiles = (int)tiles.size();
     const int spp = p->spp_side * p->spp_side;
-    if (ntiles == 0) return;
     const int levels = p->max_level + 1;
     // pipeline slots: tiles dealt round-robin (slot j gets tiles j, j+K, ...)
-    static const int want_slots = [] {
+    // (one slot per frame when frames are in flight: the concurrent frames fill the CUs instead,
+    // r1 scan: 6 frames x 1 slot 0.39 ms/frame, 3 frames x 2 slots 0.53)
+    static const int env_slots = [] {
         const char* e = getenv("PGRT_SLOTS");
-        return e ? std::max(1, std::min(3, atoi(e))) : kDefaultSlots;
+        return e ? std::max(1, std::min(3, atoi(e))) : 0;
     }();
+    const int want_slots = env_slots ? env_slots : (ctx->frames_in_flight > 1 ? 1 : kDefaultSlots);
     static const int stagger_level = [] {  // slot k+1 starts after slot k's level-L shade (-1: no stagger)
         const char* e = getenv("PGRT_STAGGER_LEVEL");
         return e ? atoi(e) : -1;
@@ -505,12 +600,11 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
         const char* e = getenv("PGRT_PACKET_LEVELS");
         return e ? atoi(e) : 0;
     }();
-    const int K = std::max(1, std::min(want_slots, ntiles));
-    while ((int)ctx->slots.size() < K) ctx->slots.emplace_back(new FrameSlot());
+    const int K = ntiles == 0 ? 0 : std::max(1, std::min(want_slots, ntiles));
+    fs->K = K;
+    while ((int)fs->slots.size() < K) fs->slots.emplace_back(new FrameSlot());
     ctx->timer.on = p->profile > 0;
-    double ms[CAT_N] = {0};
-    uint64_t rays_shadow = 0, rays_reflect = 0, rays_refract = 0, trav_nodes = 0, trav_tests = 0, trav_wide = 0;
-    int retries = 0, trace_launches = 0;
+    int trace_launches = 0;
     FrameParams fp0{};
     fp0.spp_side = p->spp_side;
     fp0.max_level = p->max_level;
@@ -521,106 +615,184 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
     fp0.jitter = p->jitter;
     fp0.seed = p->seed;
     fp0.frame = p->frame;
-    // the main stream's prior work (scene upload, camera) happens before any slot starts
-    hipEvent_t ev_start;
-    PGRT_HIP(hipEventCreateWithFlags(&ev_start, hipEventDisableTiming));
-    struct EvGuard {
-        hipEvent_t e;
-        ~EvGuard() { (void)hipEventDestroy(e); }
-    } evg{ev_start};
-    for (;;) {  // whole-frame retry if any queue overflowed
-        PGRT_HIP(hipEventRecord(ev_start, ctx->stream));
-        for (int j = 0; j < K; ++j) {
-            FrameSlot* sl = ctx->slots[j].get();
-            hipStream_t s = sl->stream;
-            const int nt = (ntiles - j + K - 1) / K;
-            const long long npix = (long long)nt * kTile * kTile;
-            PGRT_REQUIRE(npix <= kMaxBatchRays * 8, PGRT_ERR_INVALID_ARGUMENT, "frame too large");
-            const int nsb = (int)std::max(1ll, std::min<long long>(spp, kMaxBatchRays / npix));
-            const int batches = (spp + nsb - 1) / nsb;
-            ensure_frame_buffers(sl, (int)(npix * nsb), levels, ctx->view.nlight, batches);
-            sl->ensure_pinned(batches, nt);
-            for (int t = j, q = 0; t < ntiles; t += K, ++q) sl->pinned_tiles[q] = tiles[t];
-            PGRT_HIP(hipStreamWaitEvent(s, ev_start, 0));
-            if (j > 0 && stagger_level >= 0) PGRT_HIP(hipStreamWaitEvent(s, ctx->slots[j - 1]->ev_stagger, 0));
-            sl->tiles.alloc(nt);
-            PGRT_HIP(hipMemcpyAsync(sl->tiles.p, sl->pinned_tiles, sizeof(int4) * nt, hipMemcpyHostToDevice, s));
-            sl->accum.alloc((size_t)npix);
-            PGRT_HIP(hipMemsetAsync(sl->fc.p, 0, sizeof(FrameCounters) * batches, s));
-            FrameParams fp = fp0;
-            fp.ntiles = nt;
-            bool staggered = false;
-            for (int bi = 0; bi < batches; ++bi) {
-                const int s0 = bi * nsb;
-                fp.s0 = s0;
-                fp.nsb = std::min(nsb, spp - s0);
-                const int n0 = (int)(npix * fp.nsb);
-                FrameCounters* fcd = sl->fc.p + bi;
-                Queue q[2];
-                for (int b = 0; b < 2; ++b)
-                    q[b] = Queue{sl->q_ro[b].p, sl->q_rd[b].p, sl->q_time[b].p, sl->q_hit[b].p, sl->q_cap};
-                ShadowQueue sq{sl->s_ro.p, sl->s_rd.p, sl->s_hit.p, sl->s_contrib.p, sl->s_cap};
-                int id = ctx->timer.begin(s, CAT_RAYGEN);
-                launch_raygen(ctx->cam, fp, sl->tiles.p, q[0], n0, fcd, s);
-                ctx->timer.end(s, id);
-                for (int L = 0; L < levels; ++L) {
-                    Queue qc = q[L & 1], qn = q[(L + 1) & 1];
-                    const int maxc = L == 0 ? n0 : std::min(sl->q_cap, sl->level_cap[L]);
-                    qc.cap = maxc;
-                    qn.cap = std::min(sl->q_cap, L + 1 < levels ? sl->level_cap[L + 1] : sl->q_cap);
-                    LevelNodes ln{sl->n_color[L]->p, sl->n_link[L]->p, sl->n_att[L]->p};
-                    // grid hints: last frame's per-level counts (+25 %); level 0 is exact
-                    const int ex = L == 0 ? n0 : sl->expect_count[L];
-                    id = ctx->timer.begin(s, CAT_TRACE, CAT_LTRACE + L);
-                    launch_trace(ctx->view, qc.ro, qc.rd, qc.hit, &fcd->count[L], 0, maxc, &fcd->fetch[L],
-                                 sl->gstack.p, kTraceGridThreads, fcd->trav[L], p->profile >= 2, s, ex, 1, true,
-                                 L <= packet_levels);  // coherent 8x8-pixel waves -> packet traversal
-                    ctx->timer.end(s, id);
-                    ++trace_launches;
-                    id = ctx->timer.begin(s, CAT_SHADE, CAT_LSHADE + L);
-                    launch_shade(ctx->view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex);
-                    ctx->timer.end(s, id);
-                    if (!staggered && (L == std::min(stagger_level, levels - 1))) {
-                        PGRT_HIP(hipEventRecord(sl->ev_stagger, s));
-                        staggered = true;
-                    }
-                }
-                if (ctx->view.nlight > 0 && p->max_level > 0) {  // every level's shadow rays, one launch
-                    id = ctx->timer.begin(s, CAT_TRACE);
-                    const int sid = ctx->timer.begin(s, CAT_SHADOW);
-                    launch_trace(ctx->view, sq.ro, sq.rd, sq.hit, &fcd->shadow_count[0], 0, sq.cap,
-                                 &fcd->fetch[kMaxLevels], sl->gstack.p, kTraceGridThreads, fcd->trav[kMaxLevels],
-                                 p->profile >= 2, s, sl->expect_shadow_total, levels,
-                                 false);  // shadow rays (from the light along H) mostly miss the root
-                    ctx->timer.end(s, sid);
-                    ctx->timer.end(s, id);
-                    ++trace_launches;
-                }
-                id = ctx->timer.begin(s, CAT_COMBINE);
-                for (int L = p->max_level - 1; L >= 1; --L) {
-                    LevelNodes ln{sl->n_color[L]->p, sl->n_link[L]->p, sl->n_att[L]->p};
-                    launch_combine(ctx->view, L, ln, sl->n_color[L + 1]->p, sq, fcd,
-                                   std::min(sl->q_cap, sl->level_cap[L]), s, sl->expect_count[L]);
-                }
-                LevelNodes l0{sl->n_color[0]->p, sl->n_link[0]->p, sl->n_att[0]->p};
-                const bool resolve_l0 = fp.nsb > 1;  // several samples per pixel: trees in parallel
-                if (resolve_l0)
-                    launch_combine(ctx->view, 0, l0, levels > 1 ? sl->n_color[1]->p : sl->n_color[0]->p, sq, fcd,
-                                   n0, s, n0);
-                launch_finish(ctx->view, fp, sl->tiles.p, l0, levels > 1 ? sl->n_color[1]->p : sl->n_color[0]->p,
-                              sq, sl->accum.p, out, out_mode, ox, oy, pitch, (int)npix, s0 == 0,
-                              s0 + fp.nsb >= spp, K, j, resolve_l0, s);
-                ctx->timer.end(s, id);
+    static const bool graphs = [] {  // PGRT_GRAPHS=1: hipGraph replay (off by default, see below)
+        const char* e = getenv("PGRT_GRAPHS");
+        return e ? atoi(e) != 0 : false;
+    }();
+    // hipGraph replay: a slot's whole launch sequence (~25 launches at d=5) is captured once and
+    // replayed while every host-side launch argument is unchanged (the signature below).  It cuts
+    // the host's enqueue cost per frame 0.058 -> 0.012 ms, but r1 A/B with frames in flight
+    // (tools/inflight_scan.py) measured lower device throughput (C2, 4 in flight: 0.37 -> 0.45
+    // ms/frame), so kernels are launched one by one unless PGRT_GRAPHS=1
+    const bool use_graph = graphs && p->profile == 0 && stagger_level < 0;
+    for (int j = 0; j < K; ++j) {
+        FrameSlot* sl = fs->slots[j].get();
+        hipStream_t s = sl->stream;
+        const int nt = (ntiles - j + K - 1) / K;
+        const long long npix = (long long)nt * kTile * kTile;
+        PGRT_REQUIRE(npix <= kMaxBatchRays * 8, PGRT_ERR_INVALID_ARGUMENT, "frame too large");
+        const int nsb = (int)std::max(1ll, std::min<long long>(spp, kMaxBatchRays / npix));
+        const int batches = (spp + nsb - 1) / nsb;
+        ensure_frame_buffers(sl, (int)(npix * nsb), levels, ctx->view.nlight, batches);
+        sl->ensure_pinned(batches, nt);
+        if (sl->tiles.n < (size_t)nt) sl->tiles_dev.clear();
+        sl->tiles.alloc(nt);
+        sl->accum.alloc((size_t)npix);
+        PGRT_HIP(hipStreamWaitEvent(s, fs->ev_ready, 0));
+        // the pinned tile list may still feed this slot's previous upload
+        PGRT_HIP(hipEventSynchronize(sl->ev_done));
+        for (int t = j, q = 0; t < ntiles; t += K, ++q) sl->pinned_tiles[q] = tiles[t];
+        if (j > 0 && stagger_level >= 0) PGRT_HIP(hipStreamWaitEvent(s, fs->slots[j - 1]->ev_stagger, 0));
+        bool replay = false;
+        if (use_graph) {
+            Signature g;
+            g.add(*p);
+            g.add(ctx->cam);
+            g.add(ctx->view);
+            g.add(ctx->scene_gen);
+            g.add(K);
+            g.add(j);
+            g.add(nt);
+            g.add_bytes(sl->pinned_tiles, sizeof(int4) * nt);
+            g.add(fs->out);
+            g.add(fs->out_mode);
+            g.add(fs->ox);
+            g.add(fs->oy);
+            g.add(fs->pitch);
+            sl->add_buffers(g);
+            if (sl->gexec && g.v == sl->gsig) {
+                replay = true;
+            } else {
+                if (sl->gexec) (void)hipGraphExecDestroy(sl->gexec);
+                sl->gexec = nullptr;
+                sl->gsig = std::move(g.v);
+                PGRT_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
             }
-            if (!staggered) PGRT_HIP(hipEventRecord(sl->ev_stagger, s));
+        }
+        if (replay) {
+            PGRT_HIP(hipGraphLaunch(sl->gexec, s));
+            PGRT_HIP(hipEventRecord(sl->ev_stagger, s));
             sl->host_fc.resize(batches);
+            PGRT_HIP(hipEventRecord(sl->ev_done, s));
+            trace_launches += sl->graph_trace_launches;
+            continue;
+        }
+        const int launches_before = trace_launches;
+        // the device tile list is re-uploaded only when it changed
+        if (sl->tiles_dev.size() != (size_t)nt || !std::equal(sl->tiles_dev.begin(), sl->tiles_dev.end(),
+                                                               sl->pinned_tiles, [](const int4& a, const int4& b) {
+                                                                   return a.x == b.x && a.y == b.y && a.z == b.z &&
+                                                                          a.w == b.w;
+                                                               })) {
+            PGRT_HIP(hipMemcpyAsync(sl->tiles.p, sl->pinned_tiles, sizeof(int4) * nt, hipMemcpyHostToDevice, s));
+            sl->tiles_dev.assign(sl->pinned_tiles, sl->pinned_tiles + nt);
+        }
+        FrameParams fp = fp0;
+        fp.ntiles = nt;
+        bool staggered = false;
+        for (int bi = 0; bi < batches; ++bi) {
+            const int s0 = bi * nsb;
+            fp.s0 = s0;
+            fp.nsb = std::min(nsb, spp - s0);
+            const int n0 = (int)(npix * fp.nsb);
+            FrameCounters* fcd = sl->fc.p + bi;
+            Queue q[2];
+            for (int b = 0; b < 2; ++b)
+                q[b] = Queue{sl->q_ro[b].p, sl->q_rd[b].p, sl->q_time[b].p, sl->q_hit[b].p, sl->q_cap};
+            ShadowQueue sq{sl->s_ro.p, sl->s_rd.p, sl->s_hit.p, sl->s_contrib.p, sl->s_cap};
+            int id = ctx->timer.begin(s, CAT_RAYGEN);
+            launch_raygen(ctx->cam, fp, sl->tiles.p, q[0], n0, fcd, s);
+            ctx->timer.end(s, id);
+            for (int L = 0; L < levels; ++L) {
+                Queue qc = q[L & 1], qn = q[(L + 1) & 1];
+                const int maxc = L == 0 ? n0 : std::min(sl->q_cap, sl->level_cap[L]);
+                qc.cap = maxc;
+                qn.cap = std::min(sl->q_cap, L + 1 < levels ? sl->level_cap[L + 1] : sl->q_cap);
+                LevelNodes ln{sl->n_color[L]->p, sl->n_link[L]->p, sl->n_att[L]->p};
+                // grid hints: last frame's per-level counts (+25 %); level 0 is exact
+                const int ex = L == 0 ? n0 : sl->expect_count[L];
+                id = ctx->timer.begin(s, CAT_TRACE, CAT_LTRACE + L);
+                launch_trace(ctx->view, qc.ro, qc.rd, qc.hit, &fcd->count[L], 0, maxc, &fcd->fetch[L],
+                             sl->gstack.p, kTraceGridThreads, fcd->trav[L], p->profile >= 2, s, ex, 1, true,
+                             L <= packet_levels);  // coherent 8x8-pixel waves -> packet traversal
+                ctx->timer.end(s, id);
+                ++trace_launches;
+                id = ctx->timer.begin(s, CAT_SHADE, CAT_LSHADE + L);
+                launch_shade(ctx->view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex);
+                ctx->timer.end(s, id);
+                if (!staggered && (L == std::min(stagger_level, levels - 1))) {
+                    PGRT_HIP(hipEventRecord(sl->ev_stagger, s));
+                    staggered = true;
+                }
+            }
+            if (ctx->view.nlight > 0 && p->max_level > 0) {  // every level's shadow rays, one launch
+                id = ctx->timer.begin(s, CAT_TRACE);
+                const int sid = ctx->timer.begin(s, CAT_SHADOW);
+                launch_trace(ctx->view, sq.ro, sq.rd, sq.hit, &fcd->shadow_count[0], 0, sq.cap,
+                             &fcd->fetch[kMaxLevels], sl->gstack.p, kTraceGridThreads, fcd->trav[kMaxLevels],
+                             p->profile >= 2, s, sl->expect_shadow_total, levels,
+                             false);  // shadow rays (from the light along H) mostly miss the root
+                ctx->timer.end(s, sid);
+                ctx->timer.end(s, id);
+                ++trace_launches;
+            }
+            id = ctx->timer.begin(s, CAT_COMBINE);
+            for (int L = p->max_level - 1; L >= 1; --L) {
+                LevelNodes ln{sl->n_color[L]->p, sl->n_link[L]->p, sl->n_att[L]->p};
+                launch_combine(ctx->view, L, ln, sl->n_color[L + 1]->p, sq, fcd, std::min(sl->q_cap, sl->level_cap[L]),
+                               s, sl->expect_count[L]);
+            }
+            LevelNodes l0{sl->n_color[0]->p, sl->n_link[0]->p, sl->n_att[0]->p};
+            const bool resolve_l0 = fp.nsb > 1;  // several samples per pixel: trees in parallel
+            if (resolve_l0)
+                launch_combine(ctx->view, 0, l0, levels > 1 ? sl->n_color[1]->p : sl->n_color[0]->p, sq, fcd, n0, s,
+                               n0);
+            launch_finish(ctx->view, fp, sl->tiles.p, l0, levels > 1 ? sl->n_color[1]->p : sl->n_color[0]->p, sq,
+                          sl->accum.p, fs->out, fs->out_mode, fs->ox, fs->oy, fs->pitch, (int)npix, s0 == 0,
+                          s0 + fp.nsb >= spp, K, j, resolve_l0, s);
+            ctx->timer.end(s, id);
+        }
+        sl->host_fc.resize(batches);
+        static const bool export_kernel = [] {  // A/B knob: PGRT_EXPORT=0 copies + memsets instead
+            const char* e = getenv("PGRT_EXPORT");
+            return e ? atoi(e) != 0 : true;
+        }();
+        if (export_kernel) {
+            launch_export_counters(sl->fc.p, sl->pinned_fc, batches, s);  // and zero them for the next frame
+        } else {
             PGRT_HIP(hipMemcpyAsync(sl->pinned_fc, sl->fc.p, sizeof(FrameCounters) * batches, hipMemcpyDeviceToHost,
                                     s));
-            PGRT_HIP(hipEventRecord(sl->ev_done, s));
+            PGRT_HIP(hipMemsetAsync(sl->fc.p, 0, sizeof(FrameCounters) * batches, s));
         }
-        for (int j = 0; j < K; ++j) PGRT_HIP(hipStreamWaitEvent(ctx->stream, ctx->slots[j]->ev_done, 0));
+        if (use_graph) {
+            hipGraph_t graph = nullptr;
+            PGRT_HIP(hipStreamEndCapture(s, &graph));
+            const hipError_t e = hipGraphInstantiate(&sl->gexec, graph, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(graph);
+            PGRT_HIP(e);
+            sl->graph_trace_launches = trace_launches - launches_before;
+            PGRT_HIP(hipGraphLaunch(sl->gexec, s));
+        }
+        if (!staggered) PGRT_HIP(hipEventRecord(sl->ev_stagger, s));
+        PGRT_HIP(hipEventRecord(sl->ev_done, s));
+    }
+    PGRT_HIP(hipGetLastError());
+    fs->stats.trace_launches = trace_launches;
+}
+
+// Wait for fs's frame, re-render it after a queue overflow (larger queues), fill fs->stats; the
+// context stream is then ordered after the frame.
+void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
+    const pgrt_render_params* p = &fs->params;
+    const int levels = p->max_level + 1;
+    const int spp = p->spp_side * p->spp_side;
+    double ms[CAT_N] = {0};
+    uint64_t rays_shadow = 0, rays_reflect = 0, rays_refract = 0, trav_nodes = 0, trav_tests = 0, trav_wide = 0;
+    int retries = 0;
+    for (;;) {
+        const int K = fs->K;
         for (int j = 0; j < K; ++j) {
-            FrameSlot* sl = ctx->slots[j].get();
+            FrameSlot* sl = fs->slots[j].get();
             PGRT_HIP(hipEventSynchronize(sl->ev_done));
             std::copy(sl->pinned_fc, sl->pinned_fc + sl->host_fc.size(), sl->host_fc.begin());
         }
@@ -628,7 +800,7 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
         bool overflow = false;
         ctx->last_fc.clear();
         for (int j = 0; j < K; ++j) {
-            FrameSlot* sl = ctx->slots[j].get();
+            FrameSlot* sl = fs->slots[j].get();
             for (auto& h : sl->host_fc) {
                 overflow |= h.overflow != 0;
                 ctx->last_fc.push_back(h);
@@ -639,20 +811,25 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
                 for (int L = 0; L < kMaxLevels; ++L) sc += h.shadow_count[L];
                 shadow_need = std::max(shadow_need, sc);
             }
-            for (int L = 0; L < kMaxLevels; ++L) {  // grid hints for the next frame
+            // grid hints for the next frame: kept while the count stays within [hint/2, hint]
+            // (a stable hint keeps the captured launch sequence valid)
+            auto hint = [](int& e, int c) {
+                if (e == 0 || c > e || 2 * c + 2048 < e) e = c + c / 4 + 1024;
+            };
+            for (int L = 0; L < kMaxLevels; ++L) {
                 int c = 0;
                 for (auto& h : sl->host_fc) c = std::max(c, h.count[L]);
-                sl->expect_count[L] = c + c / 4 + 1024;
+                hint(sl->expect_count[L], c);
             }
-            sl->expect_shadow_total = shadow_need + shadow_need / 4 + 1024;
+            hint(sl->expect_shadow_total, shadow_need);
         }
         if (overflow) {
-            for (int j = 0; j < K; ++j) grow_after_overflow(ctx->slots[j].get(), levels);
+            for (int j = 0; j < K; ++j) grow_after_overflow(fs->slots[j].get(), levels);
             ctx->timer.collect(ms);
             std::fill(ms, ms + CAT_N, 0.0);
             ++retries;
             PGRT_REQUIRE(retries < 8, PGRT_ERR_OUT_OF_MEMORY, "ray queues kept overflowing");
-            trace_launches = 0;
+            enqueue_frame(ctx, fs);
             continue;
         }
         for (auto& h : ctx->last_fc) {
@@ -671,31 +848,129 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
         }
         break;
     }
-    PGRT_HIP(hipGetLastError());
+    for (int j = 0; j < fs->K; ++j) PGRT_HIP(hipStreamWaitEvent(ctx->stream, fs->slots[j]->ev_done, 0));
     ctx->timer.collect(ms);
-    if (st) {
-        long long real_pix = 0;
-        for (auto& t : tiles) real_pix += (long long)t.z * t.w;
-        st->rays_primary = (uint64_t)(real_pix * spp);
-        st->rays_shadow = rays_shadow;
-        st->rays_reflect = rays_reflect;
-        st->rays_refract = rays_refract;
-        st->node_visits = trav_nodes;
-        st->wide_node_visits = trav_wide;
-        st->tri_tests = trav_tests;
-        st->ms_raygen = ms[CAT_RAYGEN];
-        st->ms_trace = ms[CAT_TRACE];
-        st->ms_shade = ms[CAT_SHADE];
-        st->ms_shadow = ms[CAT_SHADOW];
-        st->ms_combine = ms[CAT_COMBINE];
-        for (int L = 0; L < kMaxLevels; ++L) {
-            ctx->level_ms[L][0] = ms[CAT_LTRACE + L];
-            ctx->level_ms[L][1] = ms[CAT_LSHADE + L];
-        }
-        st->trace_launches = trace_launches;
-        st->levels = levels;
-        st->overflow_retries = retries;
+    pgrt_stats* st = &fs->stats;
+    const int launches = st->trace_launches;
+    *st = pgrt_stats{};
+    long long real_pix = 0;
+    for (auto& t : fs->tiles) real_pix += (long long)t.z * t.w;
+    st->rays_primary = (uint64_t)(real_pix * spp);
+    st->rays_shadow = rays_shadow;
+    st->rays_reflect = rays_reflect;
+    st->rays_refract = rays_refract;
+    st->node_visits = trav_nodes;
+    st->wide_node_visits = trav_wide;
+    st->tri_tests = trav_tests;
+    st->ms_raygen = ms[CAT_RAYGEN];
+    st->ms_trace = ms[CAT_TRACE];
+    st->ms_shade = ms[CAT_SHADE];
+    st->ms_shadow = ms[CAT_SHADOW];
+    st->ms_combine = ms[CAT_COMBINE];
+    for (int L = 0; L < kMaxLevels; ++L) {
+        ctx->level_ms[L][0] = ms[CAT_LTRACE + L];
+        ctx->level_ms[L][1] = ms[CAT_LSHADE + L];
     }
+    st->trace_launches = launches;
+    st->levels = levels;
+    st->overflow_retries = retries;
+}
+
+// distributed frame: ncclGather of every rank's tile-compact buffer to rank 0 and the unpack
+// kernel there, on the context stream (after the frame's slots)
+void gather_frame(pgrt_ctx* ctx, FrameSet* fs) {
+    const int W = fs->cam_w, H = fs->cam_h;
+    const int total = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
+    const int per_rank = (total + ctx->world - 1) / ctx->world;
+    const size_t tile_floats = (size_t)kTile * kTile * 4;
+    if (ctx->world == 1 && !ctx->comm) {
+        launch_unpack_tiles(fs->tilebuf.p, fs->dist_fb, W, H, 1, per_rank, ctx->stream);
+    } else {
+        PGRT_REQUIRE(ctx->comm, PGRT_ERR_RCCL, "pgrt_comm_init has not been called");
+        if (ctx->rank == 0) ctx->gathered.alloc((size_t)per_rank * tile_floats * ctx->world);
+        ncclResult_t r = ncclGather(fs->tilebuf.p, ctx->rank == 0 ? ctx->gathered.p : nullptr,
+                                    (size_t)per_rank * tile_floats, ncclFloat, 0, ctx->comm, ctx->stream);
+        if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string("ncclGather: ") + ncclGetErrorString(r));
+        if (ctx->rank == 0)
+            launch_unpack_tiles(ctx->gathered.p, fs->dist_fb, W, H, ctx->world, per_rank, ctx->stream);
+    }
+    PGRT_HIP(hipGetLastError());
+}
+
+// complete a pending frame: collect, gather (distributed), release the set's buffers
+void finish_frame(pgrt_ctx* ctx, FrameSet* fs) {
+    fs->pending = false;
+    collect_frame(ctx, fs);
+    if (fs->distributed) gather_frame(ctx, fs);
+    PGRT_HIP(hipEventRecord(fs->ev_ready, ctx->stream));
+    fs->has_result = true;
+    fs->stats.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - fs->t0).count();
+}
+
+// finish every pending frame with ticket <= last, oldest first (distributed frames gather in
+// submission order on every rank)
+void finish_through(pgrt_ctx* ctx, unsigned long long last) {
+    for (;;) {
+        FrameSet* oldest = nullptr;
+        for (auto& s : ctx->sets)
+            if (s->pending && s->ticket <= last && (!oldest || s->ticket < oldest->ticket)) oldest = s.get();
+        if (!oldest) return;
+        finish_frame(ctx, oldest);
+    }
+}
+
+void drain_frames(pgrt_ctx* ctx) { finish_through(ctx, ~0ull); }
+
+void check_frame(const pgrt_ctx* ctx, const pgrt_render_params* p) {
+    PGRT_REQUIRE(ctx->has_scene, PGRT_ERR_NO_SCENE, "pgrt_set_scene has not been called");
+    PGRT_REQUIRE(ctx->has_cam, PGRT_ERR_NO_CAMERA, "pgrt_set_camera has not been called");
+    PGRT_REQUIRE(p->spp_side >= 1 && p->spp_side <= 64, PGRT_ERR_INVALID_ARGUMENT, "spp_side must be in [1, 64]");
+    PGRT_REQUIRE(p->max_level >= 0 && p->max_level <= kMaxLevels - 2, PGRT_ERR_INVALID_ARGUMENT,
+                 "max_level must be in [0, 14]");
+}
+
+// Start a frame on set fs (its previous frame must be finished).  distributed: out is ignored,
+// the tiles land in fs->tilebuf and finish_frame gathers them into fb (rank 0).
+void start_frame(pgrt_ctx* ctx, FrameSet* fs, const pgrt_render_params* p, std::vector<int4> tiles, float* out,
+                 int out_mode, int ox, int oy, int pitch, bool distributed, float* fb) {
+    check_frame(ctx, p);
+    fs->t0 = std::chrono::steady_clock::now();
+    fs->params = *p;
+    fs->tiles = std::move(tiles);
+    fs->distributed = distributed;
+    fs->dist_fb = fb;
+    fs->cam_w = ctx->cam.width;
+    fs->cam_h = ctx->cam.height;
+    if (distributed) {
+        const int W = fs->cam_w, H = fs->cam_h;
+        const int total = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
+        const int per_rank = (total + ctx->world - 1) / ctx->world;
+        // padded slots of the tile-compact buffer are never unpacked (t >= total)
+        fs->tilebuf.alloc((size_t)per_rank * kTile * kTile * 4);
+        out = fs->tilebuf.p;
+        out_mode = 1;
+        ox = oy = pitch = 0;
+    }
+    fs->out = out;
+    fs->out_mode = out_mode;
+    fs->ox = ox;
+    fs->oy = oy;
+    fs->pitch = pitch;
+    fs->has_result = false;
+    fs->ticket = ctx->next_ticket++;
+    enqueue_frame(ctx, fs);
+    fs->pending = true;
+}
+
+// Synchronous render of `tiles` (pending asynchronous frames complete first).
+void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<int4>& tiles, float* out,
+                  int out_mode, int ox, int oy, int pitch, pgrt_stats* st) {
+    drain_frames(ctx);
+    FrameSet* fs = frame_set(ctx, 0);
+    PGRT_HIP(hipEventRecord(fs->ev_ready, ctx->stream));  // prior context-stream work first
+    start_frame(ctx, fs, p, tiles, out, out_mode, ox, oy, pitch, false, nullptr);
+    finish_frame(ctx, fs);
+    if (st) *st = fs->stats;
 }
 
 std::vector<int4> rect_tiles(int x0, int y0, int w, int h) {
@@ -773,7 +1048,12 @@ const char* pgrt_last_error(const pgrt_ctx* ctx) { return ctx ? ctx->err.c_str()
 
 int pgrt_set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* scene) {
     if (!ctx) return PGRT_ERR_INVALID_ARGUMENT;
-    return guarded(ctx, [&] { set_scene(ctx, scene); });
+    return guarded(ctx, [&] {
+        drain_frames(ctx);  // frames in flight read the old scene
+        PGRT_HIP(hipStreamSynchronize(ctx->stream));
+        ++ctx->scene_gen;
+        set_scene(ctx, scene);
+    });
 }
 
 int pgrt_bvh_get_info(const pgrt_ctx* ctx, pgrt_bvh_info* info) {
@@ -1006,35 +1286,93 @@ int pgrt_render_distributed_device(pgrt_ctx* ctx, const pgrt_render_params* p, v
     return guarded(ctx, [&] {
         PGRT_REQUIRE(ctx->has_cam, PGRT_ERR_NO_CAMERA, "pgrt_set_camera has not been called");
         PGRT_REQUIRE(ctx->rank != 0 || rgba_device, PGRT_ERR_INVALID_ARGUMENT, "rank 0 needs an output buffer");
-        auto t0 = std::chrono::steady_clock::now();
-        const int W = ctx->cam.width, H = ctx->cam.height;
-        const int total = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
-        const int per_rank = (total + ctx->world - 1) / ctx->world;
-        const size_t tile_floats = (size_t)kTile * kTile * 4;
-        std::vector<int4> mine = rank_tiles(W, H, ctx->rank, ctx->world);
-        ctx->tilebuf.alloc((size_t)per_rank * tile_floats);
-        if ((int)mine.size() < per_rank)
-            PGRT_HIP(hipMemsetAsync(ctx->tilebuf.p, 0, ctx->tilebuf.bytes(), ctx->stream));
-        render_tiles(ctx, p, mine, ctx->tilebuf.p, 1, 0, 0, 0, st);
+        drain_frames(ctx);
+        FrameSet* fs = frame_set(ctx, 0);
+        PGRT_HIP(hipEventRecord(fs->ev_ready, ctx->stream));
+        start_frame(ctx, fs, p, rank_tiles(ctx->cam.width, ctx->cam.height, ctx->rank, ctx->world), nullptr, 1, 0,
+                    0, 0, true, static_cast<float*>(rgba_device));
+        fs->pending = false;
+        collect_frame(ctx, fs);
         auto tg = std::chrono::steady_clock::now();
-        if (ctx->world == 1 && !ctx->comm) {
-            launch_unpack_tiles(ctx->tilebuf.p, static_cast<float*>(rgba_device), W, H, 1, per_rank, ctx->stream);
-        } else {
-            PGRT_REQUIRE(ctx->comm, PGRT_ERR_RCCL, "pgrt_comm_init has not been called");
-            if (ctx->rank == 0) ctx->gathered.alloc((size_t)per_rank * tile_floats * ctx->world);
-            ncclResult_t r = ncclGather(ctx->tilebuf.p, ctx->rank == 0 ? ctx->gathered.p : nullptr,
-                                        (size_t)per_rank * tile_floats, ncclFloat, 0, ctx->comm, ctx->stream);
-            if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string("ncclGather: ") + ncclGetErrorString(r));
-            if (ctx->rank == 0)
-                launch_unpack_tiles(ctx->gathered.p, static_cast<float*>(rgba_device), W, H, ctx->world, per_rank,
-                                    ctx->stream);
-        }
-        PGRT_HIP(hipGetLastError());
+        gather_frame(ctx, fs);
+        PGRT_HIP(hipEventRecord(fs->ev_ready, ctx->stream));
         PGRT_HIP(hipStreamSynchronize(ctx->stream));
-        if (st) {
-            st->ms_gather = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tg).count();
-            st->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        fs->has_result = true;
+        auto t1 = std::chrono::steady_clock::now();
+        fs->stats.ms_gather = std::chrono::duration<double, std::milli>(t1 - tg).count();
+        fs->stats.ms_total = std::chrono::duration<double, std::milli>(t1 - fs->t0).count();
+        if (st) *st = fs->stats;
+    });
+}
+
+// ---- frames in flight ------------------------------------------------------------------
+
+int pgrt_set_frames_in_flight(pgrt_ctx* ctx, int n) {
+    if (!ctx || n < 1 || n > kMaxFramesInFlight) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        drain_frames(ctx);
+        ctx->frames_in_flight = n;
+    });
+}
+
+namespace {
+int submit_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device, unsigned long long* ticket,
+                 bool distributed) {
+    if (!ctx || !p || !ticket || (!distributed && !rgba_device)) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        PGRT_REQUIRE(ctx->has_cam, PGRT_ERR_NO_CAMERA, "pgrt_set_camera has not been called");
+        PGRT_REQUIRE(p->profile == 0, PGRT_ERR_INVALID_ARGUMENT, "profiled frames are synchronous (profile must be 0)");
+        PGRT_REQUIRE(!distributed || ctx->rank != 0 || rgba_device, PGRT_ERR_INVALID_ARGUMENT,
+                     "rank 0 needs an output buffer");
+        FrameSet* fs = frame_set(ctx, (int)(ctx->next_ticket % (unsigned long long)ctx->frames_in_flight));
+        if (fs->pending) finish_through(ctx, fs->ticket);  // the set's previous frame completes first
+        if (distributed) {
+            start_frame(ctx, fs, p, rank_tiles(ctx->cam.width, ctx->cam.height, ctx->rank, ctx->world), nullptr, 1,
+                        0, 0, 0, true, static_cast<float*>(rgba_device));
+        } else {
+            int x, y, w, h;
+            frame_rect(ctx, p, x, y, w, h);
+            start_frame(ctx, fs, p, rect_tiles(x, y, w, h), static_cast<float*>(rgba_device), 0, x, y, w, false,
+                        nullptr);
         }
+        *ticket = fs->ticket;
+    });
+}
+}  // namespace
+
+int pgrt_render_device_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device,
+                             unsigned long long* ticket) {
+    return submit_async(ctx, p, rgba_device, ticket, false);
+}
+
+int pgrt_render_distributed_device_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device,
+                                         unsigned long long* ticket) {
+    return submit_async(ctx, p, rgba_device, ticket, true);
+}
+
+int pgrt_render_wait(pgrt_ctx* ctx, unsigned long long ticket, pgrt_stats* st) {
+    if (!ctx) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        FrameSet* fs = nullptr;
+        for (auto& s : ctx->sets)
+            if ((s->pending || s->has_result) && s->ticket == ticket) fs = s.get();
+        PGRT_REQUIRE(fs, PGRT_ERR_INVALID_ARGUMENT, "unknown ticket (or its frame set was reused)");
+        finish_through(ctx, ticket);
+        PGRT_HIP(hipEventSynchronize(fs->ev_ready));
+        if (st) *st = fs->stats;
+    });
+}
+
+int pgrt_render_tiles_device(pgrt_ctx* ctx, const pgrt_render_params* p, int rank, int world, void* tiles_device,
+                             pgrt_stats* st) {
+    if (!ctx || !p || !tiles_device || world <= 0 || rank < 0 || rank >= world) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        PGRT_REQUIRE(ctx->has_cam, PGRT_ERR_NO_CAMERA, "pgrt_set_camera has not been called");
+        auto t0 = std::chrono::steady_clock::now();
+        render_tiles(ctx, p, rank_tiles(ctx->cam.width, ctx->cam.height, rank, world),
+                     static_cast<float*>(tiles_device), 1, 0, 0, 0, st);
+        PGRT_HIP(hipStreamSynchronize(ctx->stream));
+        if (st) st->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     });
 }
 

@@ -515,6 +515,25 @@ void launch_accumulate_frame(const float* frame, float* sum, float* mean, long l
                        reinterpret_cast<float4*>(mean), pixels, count);
 }
 
+// ------------------------------------------------------------------ counter export
+
+// last launch of a slot's frame: the frame counters go to pinned host memory and the device
+// copy is zeroed for the next frame (replaces a D2H copy + a memset: two fewer queue operations
+// per frame)
+__global__ void k_export_counters(uint4* dev, uint4* host, int n16) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += gridDim.x * blockDim.x) {
+        host[i] = dev[i];
+        dev[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+}
+
+void launch_export_counters(FrameCounters* dev, FrameCounters* host, int n, hipStream_t stream) {
+    static_assert(sizeof(FrameCounters) % 16 == 0, "FrameCounters must be a multiple of 16 bytes");
+    const int n16 = (int)(sizeof(FrameCounters) / 16) * n;
+    hipLaunchKernelGGL(k_export_counters, dim3((unsigned)std::min(64, (n16 + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       stream, reinterpret_cast<uint4*>(dev), reinterpret_cast<uint4*>(host), n16);
+}
+
 // ------------------------------------------------------------------ math self-test
 
 __global__ void k_selftest(const float* in, int n, float* out) {

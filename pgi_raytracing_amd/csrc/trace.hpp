@@ -91,6 +91,8 @@ void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles,
 // frame sink: sum += frame (count-th frame; count == 1 resets), mean = sum / count
 void launch_accumulate_frame(const float* frame, float* sum, float* mean, long long pixels, int count,
                              hipStream_t stream);
+// copy `n` FrameCounters to pinned host memory and zero them on the device
+void launch_export_counters(FrameCounters* dev, FrameCounters* host, int n, hipStream_t stream);
 void launch_unpack_tiles(const float* gathered, float* rgba, int width, int height, int world, int tiles_per_rank,
                          hipStream_t stream);
 

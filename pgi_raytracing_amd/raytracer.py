@@ -57,11 +57,17 @@ def lib():
         "pgrt_accumulate_reset": (ip, [vp]),
         "pgrt_render_accumulate": (ip, [vp, C.POINTER(abi.RenderParams), fp, C.POINTER(C.c_int),
                                         C.POINTER(abi.Stats)]),
+        "pgrt_set_frames_in_flight": (ip, [vp, ip]),
+        "pgrt_render_device_async": (ip, [vp, C.POINTER(abi.RenderParams), vp, C.POINTER(C.c_ulonglong)]),
+        "pgrt_render_distributed_device_async": (ip, [vp, C.POINTER(abi.RenderParams), vp,
+                                                      C.POINTER(C.c_ulonglong)]),
+        "pgrt_render_wait": (ip, [vp, C.c_ulonglong, C.POINTER(abi.Stats)]),
         "pgrt_tile_count": (ip, [ip, ip, ip, ip, ip]),
         "pgrt_tile_rect": (ip, [ip, ip, ip, ip, C.POINTER(C.c_int)]),
         "pgrt_unpack_tiles_host": (ip, [ip, ip, ip, ip, fp, fp]),
         "pgrt_comm_unique_id": (ip, [C.c_char_p]),
         "pgrt_comm_init": (ip, [vp, ip, ip, C.c_char_p]),
+        "pgrt_render_tiles_device": (ip, [vp, C.POINTER(abi.RenderParams), ip, ip, vp, C.POINTER(abi.Stats)]),
         "pgrt_render_distributed": (ip, [vp, C.POINTER(abi.RenderParams), fp, C.POINTER(abi.Stats)]),
         "pgrt_render_distributed_device": (ip, [vp, C.POINTER(abi.RenderParams), vp, C.POINTER(abi.Stats)]),
         "pgrt_obj_load": (ip, [C.c_char_p, ip, C.POINTER(vp)]),
@@ -205,6 +211,28 @@ class Context:
         _check(self.h, self.L.pgrt_selftest_math(self.h, abi.fptr(pairs), pairs.shape[0], abi.fptr(out)))
         return out
 
+    # ---- frames in flight ----
+    def set_frames_in_flight(self, n: int):
+        _check(self.h, self.L.pgrt_set_frames_in_flight(self.h, n))
+
+    def render_device_async(self, params, dev_ptr: int) -> int:
+        """Enqueue a frame (pgrt_render_device_async); returns its ticket."""
+        t = C.c_ulonglong()
+        _check(self.h, self.L.pgrt_render_device_async(self.h, C.byref(params), C.c_void_p(dev_ptr), C.byref(t)))
+        return t.value
+
+    def render_distributed_device_async(self, params, dev_ptr: int | None) -> int:
+        t = C.c_ulonglong()
+        _check(self.h, self.L.pgrt_render_distributed_device_async(self.h, C.byref(params), C.c_void_p(dev_ptr or 0),
+                                                                   C.byref(t)))
+        return t.value
+
+    def render_wait(self, ticket: int):
+        """Complete the frames up to `ticket`; returns that frame's Stats."""
+        st = abi.Stats()
+        _check(self.h, self.L.pgrt_render_wait(self.h, C.c_ulonglong(ticket), C.byref(st)))
+        return st
+
     # ---- multi-GPU ----
     @staticmethod
     def comm_unique_id() -> bytes:
@@ -216,6 +244,13 @@ class Context:
 
     def comm_init(self, world: int, rank: int, uid: bytes):
         _check(self.h, self.L.pgrt_comm_init(self.h, world, rank, C.c_char_p(uid)))
+
+    def render_tiles_device(self, params, rank: int, world: int, dev_ptr: int):
+        """This rank's tiles into a tile-compact device buffer (pgrt_render_tiles_device)."""
+        st = abi.Stats()
+        _check(self.h, self.L.pgrt_render_tiles_device(self.h, C.byref(params), rank, world, C.c_void_p(dev_ptr),
+                                                       C.byref(st)))
+        return st
 
     def render_distributed_device(self, params, dev_ptr: int | None):
         st = abi.Stats()

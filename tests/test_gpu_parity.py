@@ -259,3 +259,35 @@ def test_progressive_accumulation_is_mean_of_frames(gpu_ctx, avenger_scene):
     m1, n1 = gpu_ctx.render_accumulate(abi.make_params(spp_side=1, max_level=3, dof=1, jitter=abi.PGRT_JITTER_HASH,
                                                        frame=0))
     assert n1 == 1 and ((m1 == frames[0]) | (np.isnan(m1) & np.isnan(frames[0]))).all()
+
+
+def test_frames_in_flight_match_synchronous(gpu_ctx, avenger_scene):
+    """Asynchronous frames (3 in flight, different depth / spp / DoF / seed per frame, the
+    distributed form included) are bit-identical to synchronous renders; a recycled ticket is
+    refused."""
+    from pgi_raytracing_amd.raytracer import PgrtError
+
+    gpu_ctx.set_scene(avenger_scene)
+    W, H = 200, 120
+    gpu_ctx.set_camera(abi.default_camera(W, H))
+    params = [abi.make_params(max_level=5 if f % 2 == 0 else 3, spp_side=2 if f % 3 == 2 else 1, dof=f % 2,
+                              jitter=abi.PGRT_JITTER_HASH, frame=f) for f in range(7)]
+    refs = [gpu_ctx.render(p) for p in params]
+    bufs = [gpu_ctx.alloc(W * H * 16) for _ in params]
+    try:
+        gpu_ctx.set_frames_in_flight(3)
+        tickets = [gpu_ctx.render_device_async(p, b) if f != 4 else gpu_ctx.render_distributed_device_async(p, b)
+                   for f, (p, b) in enumerate(zip(params, bufs))]
+        with pytest.raises(PgrtError):
+            gpu_ctx.render_wait(tickets[0])  # its frame set was reused by tickets[3]
+        stats = [gpu_ctx.render_wait(t) for t in tickets[4:]]
+        for (ref, st_ref), st in zip(refs[4:], stats):
+            assert st.rays() == st_ref.rays()
+        for f, (b, (ref, _)) in enumerate(zip(bufs, refs)):
+            out = gpu_ctx.to_host(b, (H, W, 4))
+            same = (out == ref) | (np.isnan(out) & np.isnan(ref))
+            assert same.all(), f"frame {f}: {(~same).sum()} pixels differ"
+    finally:
+        gpu_ctx.set_frames_in_flight(1)
+        for b in bufs:
+            gpu_ctx.free(b)
