@@ -232,6 +232,7 @@ struct pgrt_ctx {
     SceneView view{};
     bool has_scene = false;
     unsigned long long scene_gen = 0;  // bumped by every pgrt_set_scene
+    bool group_max_env = false;        // PGRT_GROUP_MAX given (else the default follows the mode)
     pgrt_bvh_info info{};
 
     CameraView cam{};
@@ -457,6 +458,7 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
     v.depth8 = wide_depth;
     const char* eg = getenv("PGRT_GROUP_MAX");  // read per set_scene (tests compare settings)
     v.group_max = eg ? atoi(eg) : kDefaultGroupMax;
+    ctx->group_max_env = eg != nullptr;
     v.wide = width == 8 ? 1 : 0;
     v.ntri = n;
     v.depth = bo.max_depth;
@@ -601,6 +603,8 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
         return e ? atoi(e) : 0;
     }();
     const int K = ntiles == 0 ? 0 : std::max(1, std::min(want_slots, ntiles));
+    SceneView view = ctx->view;
+    if (!ctx->group_max_env && ctx->frames_in_flight > 1) view.group_max = kDefaultGroupMaxInFlight;
     fs->K = K;
     while ((int)fs->slots.size() < K) fs->slots.emplace_back(new FrameSlot());
     ctx->timer.on = p->profile > 0;
@@ -633,7 +637,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
         PGRT_REQUIRE(npix <= kMaxBatchRays * 8, PGRT_ERR_INVALID_ARGUMENT, "frame too large");
         const int nsb = (int)std::max(1ll, std::min<long long>(spp, kMaxBatchRays / npix));
         const int batches = (spp + nsb - 1) / nsb;
-        ensure_frame_buffers(sl, (int)(npix * nsb), levels, ctx->view.nlight, batches);
+        ensure_frame_buffers(sl, (int)(npix * nsb), levels, view.nlight, batches);
         sl->ensure_pinned(batches, nt);
         if (sl->tiles.n < (size_t)nt) sl->tiles_dev.clear();
         sl->tiles.alloc(nt);
@@ -648,7 +652,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             Signature g;
             g.add(*p);
             g.add(ctx->cam);
-            g.add(ctx->view);
+            g.add(view);
             g.add(ctx->scene_gen);
             g.add(K);
             g.add(j);
@@ -712,23 +716,23 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 // grid hints: last frame's per-level counts (+25 %); level 0 is exact
                 const int ex = L == 0 ? n0 : sl->expect_count[L];
                 id = ctx->timer.begin(s, CAT_TRACE, CAT_LTRACE + L);
-                launch_trace(ctx->view, qc.ro, qc.rd, qc.hit, &fcd->count[L], 0, maxc, &fcd->fetch[L],
+                launch_trace(view, qc.ro, qc.rd, qc.hit, &fcd->count[L], 0, maxc, &fcd->fetch[L],
                              sl->gstack.p, kTraceGridThreads, fcd->trav[L], p->profile >= 2, s, ex, 1, true,
                              L <= packet_levels);  // coherent 8x8-pixel waves -> packet traversal
                 ctx->timer.end(s, id);
                 ++trace_launches;
                 id = ctx->timer.begin(s, CAT_SHADE, CAT_LSHADE + L);
-                launch_shade(ctx->view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex);
+                launch_shade(view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex);
                 ctx->timer.end(s, id);
                 if (!staggered && (L == std::min(stagger_level, levels - 1))) {
                     PGRT_HIP(hipEventRecord(sl->ev_stagger, s));
                     staggered = true;
                 }
             }
-            if (ctx->view.nlight > 0 && p->max_level > 0) {  // every level's shadow rays, one launch
+            if (view.nlight > 0 && p->max_level > 0) {  // every level's shadow rays, one launch
                 id = ctx->timer.begin(s, CAT_TRACE);
                 const int sid = ctx->timer.begin(s, CAT_SHADOW);
-                launch_trace(ctx->view, sq.ro, sq.rd, sq.hit, &fcd->shadow_count[0], 0, sq.cap,
+                launch_trace(view, sq.ro, sq.rd, sq.hit, &fcd->shadow_count[0], 0, sq.cap,
                              &fcd->fetch[kMaxLevels], sl->gstack.p, kTraceGridThreads, fcd->trav[kMaxLevels],
                              p->profile >= 2, s, sl->expect_shadow_total, levels,
                              false);  // shadow rays (from the light along H) mostly miss the root
@@ -739,15 +743,15 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             id = ctx->timer.begin(s, CAT_COMBINE);
             for (int L = p->max_level - 1; L >= 1; --L) {
                 LevelNodes ln{sl->n_color[L]->p, sl->n_link[L]->p, sl->n_att[L]->p};
-                launch_combine(ctx->view, L, ln, sl->n_color[L + 1]->p, sq, fcd, std::min(sl->q_cap, sl->level_cap[L]),
+                launch_combine(view, L, ln, sl->n_color[L + 1]->p, sq, fcd, std::min(sl->q_cap, sl->level_cap[L]),
                                s, sl->expect_count[L]);
             }
             LevelNodes l0{sl->n_color[0]->p, sl->n_link[0]->p, sl->n_att[0]->p};
             const bool resolve_l0 = fp.nsb > 1;  // several samples per pixel: trees in parallel
             if (resolve_l0)
-                launch_combine(ctx->view, 0, l0, levels > 1 ? sl->n_color[1]->p : sl->n_color[0]->p, sq, fcd, n0, s,
+                launch_combine(view, 0, l0, levels > 1 ? sl->n_color[1]->p : sl->n_color[0]->p, sq, fcd, n0, s,
                                n0);
-            launch_finish(ctx->view, fp, sl->tiles.p, l0, levels > 1 ? sl->n_color[1]->p : sl->n_color[0]->p, sq,
+            launch_finish(view, fp, sl->tiles.p, l0, levels > 1 ? sl->n_color[1]->p : sl->n_color[0]->p, sq,
                           sl->accum.p, fs->out, fs->out_mode, fs->ox, fs->oy, fs->pitch, (int)npix, s0 == 0,
                           s0 + fp.nsb >= spp, K, j, resolve_l0, s);
             ctx->timer.end(s, id);

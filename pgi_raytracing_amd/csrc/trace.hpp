@@ -103,6 +103,9 @@ constexpr float kDefaultSplitBeta = 0.0f;  // PGRT_SPLIT default (extra referenc
 constexpr int kDefaultSlots = 2;           // PGRT_SLOTS default: staggered pipeline slots per frame
 constexpr int kDefaultGroupMax = 400000;   // PGRT_GROUP_MAX default: queues up to this many rays use
                                            // the 8-lanes-per-ray kernel (r1 A/B: tail levels -45 %)
+constexpr int kDefaultGroupMaxInFlight = 100000;  // with frames in flight the concurrent frames hide
+                                                  // the latency floors: level 2 (~150k rays) runs
+                                                  // faster one lane per ray (r1 scan: 0.392 -> 0.366)
 struct BuildOut {
     int builder;   // in: kBuilder*
     int leaf_max;  // in: triangles per binary leaf (<= kLeafMaxTris)
