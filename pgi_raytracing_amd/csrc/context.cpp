@@ -886,9 +886,9 @@ void gather_frame(pgrt_ctx* ctx, FrameSet* fs) {
     const int W = fs->cam_w, H = fs->cam_h;
     const int total = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
     const int per_rank = (total + ctx->world - 1) / ctx->world;
-    const size_t tile_floats = (size_t)kTile * kTile * 4;
+    const size_t tile_floats = (size_t)kTile * kTile * 3;  // RGB tiles (out_mode 2)
     if (ctx->world == 1 && !ctx->comm) {
-        launch_unpack_tiles(fs->tilebuf.p, fs->dist_fb, W, H, 1, per_rank, ctx->stream);
+        launch_unpack_tiles(fs->tilebuf.p, fs->dist_fb, W, H, 1, per_rank, 3, ctx->stream);
     } else {
         PGRT_REQUIRE(ctx->comm, PGRT_ERR_RCCL, "pgrt_comm_init has not been called");
         if (ctx->rank == 0) ctx->gathered.alloc((size_t)per_rank * tile_floats * ctx->world);
@@ -896,7 +896,7 @@ void gather_frame(pgrt_ctx* ctx, FrameSet* fs) {
                                     (size_t)per_rank * tile_floats, ncclFloat, 0, ctx->comm, ctx->stream);
         if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string("ncclGather: ") + ncclGetErrorString(r));
         if (ctx->rank == 0)
-            launch_unpack_tiles(ctx->gathered.p, fs->dist_fb, W, H, ctx->world, per_rank, ctx->stream);
+            launch_unpack_tiles(ctx->gathered.p, fs->dist_fb, W, H, ctx->world, per_rank, 3, ctx->stream);
     }
     PGRT_HIP(hipGetLastError());
 }
@@ -950,9 +950,9 @@ void start_frame(pgrt_ctx* ctx, FrameSet* fs, const pgrt_render_params* p, std::
         const int total = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
         const int per_rank = (total + ctx->world - 1) / ctx->world;
         // padded slots of the tile-compact buffer are never unpacked (t >= total)
-        fs->tilebuf.alloc((size_t)per_rank * kTile * kTile * 4);
+        fs->tilebuf.alloc((size_t)per_rank * kTile * kTile * 3);
         out = fs->tilebuf.p;
-        out_mode = 1;
+        out_mode = 2;
         ox = oy = pitch = 0;
     }
     fs->out = out;

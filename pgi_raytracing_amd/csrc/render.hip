@@ -434,16 +434,22 @@ __global__ __launch_bounds__(kBlock) void k_finish(SceneView s, FrameParams fp, 
     const int area = fp.spp_side * fp.spp_side;
     // gamma(Color4f{final.b/area, final.g/area, final.r/area}) (raytracer.cpp:431-435)
     const float4 o = gamma_rgba(acc.z / (float)area, acc.y / (float)area, acc.x / (float)area, fp.gamma);
-    float* dst;
     if (out_mode == 0) {
-        dst = out + ((size_t)(py - oy) * (size_t)pitch + (size_t)(px - ox)) * 4;
-    } else {
-        const int tile = p / (kTile * kTile);
-        const int4 tr = tiles[tile];
-        const size_t gtile = (size_t)tile * K + j;  // position in the caller's tile list
-        dst = out + (gtile * kTile * kTile + (size_t)(py - tr.y) * kTile + (size_t)(px - tr.x)) * 4;
+        float* dst = out + ((size_t)(py - oy) * (size_t)pitch + (size_t)(px - ox)) * 4;
+        *reinterpret_cast<float4*>(dst) = o;
+        return;
     }
-    *reinterpret_cast<float4*>(dst) = o;
+    const int tile = p / (kTile * kTile);
+    const int4 tr = tiles[tile];
+    const size_t gtile = (size_t)tile * K + j;  // position in the caller's tile list
+    const size_t q = gtile * kTile * kTile + (size_t)(py - tr.y) * kTile + (size_t)(px - tr.x);
+    if (out_mode == 1) {
+        *reinterpret_cast<float4*>(out + q * 4) = o;
+    } else {  // 2: RGB only (alpha is always 1): the multi-GPU gather moves 12 B per pixel
+        out[q * 3 + 0] = o.x;
+        out[q * 3 + 1] = o.y;
+        out[q * 3 + 2] = o.z;
+    }
 }
 
 void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles, LevelNodes l0, const float4* child,
@@ -456,8 +462,8 @@ void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles,
 
 // ------------------------------------------------------------------ multi-GPU unpack
 
-__global__ __launch_bounds__(kBlock) void k_unpack(const float4* __restrict__ g, float4* __restrict__ rgba, int width,
-                                                   int height, int world, int tiles_per_rank) {
+__global__ __launch_bounds__(kBlock) void k_unpack(const float* __restrict__ g, float4* __restrict__ rgba, int width,
+                                                   int height, int world, int tiles_per_rank, int channels) {
     const long long idx = (long long)blockIdx.x * kBlock + threadIdx.x;
     const long long per_rank = (long long)tiles_per_rank * kTile * kTile;
     if (idx >= per_rank * world) return;
@@ -472,16 +478,16 @@ __global__ __launch_bounds__(kBlock) void k_unpack(const float4* __restrict__ g,
     const int x = (t % tiles_x) * kTile + (p % kTile);
     const int y = (t / tiles_x) * kTile + (p / kTile);
     if (x >= width || y >= height) return;
-    rgba[(size_t)y * width + x] = g[idx];
+    rgba[(size_t)y * width + x] = channels == 4 ? reinterpret_cast<const float4*>(g)[idx]
+                                                 : make_float4(g[idx * 3], g[idx * 3 + 1], g[idx * 3 + 2], 1.0f);
 }
 
 void launch_unpack_tiles(const float* gathered, float* rgba, int width, int height, int world, int tiles_per_rank,
-                         hipStream_t stream) {
+                         int channels, hipStream_t stream) {
     const long long total = (long long)world * tiles_per_rank * kTile * kTile;
     if (total <= 0) return;
-    hipLaunchKernelGGL(k_unpack, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
-                       reinterpret_cast<const float4*>(gathered), reinterpret_cast<float4*>(rgba), width, height,
-                       world, tiles_per_rank);
+    hipLaunchKernelGGL(k_unpack, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, gathered,
+                       reinterpret_cast<float4*>(rgba), width, height, world, tiles_per_rank, channels);
 }
 
 // ------------------------------------------------------------------ progressive accumulation

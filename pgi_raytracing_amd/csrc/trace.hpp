@@ -81,7 +81,8 @@ void launch_shade(const SceneView& s, const FrameParams& fp, int level, Queue q,
 void launch_combine(const SceneView& s, int level, LevelNodes nodes, const float4* child, ShadowQueue sq,
                     const FrameCounters* fc, int max_count, hipStream_t stream, int expect = 0);
 // level-0 combine + sample accumulation (+ gamma and framebuffer write on the last batch).
-// out_mode 0: framebuffer (rect origin ox,oy, row pitch in pixels); 1: tile-compact
+// out_mode 0: framebuffer (rect origin ox,oy, row pitch in pixels); 1: tile-compact RGBA;
+// 2: tile-compact RGB (the multi-GPU gather format)
 // tiles of this launch are tiles j, j + K, ... of the caller's list (pipeline slot j of K):
 // out_mode 1 writes local tile t at tile-compact position t * K + j.  resolved: level 0's final
 // colours were written by launch_combine(level 0) (several samples per pixel)
@@ -93,8 +94,9 @@ void launch_accumulate_frame(const float* frame, float* sum, float* mean, long l
                              hipStream_t stream);
 // copy `n` FrameCounters to pinned host memory and zero them on the device
 void launch_export_counters(FrameCounters* dev, FrameCounters* host, int n, hipStream_t stream);
+// gathered: rank-major tile-compact buffers, `channels` floats per pixel (4: RGBA, 3: RGB + alpha 1)
 void launch_unpack_tiles(const float* gathered, float* rgba, int width, int height, int world, int tiles_per_rank,
-                         hipStream_t stream);
+                         int channels, hipStream_t stream);
 
 // scene / BVH build
 constexpr int kBuilderLbvh = 0;  // Karras 2012 over 63-bit Morton codes
