@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--dof", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--roofline-only", action="store_true",
+                    help="only the profiled roofline frames (the run profiles/ rocprofv3 summaries are taken of)")
     ap.add_argument("--in-flight", type=int, default=None,
                     help="frames in flight (pgrt_set_frames_in_flight); default 6 (r1 scan, tools/inflight_scan.py)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -131,6 +133,8 @@ def main():
             rays_n += ctx.render_wait(pending.popleft()).rays()
         return rays_n
 
+    if args.roofline_only:
+        args.warmup = args.steps = 0
     run_frames(args.warmup)
     ctx.synchronize()
     if dist:
@@ -142,11 +146,12 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     # frame latency (one synchronous frame at a time), reported beside the throughput
-    lat = []
+    lat = [0.0]
     for _ in range(min(args.steps, 30)):
         t1 = time.perf_counter()
         frame(params)
         lat.append(time.perf_counter() - t1)
+    lat = lat[1:] or lat
     latency_ms = sorted(lat)[len(lat) // 2] * 1e3
     if dist:
         import torch
@@ -208,6 +213,14 @@ def main():
                 roof["traffic"] = json.load(open(tf)).get("bytes_per_launch")
             except Exception:  # noqa: BLE001
                 pass
+
+    if args.roofline_only:
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "config": args.config, "roofline": roof}), flush=True)
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     host_fb = None
     if world == 1 and not args.no_roofline:

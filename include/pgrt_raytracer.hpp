@@ -206,6 +206,23 @@ public:
         return frames;
     }
 
+    // Frames in flight (pgrt_render_device_async): the Producer loop without a host round trip
+    // per frame.  Submit enqueues the next frame into a device framebuffer (pgrt_device_alloc,
+    // W*H*4 floats) and returns at once; Wait completes every frame up to the ticket.
+    void SetFramesInFlight(int n) { check(ctx_, pgrt_set_frames_in_flight(ctx_, n), "pgrt_set_frames_in_flight"); }
+    unsigned long long Submit(void* rgba_device) {
+        params_.gamma_level = gamma_level;
+        unsigned long long t = 0;
+        check(ctx_, pgrt_render_device_async(ctx_, &params_, rgba_device, &t), "pgrt_render_device_async");
+        ++params_.frame;
+        return t;
+    }
+    pgrt_stats Wait(unsigned long long ticket) {
+        pgrt_stats st{};
+        check(ctx_, pgrt_render_wait(ctx_, ticket, &st), "pgrt_render_wait");
+        return st;
+    }
+
     // get_pixel(x, y, t) (raytracer.cpp:396-437): reads the last rendered frame.
     Color4f get_pixel(const int x, const int y, const float /*t*/ = 0.0f) {
         if (frame_.empty()) Render();

@@ -52,6 +52,22 @@ struct StageTimer {
     void end(hipStream_t s, int id) {
         if (id >= 0) PGRT_HIP(hipEventRecord(recs[id].b, s));
     }
+    // a closest-hit launch: its kernel records the pair itself (set_trace_events); nothing
+    // launched -> both recorded here (zero time)
+    int begin_kernel(int cat, int cat2 = -1) {
+        if (!on) return -1;
+        recs.push_back(Rec{get(), get(), cat, cat2});
+        const int id = (int)recs.size() - 1;
+        set_trace_events(recs[id].a, recs[id].b);
+        return id;
+    }
+    void end_kernel(hipStream_t s, int id, bool launched) {
+        set_trace_events(nullptr, nullptr);
+        if (id >= 0 && !launched) {
+            PGRT_HIP(hipEventRecord(recs[id].a, s));
+            PGRT_HIP(hipEventRecord(recs[id].b, s));
+        }
+    }
     void collect(double* ms) {  // after stream sync
         for (auto& r : recs) {
             float t = 0;
@@ -569,6 +585,18 @@ void grow_after_overflow(FrameSlot* sl, int levels) {
     }
 }
 
+// PGRT_DEBUG_SYNC=1: synchronise after every launch of the frame pipeline and name the launch
+// that failed (a device fault is otherwise reported by whichever HIP call comes next)
+void debug_sync(hipStream_t s, const char* what, int level, int batch) {
+    static const bool on = getenv("PGRT_DEBUG_SYNC") != nullptr;
+    if (!on) return;
+    hipError_t e = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e != hipSuccess)
+        throw Error(PGRT_ERR_HIP, std::string(what) + " (level " + std::to_string(level) + ", batch " +
+                                      std::to_string(batch) + "): " + hipGetErrorString(e));
+}
+
 FrameSet* frame_set(pgrt_ctx* ctx, int i) {
     while ((int)ctx->sets.size() <= i) {
         ctx->sets.emplace_back(new FrameSet());
@@ -706,6 +734,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             ShadowQueue sq{sl->s_ro.p, sl->s_rd.p, sl->s_hit.p, sl->s_contrib.p, sl->s_cap};
             int id = ctx->timer.begin(s, CAT_RAYGEN);
             launch_raygen(ctx->cam, fp, sl->tiles.p, q[0], n0, fcd, s);
+            debug_sync(s, "raygen", 0, bi);
             ctx->timer.end(s, id);
             for (int L = 0; L < levels; ++L) {
                 Queue qc = q[L & 1], qn = q[(L + 1) & 1];
@@ -715,14 +744,17 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 LevelNodes ln{sl->n_color[L]->p, sl->n_link[L]->p, sl->n_att[L]->p};
                 // grid hints: last frame's per-level counts (+25 %); level 0 is exact
                 const int ex = L == 0 ? n0 : sl->expect_count[L];
-                id = ctx->timer.begin(s, CAT_TRACE, CAT_LTRACE + L);
-                launch_trace(view, qc.ro, qc.rd, qc.hit, &fcd->count[L], 0, maxc, &fcd->fetch[L],
-                             sl->gstack.p, kTraceGridThreads, fcd->trav[L], p->profile >= 2, s, ex, 1, true,
-                             L <= packet_levels);  // coherent 8x8-pixel waves -> packet traversal
-                ctx->timer.end(s, id);
+                id = ctx->timer.begin_kernel(CAT_TRACE, CAT_LTRACE + L);
+                const bool launched =
+                    launch_trace(view, qc.ro, qc.rd, qc.hit, &fcd->count[L], 0, maxc, &fcd->fetch[L], sl->gstack.p,
+                                 kTraceGridThreads, fcd->trav[L], p->profile >= 2, s, ex, 1, true,
+                                 L <= packet_levels);  // coherent 8x8-pixel waves -> packet traversal
+                ctx->timer.end_kernel(s, id, launched);
+                debug_sync(s, "trace", L, bi);
                 ++trace_launches;
                 id = ctx->timer.begin(s, CAT_SHADE, CAT_LSHADE + L);
                 launch_shade(view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex);
+                debug_sync(s, "shade", L, bi);
                 ctx->timer.end(s, id);
                 if (!staggered && (L == std::min(stagger_level, levels - 1))) {
                     PGRT_HIP(hipEventRecord(sl->ev_stagger, s));
@@ -730,14 +762,13 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 }
             }
             if (view.nlight > 0 && p->max_level > 0) {  // every level's shadow rays, one launch
-                id = ctx->timer.begin(s, CAT_TRACE);
-                const int sid = ctx->timer.begin(s, CAT_SHADOW);
-                launch_trace(view, sq.ro, sq.rd, sq.hit, &fcd->shadow_count[0], 0, sq.cap,
-                             &fcd->fetch[kMaxLevels], sl->gstack.p, kTraceGridThreads, fcd->trav[kMaxLevels],
-                             p->profile >= 2, s, sl->expect_shadow_total, levels,
-                             false);  // shadow rays (from the light along H) mostly miss the root
-                ctx->timer.end(s, sid);
-                ctx->timer.end(s, id);
+                id = ctx->timer.begin_kernel(CAT_TRACE, CAT_SHADOW);
+                const bool launched = launch_trace(
+                    view, sq.ro, sq.rd, sq.hit, &fcd->shadow_count[0], 0, sq.cap, &fcd->fetch[kMaxLevels],
+                    sl->gstack.p, kTraceGridThreads, fcd->trav[kMaxLevels], p->profile >= 2, s,
+                    sl->expect_shadow_total, levels, false);  // shadow rays (from the light along H) mostly miss the root
+                ctx->timer.end_kernel(s, id, launched);
+                debug_sync(s, "shadow trace", levels, bi);
                 ++trace_launches;
             }
             id = ctx->timer.begin(s, CAT_COMBINE);
@@ -751,9 +782,11 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             if (resolve_l0)
                 launch_combine(view, 0, l0, levels > 1 ? sl->n_color[1]->p : sl->n_color[0]->p, sq, fcd, n0, s,
                                n0);
+            debug_sync(s, "combine", 0, bi);
             launch_finish(view, fp, sl->tiles.p, l0, levels > 1 ? sl->n_color[1]->p : sl->n_color[0]->p, sq,
                           sl->accum.p, fs->out, fs->out_mode, fs->ox, fs->oy, fs->pitch, (int)npix, s0 == 0,
                           s0 + fp.nsb >= spp, K, j, resolve_l0, s);
+            debug_sync(s, "finish", 0, bi);
             ctx->timer.end(s, id);
         }
         sl->host_fc.resize(batches);
@@ -763,6 +796,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
         }();
         if (export_kernel) {
             launch_export_counters(sl->fc.p, sl->pinned_fc, batches, s);  // and zero them for the next frame
+            debug_sync(s, "export", 0, 0);
         } else {
             PGRT_HIP(hipMemcpyAsync(sl->pinned_fc, sl->fc.p, sizeof(FrameCounters) * batches, hipMemcpyDeviceToHost,
                                     s));

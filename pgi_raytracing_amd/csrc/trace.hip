@@ -18,6 +18,8 @@
 #include "shade_ops.hpp"
 #include <string>
 
+#include <hip/hip_ext.h>
+
 #include "trace.hpp"
 
 namespace pgrt {
@@ -708,22 +710,35 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const fl
     }
 }
 
-void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4* hits, const int* count_dev,
+// Kernel-exact launch timing (profile frames): the closest-hit launch records the caller's
+// events itself (hipExtLaunchKernel: taken by the packet processor at kernel start / end, the
+// same clock rocprofv3's kernel trace reads), instead of event records queued around it.
+namespace {
+thread_local hipEvent_t t_ev_start = nullptr, t_ev_stop = nullptr;
+}
+void set_trace_events(hipEvent_t start, hipEvent_t stop) {
+    t_ev_start = start;
+    t_ev_stop = stop;
+}
+#define PGRT_TLAUNCH(kernel, grid, block, lds, stream, ...) \
+    hipExtLaunchKernelGGL(kernel, grid, block, lds, stream, t_ev_start, t_ev_stop, 0, __VA_ARGS__)
+
+bool launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4* hits, const int* count_dev,
                   int count_host, int max_count, int* fetch, int* gstack, int gstack_threads,
                   unsigned long long* counters, bool count, hipStream_t stream, int expect, int count_terms,
                   bool allow_group, bool coherent) {
-    if (max_count <= 0) return;
+    if (max_count <= 0) return false;
     static const bool force_spill = getenv("PGRT_FORCE_SPILL") != nullptr;  // A/B of the stack layout
     if (s.wide) {
         int grid = ceil_div(expect > 0 && expect < max_count ? expect : max_count, kTraceBlock);
         if (grid > gstack_threads / kTraceBlock) grid = gstack_threads / kTraceBlock;
         if (count)
-            hipLaunchKernelGGL((k_trace8<true>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
+            PGRT_TLAUNCH((k_trace8<true>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
                                count_dev, count_terms, count_host, max_count, gstack, counters);
         else
-            hipLaunchKernelGGL((k_trace8<false>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
+            PGRT_TLAUNCH((k_trace8<false>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
                                count_dev, count_terms, count_host, max_count, gstack, counters);
-        return;
+        return true;
     }
     // small queues: 8 lanes per ray over the 8-wide BVH (PGRT_GROUP_MAX: largest queue, rays)
     static const bool packets = [] {  // PGRT_PACKETS=0: level 0 on the one-lane kernel too
@@ -735,12 +750,12 @@ void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4
         int grid = ceil_div(exg, kTraceBlock);
         if (grid > 16384) grid = 16384;
         if (count)
-            hipLaunchKernelGGL((k_trace_pkt<true>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
+            PGRT_TLAUNCH((k_trace_pkt<true>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
                                count_dev, count_terms, count_host, max_count, counters);
         else
-            hipLaunchKernelGGL((k_trace_pkt<false>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
+            PGRT_TLAUNCH((k_trace_pkt<false>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
                                count_dev, count_terms, count_host, max_count, counters);
-        return;
+        return true;
     }
     const int group_max = s.group_max;
     static const int group8_max = [] {
@@ -754,7 +769,7 @@ void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4
             // 4 lanes (two child slots each) when there are enough rays to fill the machine
             const bool g4 = exg > group8_max;
 #define PGRT_LAUNCH_G(C, G)                                                                                        \
-    hipLaunchKernelGGL((k_trace8g<C, G>), dim3(ceil_div(exg, kTraceBlock / G) > 16384 ? 16384 : ceil_div(exg, kTraceBlock / G)), \
+    PGRT_TLAUNCH((k_trace8g<C, G>), dim3(ceil_div(exg, kTraceBlock / G) > 16384 ? 16384 : ceil_div(exg, kTraceBlock / G)), \
                        dim3(kTraceBlock), 0, stream, s, ro, rd, hits, count_dev, count_terms, count_host, max_count, counters)
             if (count) {
                 if (g4) PGRT_LAUNCH_G(true, 4); else PGRT_LAUNCH_G(true, 8);
@@ -762,7 +777,7 @@ void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4
                 if (g4) PGRT_LAUNCH_G(false, 4); else PGRT_LAUNCH_G(false, 8);
             }
 #undef PGRT_LAUNCH_G
-            return;
+            return true;
         }
     }
     // rays per wave: full waves for big queues; small (tail) queues may spread thinner
@@ -783,7 +798,7 @@ void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4
     const bool spill = force_spill || entries * kTraceBlock * 4 > 65536;
     const size_t lds = (size_t)(spill ? kLdsStack : entries) * kTraceBlock * sizeof(int);
 #define PGRT_LAUNCH(C, S)                                                                                   \
-    hipLaunchKernelGGL((k_trace<C, S>), dim3(grid), dim3(kTraceBlock), lds, stream, s, ro, rd, hits, count_dev, \
+    PGRT_TLAUNCH((k_trace<C, S>), dim3(grid), dim3(kTraceBlock), lds, stream, s, ro, rd, hits, count_dev, \
                        count_terms, count_host, max_count, gstack, counters, rpw)
     if (count) {
         if (spill) PGRT_LAUNCH(true, true); else PGRT_LAUNCH(true, false);
@@ -791,6 +806,7 @@ void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4
         if (spill) PGRT_LAUNCH(false, true); else PGRT_LAUNCH(false, false);
     }
 #undef PGRT_LAUNCH
+    return true;
 }
 
 

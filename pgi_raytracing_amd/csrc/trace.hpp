@@ -62,10 +62,13 @@ struct ShadowQueue {  // one per batch: the shadow rays of every level, level-ma
 
 // fetch: a zeroed device int per launch (persistent waves pull 64 rays per atomic).
 // Ray count: sum of count_dev[0 .. count_terms) when count_dev is set, else count_host.
-void launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4* hits, const int* count_dev,
+// returns false when nothing was launched (max_count <= 0)
+bool launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4* hits, const int* count_dev,
                   int count_host, int max_count, int* fetch, int* gstack, int gstack_threads,
                   unsigned long long* counters, bool count, hipStream_t stream, int expect = 0,
                   int count_terms = 1, bool allow_group = true, bool coherent = false);
+// events the next launch_trace records at its kernel's start / end (nullptr: none)
+void set_trace_events(hipEvent_t start, hipEvent_t stop);
 int trace_block_size();
 // any-hit query (rtcOccluded1 semantics): occluded[i] = 1 when some triangle is hit in (tnear, tfar]
 void launch_occluded(const SceneView& s, const float4* ro, const float4* rd, int n, int* occluded,

@@ -7,7 +7,7 @@ set -u
 cd "$(dirname "$0")/.."
 TAG=${1:-r1}
 shift || true
-ARGS=${*:-"--steps 10 --warmup 2 --no-cpu-baseline --no-roofline"}
+ARGS=${*:-"--roofline-only"}
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp

@@ -32,8 +32,8 @@ def main():
     fetch, fn = per_dispatch(os.path.join(root, "pmc_fetch"), "FETCH_SIZE")
     write, wn = per_dispatch(os.path.join(root, "pmc_write"), "WRITE_SIZE")
 
-    def trace_ids(names):
-        return [d for d, n in names.items() if "k_trace" in n]
+    def trace_ids(names):  # the uninstrumented closest-hit launches (COUNT=false variants)
+        return [d for d, n in names.items() if "k_trace" in n and "<true" not in n]
 
     fids, wids = trace_ids(fn), trace_ids(wn)
     f_kb = sum(fetch[d] for d in fids) / max(1, len(fids))
