@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -58,6 +59,8 @@ struct DevBuf {
                                                     " bytes failed: " + hipGetErrorString(e));
         }
         n = count;
+        static const bool log = getenv("PGRT_LOG_ALLOC") != nullptr;  // fault triage: address map
+        if (log) fprintf(stderr, "pgrt alloc %p %zu\n", (void*)p, count * sizeof(T));
     }
     size_t bytes() const { return n * sizeof(T); }
 };

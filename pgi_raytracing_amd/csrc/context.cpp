@@ -23,6 +23,12 @@ namespace {
 constexpr long long kMaxBatchRays = 16ll << 20;  // level-0 rays per sample batch
 constexpr int kTraceGridThreads = 2048 * 256;    // persistent trace grid (global overflow stacks)
 constexpr int kMaxFramesInFlight = 8;
+// sample batches queued on the device across all frames in flight (each batch is ~3 launches per
+// level): a frame is submitted only when the pending frames leave room for its batches (the
+// oldest pending frames complete first).  C4 on one GPU (32 batches per frame) faulted with 6
+// frames = ~3800 launches queued at once and ran clean with 2 (r1d); frames of one or a few
+// batches (C2, C3) are unaffected.
+constexpr int kMaxBatchesInFlight = 64;
 
 struct StageTimer {
     struct Rec {
@@ -215,6 +221,7 @@ struct FrameSet {
     float* out = nullptr;
     int out_mode = 0, ox = 0, oy = 0, pitch = 0;
     int K = 0;             // slots of the pending frame
+    int batches = 0;       // sample batches the pending frame enqueued (all slots)
     bool distributed = false;
     float* dist_fb = nullptr;
     DevBuf<float> tilebuf;  // distributed: this rank's tiles, tile-compact
@@ -630,10 +637,15 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
         const char* e = getenv("PGRT_PACKET_LEVELS");
         return e ? atoi(e) : 0;
     }();
+    static const bool packet_shadow = [] {  // shadow queue as wave packets (A/B knob)
+        const char* e = getenv("PGRT_PACKET_SHADOW");
+        return e ? atoi(e) != 0 : false;
+    }();
     const int K = ntiles == 0 ? 0 : std::max(1, std::min(want_slots, ntiles));
     SceneView view = ctx->view;
     if (!ctx->group_max_env && ctx->frames_in_flight > 1) view.group_max = kDefaultGroupMaxInFlight;
     fs->K = K;
+    fs->batches = 0;
     while ((int)fs->slots.size() < K) fs->slots.emplace_back(new FrameSlot());
     ctx->timer.on = p->profile > 0;
     int trace_launches = 0;
@@ -665,6 +677,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
         PGRT_REQUIRE(npix <= kMaxBatchRays * 8, PGRT_ERR_INVALID_ARGUMENT, "frame too large");
         const int nsb = (int)std::max(1ll, std::min<long long>(spp, kMaxBatchRays / npix));
         const int batches = (spp + nsb - 1) / nsb;
+        fs->batches += batches;
         ensure_frame_buffers(sl, (int)(npix * nsb), levels, view.nlight, batches);
         sl->ensure_pinned(batches, nt);
         if (sl->tiles.n < (size_t)nt) sl->tiles_dev.clear();
@@ -766,7 +779,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 const bool launched = launch_trace(
                     view, sq.ro, sq.rd, sq.hit, &fcd->shadow_count[0], 0, sq.cap, &fcd->fetch[kMaxLevels],
                     sl->gstack.p, kTraceGridThreads, fcd->trav[kMaxLevels], p->profile >= 2, s,
-                    sl->expect_shadow_total, levels, false);  // shadow rays (from the light along H) mostly miss the root
+                    sl->expect_shadow_total, levels, false, packet_shadow);  // shadow rays: no 8-lane groups
                 ctx->timer.end_kernel(s, id, launched);
                 debug_sync(s, "shadow trace", levels, bi);
                 ++trace_launches;
@@ -1364,6 +1377,33 @@ int submit_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device, 
                      "rank 0 needs an output buffer");
         FrameSet* fs = frame_set(ctx, (int)(ctx->next_ticket % (unsigned long long)ctx->frames_in_flight));
         if (fs->pending) finish_through(ctx, fs->ticket);  // the set's previous frame completes first
+        // bound the batches queued across frames in flight (this frame's own count estimated
+        // with one slot per frame, as enqueue_frame deals them when frames are in flight)
+        {
+            long long nt;
+            if (distributed) {
+                nt = (long long)rank_tiles(ctx->cam.width, ctx->cam.height, ctx->rank, ctx->world).size();
+            } else {
+                int x, y, w, h;
+                frame_rect(ctx, p, x, y, w, h);
+                nt = (long long)((w + kTile - 1) / kTile) * ((h + kTile - 1) / kTile);
+            }
+            const long long npix = std::max(1ll, nt) * kTile * kTile;
+            const int spp = p->spp_side * p->spp_side;
+            const int nsb = (int)std::max(1ll, std::min<long long>(spp, kMaxBatchRays / npix));
+            const int mine = (spp + nsb - 1) / nsb;
+            for (;;) {
+                int queued = 0;
+                unsigned long long oldest = 0;
+                for (auto& s : ctx->sets)
+                    if (s->pending) {
+                        queued += s->batches;
+                        if (!oldest || s->ticket < oldest) oldest = s->ticket;
+                    }
+                if (!oldest || queued + mine <= kMaxBatchesInFlight) break;
+                finish_through(ctx, oldest);
+            }
+        }
         if (distributed) {
             start_frame(ctx, fs, p, rank_tiles(ctx->cam.width, ctx->cam.height, ctx->rank, ctx->world), nullptr, 1,
                         0, 0, 0, true, static_cast<float*>(rgba_device));
