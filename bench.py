@@ -8,8 +8,10 @@ the other BASELINE configs for the records in DESIGN.md).  N > 1: one process
 per GPU (torch.distributed launcher env), 64x64 image tiles dealt round-robin to ranks, one
 ncclGather (RCCL over xGMI) to rank 0 and an unpack kernel there -- the total frame is fixed
 (strong scaling).  Rays = every closest-hit query (primary + shadow + reflect + refract).
-Frames run asynchronously with up to --in-flight frames overlapping on the device (throughput =
-ms_per_step); the latency of one synchronous frame is reported beside it (frame_latency_ms).
+Frames are submitted in batches of --frames-per-call consecutive frames (one launch sequence
+covers all of them, pgrt_render_frames_device_async; every frame is fully traced into its own
+framebuffer) with up to --in-flight calls overlapping on the device (throughput = ms_per_step);
+the latency of one synchronous frame is reported beside it (frame_latency_ms).
 """
 from __future__ import annotations
 
@@ -64,6 +66,8 @@ def parse():
                     help="only the profiled roofline frames (the run profiles/ rocprofv3 summaries are taken of)")
     ap.add_argument("--in-flight", type=int, default=None,
                     help="frames in flight (pgrt_set_frames_in_flight); default 6 (r1 scan, tools/inflight_scan.py)")
+    ap.add_argument("--frames-per-call", type=int, default=None,
+                    help="frames per submission (pgrt_render_frames_*_async, 1..16); default 16 (r1e scan)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (multi-thread leg)")
     a = ap.parse_args()
@@ -105,7 +109,8 @@ def main():
     ctx.set_scene(scene)
     ctx.set_camera(cam)
     bvh = ctx.bvh_info()
-    fb = ctx.alloc(args.width * args.height * 16) if rank == 0 or world == 1 else None
+    F = max(1, min(16, args.frames_per_call or 16))
+    fb = ctx.alloc(F * args.width * args.height * 16) if rank == 0 or world == 1 else None
     if world > 1:
         uid = [Context.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -124,9 +129,10 @@ def main():
 
     def run_frames(n):
         pending, rays_n = deque(), 0
-        for _ in range(n):
-            pending.append(ctx.render_distributed_device_async(params, fb) if world > 1
-                           else ctx.render_device_async(params, fb))
+        for f0 in range(0, n, F):
+            nf = min(F, n - f0)
+            pending.append(ctx.render_frames_distributed_device_async(params, nf, fb) if world > 1
+                           else ctx.render_frames_device_async(params, nf, fb))
             if len(pending) >= in_flight:
                 rays_n += ctx.render_wait(pending.popleft()).rays()
         while pending:
@@ -135,6 +141,8 @@ def main():
 
     if args.roofline_only:
         args.warmup = args.steps = 0
+    if not args.roofline_only:  # every frame set is allocated and warm before the timed region
+        args.warmup = max(args.warmup, in_flight * F)
     run_frames(args.warmup)
     ctx.synchronize()
     if dist:
@@ -174,17 +182,22 @@ def main():
     if not args.no_roofline:
         # live per-kernel timing: HIP events on libpgrt's own stream around every closest-hit
         # launch (profile=1), and the instrumented traversal counts (profile=2, separate frame)
+        # (1 GPU: the timed configuration, F frames per launch sequence)
+        def prof_call(p):
+            return ctx.render_frames_device(p, F, fb) if world == 1 else frame(p)
+
+        frames_per_prof = F if world == 1 else 1
         p1 = abi.RenderParams.from_buffer_copy(params)
         p1.profile = 1
         reps = 5
         ms_trace = 0.0
         launches = 0
         for _ in range(reps):
-            s1 = frame(p1)
+            s1 = prof_call(p1)
             ms_trace += s1.ms_trace
             launches += s1.trace_launches
         p1.profile = 2
-        s2 = frame(p1)
+        s2 = prof_call(p1)
         frame_rays = s2.rays()
         alg_bytes = (RAY_BYTES * frame_rays + NODE_BYTES * s2.node_visits + WIDE_NODE_BYTES * s2.wide_node_visits
                      + TRI_BYTES * s2.tri_tests)
@@ -200,8 +213,9 @@ def main():
             "traffic": None,
             "kernel": "closest hit: k_trace (binary BVH, big queues) + k_trace8g (8 lanes/ray, small queues)",
             "avg_launch_ms": round(avg_launch_ms, 4),
-            "launches_per_frame": launches // reps,
-            "trace_ms_per_frame": round(ms_trace / reps, 4),
+            "frames_per_launch": frames_per_prof,
+            "launches_per_call": launches // reps,
+            "trace_ms_per_frame": round(ms_trace / reps / frames_per_prof, 4),
             "node_visits_per_ray": round(s2.node_visits / max(1, frame_rays), 2),
             "wide_node_visits_per_ray": round(s2.wide_node_visits / max(1, frame_rays), 2),
             "tri_tests_per_ray": round(s2.tri_tests / max(1, frame_rays), 2),
@@ -272,6 +286,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "frames_in_flight": in_flight,
+            "frames_per_call": F,
             "frame_latency_ms": round(latency_ms, 4),
             "higher_is_better": True,
             "scaling": "strong",

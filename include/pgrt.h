@@ -202,6 +202,17 @@ int pgrt_set_frames_in_flight(pgrt_ctx* ctx, int n);
 int pgrt_render_device_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device,
                              unsigned long long* ticket);
 int pgrt_render_wait(pgrt_ctx* ctx, unsigned long long ticket, pgrt_stats* st);
+/* Batched frames: one call renders nframes (1..16) consecutive frames of the same camera and
+ * params, frame f with jitter frame index p->frame + f, into rgba_device + f * (frame floats)
+ * (W*H*4 floats per frame, or the rect's w*h*4).  Every launch covers all nframes frames, so
+ * small frames fill the GPU and pay the per-launch latency once per call instead of once per
+ * frame.  Each frame is bit-identical to pgrt_render_device with params.frame = p->frame + f.
+ * One ticket completes all nframes frames; its statistics are the sums over them. */
+int pgrt_render_frames_device_async(pgrt_ctx* ctx, const pgrt_render_params* p, int nframes,
+                                    void* rgba_device, unsigned long long* ticket);
+/* Synchronous form of the batched frames (profile allowed: stage timings cover all nframes). */
+int pgrt_render_frames_device(pgrt_ctx* ctx, const pgrt_render_params* p, int nframes,
+                              void* rgba_device, pgrt_stats* st);
 
 /* ---- batched closest-hit query with rtcIntersect1 semantics ----
  * rays: n x 8 floats {org.xyz, tnear, dir.xyz, tfar}; hits: n x 4 {t, u, v, prim} where prim
@@ -242,6 +253,12 @@ int pgrt_render_distributed_device(pgrt_ctx* ctx, const pgrt_render_params* p,
  * still in flight.  Every rank must submit and wait in the same order. */
 int pgrt_render_distributed_device_async(pgrt_ctx* ctx, const pgrt_render_params* p,
                                          void* rgba_device, unsigned long long* ticket);
+/* Batched distributed frames (see pgrt_render_frames_device_async): each rank renders its tiles
+ * of nframes frames in one pass, one ncclGather moves all of them, rank 0 unpacks frame f into
+ * rgba_device + f * W*H*4 floats. */
+int pgrt_render_frames_distributed_device_async(pgrt_ctx* ctx, const pgrt_render_params* p,
+                                                int nframes, void* rgba_device,
+                                                unsigned long long* ticket);
 
 /* ---- scene ingest (LoadOBJ / LoadMTL, objloader.cpp:53-507; host only) ----
  * Texture files named by map_Kd are NOT decoded here: their paths are reported so the caller

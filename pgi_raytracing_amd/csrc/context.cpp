@@ -29,6 +29,7 @@ constexpr int kMaxFramesInFlight = 8;
 // frames = ~3800 launches queued at once and ran clean with 2 (r1d); frames of one or a few
 // batches (C2, C3) are unaffected.
 constexpr int kMaxBatchesInFlight = 64;
+constexpr int kMaxFramesPerCall = 16;
 
 struct StageTimer {
     struct Rec {
@@ -222,6 +223,10 @@ struct FrameSet {
     int out_mode = 0, ox = 0, oy = 0, pitch = 0;
     int K = 0;             // slots of the pending frame
     int batches = 0;       // sample batches the pending frame enqueued (all slots)
+    int nframes = 1;       // consecutive frames rendered by this call (tiles repeated per frame)
+    int frame_tiles = 0;   // tiles of one frame in `tiles` (nframes > 1)
+    int frame_out_tiles = 0;  // tiles per frame in the tile-compact output (>= frame_tiles)
+    long long frame_stride = 0;  // floats between frames of a framebuffer output
     bool distributed = false;
     float* dist_fb = nullptr;
     DevBuf<float> tilebuf;  // distributed: this rank's tiles, tile-compact
@@ -276,6 +281,11 @@ struct pgrt_ctx {
     // multi-GPU
     ncclComm_t comm = nullptr;
     int world = 1, rank = 0;
+    // PGRT_EMULATE_RANK=r/N (measurement tool only, no communicator): distributed frames render
+    // rank r's share of an N-GPU frame on this device; the gather becomes a device copy of this
+    // rank's tiles into a full-size gather buffer (+ the unpack on rank 0), so one GPU measures a
+    // rank's compute and rank 0's unpack at N GPUs without the xGMI transfer
+    bool emulated = false;
     DevBuf<float> tilebuf, gathered, fb_dev;
 
     // frame sink (progressive accumulation)
@@ -650,6 +660,10 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
     ctx->timer.on = p->profile > 0;
     int trace_launches = 0;
     FrameParams fp0{};
+    fp0.slots = K;
+    fp0.frame_tiles = fs->nframes > 1 ? fs->frame_tiles : 0;
+    fp0.frame_out_tiles = fs->frame_out_tiles;
+    fp0.frame_stride = fs->frame_stride;
     fp0.spp_side = p->spp_side;
     fp0.max_level = p->max_level;
     fp0.dof = p->dof;
@@ -704,6 +718,9 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             g.add(fs->ox);
             g.add(fs->oy);
             g.add(fs->pitch);
+            g.add(fs->nframes);
+            g.add(fs->frame_out_tiles);
+            g.add(fs->frame_stride);
             sl->add_buffers(g);
             if (sl->gexec && g.v == sl->gsig) {
                 replay = true;
@@ -734,6 +751,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
         }
         FrameParams fp = fp0;
         fp.ntiles = nt;
+        fp.slot = j;
         bool staggered = false;
         for (int bi = 0; bi < batches; ++bi) {
             const int s0 = bi * nsb;
@@ -933,18 +951,31 @@ void gather_frame(pgrt_ctx* ctx, FrameSet* fs) {
     const int W = fs->cam_w, H = fs->cam_h;
     const int total = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
     const int per_rank = (total + ctx->world - 1) / ctx->world;
+    const int F = fs->nframes;
     const size_t tile_floats = (size_t)kTile * kTile * 3;  // RGB tiles (out_mode 2)
-    if (ctx->world == 1 && !ctx->comm) {
-        launch_unpack_tiles(fs->tilebuf.p, fs->dist_fb, W, H, 1, per_rank, 3, ctx->stream);
+    const size_t block = (size_t)F * per_rank * tile_floats;  // one rank's frames, frame-major
+    const size_t frame_px = (size_t)W * H * 4;
+    const float* src = nullptr;
+    if (ctx->emulated) {
+        ctx->gathered.alloc(block * ctx->world);
+        PGRT_HIP(hipMemcpyAsync(ctx->gathered.p + (size_t)ctx->rank * block, fs->tilebuf.p, sizeof(float) * block,
+                                hipMemcpyDeviceToDevice, ctx->stream));
+        src = ctx->rank == 0 ? ctx->gathered.p : nullptr;
+    } else if (ctx->world == 1 && !ctx->comm) {
+        src = fs->tilebuf.p;
     } else {
         PGRT_REQUIRE(ctx->comm, PGRT_ERR_RCCL, "pgrt_comm_init has not been called");
-        if (ctx->rank == 0) ctx->gathered.alloc((size_t)per_rank * tile_floats * ctx->world);
-        ncclResult_t r = ncclGather(fs->tilebuf.p, ctx->rank == 0 ? ctx->gathered.p : nullptr,
-                                    (size_t)per_rank * tile_floats, ncclFloat, 0, ctx->comm, ctx->stream);
+        if (ctx->rank == 0) ctx->gathered.alloc(block * ctx->world);
+        // one collective for all of the call's frames
+        ncclResult_t r = ncclGather(fs->tilebuf.p, ctx->rank == 0 ? ctx->gathered.p : nullptr, block, ncclFloat, 0,
+                                    ctx->comm, ctx->stream);
         if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string("ncclGather: ") + ncclGetErrorString(r));
-        if (ctx->rank == 0)
-            launch_unpack_tiles(ctx->gathered.p, fs->dist_fb, W, H, ctx->world, per_rank, 3, ctx->stream);
+        src = ctx->rank == 0 ? ctx->gathered.p : nullptr;
     }
+    if (src)
+        for (int f = 0; f < F; ++f)
+            launch_unpack_tiles(src, fs->dist_fb + (size_t)f * frame_px, W, H, ctx->world, per_rank, 3, ctx->stream, F,
+                                f);
     PGRT_HIP(hipGetLastError());
 }
 
@@ -983,11 +1014,19 @@ void check_frame(const pgrt_ctx* ctx, const pgrt_render_params* p) {
 // Start a frame on set fs (its previous frame must be finished).  distributed: out is ignored,
 // the tiles land in fs->tilebuf and finish_frame gathers them into fb (rank 0).
 void start_frame(pgrt_ctx* ctx, FrameSet* fs, const pgrt_render_params* p, std::vector<int4> tiles, float* out,
-                 int out_mode, int ox, int oy, int pitch, bool distributed, float* fb) {
+                 int out_mode, int ox, int oy, int pitch, bool distributed, float* fb, int nframes = 1,
+                 long long frame_stride = 0) {
     check_frame(ctx, p);
+    PGRT_REQUIRE(nframes >= 1 && nframes <= kMaxFramesPerCall, PGRT_ERR_INVALID_ARGUMENT,
+                 "frames per call must be in [1, 16]");
     fs->t0 = std::chrono::steady_clock::now();
     fs->params = *p;
-    fs->tiles = std::move(tiles);
+    fs->nframes = nframes;
+    fs->frame_tiles = (int)tiles.size();
+    fs->frame_out_tiles = (int)tiles.size();
+    fs->frame_stride = frame_stride;
+    fs->tiles.clear();
+    for (int f = 0; f < nframes; ++f) fs->tiles.insert(fs->tiles.end(), tiles.begin(), tiles.end());
     fs->distributed = distributed;
     fs->dist_fb = fb;
     fs->cam_w = ctx->cam.width;
@@ -996,8 +1035,9 @@ void start_frame(pgrt_ctx* ctx, FrameSet* fs, const pgrt_render_params* p, std::
         const int W = fs->cam_w, H = fs->cam_h;
         const int total = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
         const int per_rank = (total + ctx->world - 1) / ctx->world;
-        // padded slots of the tile-compact buffer are never unpacked (t >= total)
-        fs->tilebuf.alloc((size_t)per_rank * kTile * kTile * 3);
+        // padded slots of the tile-compact buffer are never unpacked (t >= total); frame-major
+        fs->tilebuf.alloc((size_t)nframes * per_rank * kTile * kTile * 3);
+        fs->frame_out_tiles = per_rank;
         out = fs->tilebuf.p;
         out_mode = 2;
         ox = oy = pitch = 0;
@@ -1015,11 +1055,12 @@ void start_frame(pgrt_ctx* ctx, FrameSet* fs, const pgrt_render_params* p, std::
 
 // Synchronous render of `tiles` (pending asynchronous frames complete first).
 void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<int4>& tiles, float* out,
-                  int out_mode, int ox, int oy, int pitch, pgrt_stats* st) {
+                  int out_mode, int ox, int oy, int pitch, pgrt_stats* st, int nframes = 1,
+                  long long frame_stride = 0) {
     drain_frames(ctx);
     FrameSet* fs = frame_set(ctx, 0);
     PGRT_HIP(hipEventRecord(fs->ev_ready, ctx->stream));  // prior context-stream work first
-    start_frame(ctx, fs, p, tiles, out, out_mode, ox, oy, pitch, false, nullptr);
+    start_frame(ctx, fs, p, tiles, out, out_mode, ox, oy, pitch, false, nullptr, nframes, frame_stride);
     finish_frame(ctx, fs);
     if (st) *st = fs->stats;
 }
@@ -1079,6 +1120,14 @@ int pgrt_create(int hip_device, pgrt_ctx** out) {
     pgrt_ctx* ctx = new (std::nothrow) pgrt_ctx();
     if (!ctx) return PGRT_ERR_OUT_OF_MEMORY;
     ctx->device = hip_device;
+    if (const char* e = getenv("PGRT_EMULATE_RANK")) {
+        int r = 0, w = 1;
+        if (sscanf(e, "%d/%d", &r, &w) == 2 && w >= 1 && r >= 0 && r < w) {
+            ctx->world = w;
+            ctx->rank = r;
+            ctx->emulated = w > 1;
+        }
+    }
     int rc = guarded(ctx, [&] { PGRT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)); });
     if (rc != PGRT_OK) {
         delete ctx;
@@ -1132,6 +1181,20 @@ int pgrt_render_device(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_de
         int x, y, w, h;
         frame_rect(ctx, p, x, y, w, h);
         render_tiles(ctx, p, rect_tiles(x, y, w, h), static_cast<float*>(rgba_device), 0, x, y, w, st);
+        if (st) st->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    });
+}
+
+int pgrt_render_frames_device(pgrt_ctx* ctx, const pgrt_render_params* p, int nframes, void* rgba_device,
+                              pgrt_stats* st) {
+    if (!ctx || !p || !rgba_device) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        PGRT_REQUIRE(ctx->has_cam, PGRT_ERR_NO_CAMERA, "pgrt_set_camera has not been called");
+        auto t0 = std::chrono::steady_clock::now();
+        int x, y, w, h;
+        frame_rect(ctx, p, x, y, w, h);
+        render_tiles(ctx, p, rect_tiles(x, y, w, h), static_cast<float*>(rgba_device), 0, x, y, w, st, nframes,
+                     (long long)w * h * 4);
         if (st) st->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     });
 }
@@ -1325,6 +1388,7 @@ int pgrt_comm_init(pgrt_ctx* ctx, int world, int rank, const char id[128]) {
         }
         ctx->world = world;
         ctx->rank = rank;
+        ctx->emulated = false;
         ncclUniqueId u;
         std::memcpy(u.internal, id, 128);
         ncclResult_t r = ncclCommInitRank(&ctx->comm, world, u, rank);
@@ -1368,8 +1432,9 @@ int pgrt_set_frames_in_flight(pgrt_ctx* ctx, int n) {
 
 namespace {
 int submit_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device, unsigned long long* ticket,
-                 bool distributed) {
+                 bool distributed, int nframes = 1) {
     if (!ctx || !p || !ticket || (!distributed && !rgba_device)) return PGRT_ERR_INVALID_ARGUMENT;
+    if (nframes < 1 || nframes > kMaxFramesPerCall) return PGRT_ERR_INVALID_ARGUMENT;
     return guarded(ctx, [&] {
         PGRT_REQUIRE(ctx->has_cam, PGRT_ERR_NO_CAMERA, "pgrt_set_camera has not been called");
         PGRT_REQUIRE(p->profile == 0, PGRT_ERR_INVALID_ARGUMENT, "profiled frames are synchronous (profile must be 0)");
@@ -1388,7 +1453,7 @@ int submit_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device, 
                 frame_rect(ctx, p, x, y, w, h);
                 nt = (long long)((w + kTile - 1) / kTile) * ((h + kTile - 1) / kTile);
             }
-            const long long npix = std::max(1ll, nt) * kTile * kTile;
+            const long long npix = std::max(1ll, nt * nframes) * kTile * kTile;
             const int spp = p->spp_side * p->spp_side;
             const int nsb = (int)std::max(1ll, std::min<long long>(spp, kMaxBatchRays / npix));
             const int mine = (spp + nsb - 1) / nsb;
@@ -1406,17 +1471,27 @@ int submit_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device, 
         }
         if (distributed) {
             start_frame(ctx, fs, p, rank_tiles(ctx->cam.width, ctx->cam.height, ctx->rank, ctx->world), nullptr, 1,
-                        0, 0, 0, true, static_cast<float*>(rgba_device));
+                        0, 0, 0, true, static_cast<float*>(rgba_device), nframes);
         } else {
             int x, y, w, h;
             frame_rect(ctx, p, x, y, w, h);
             start_frame(ctx, fs, p, rect_tiles(x, y, w, h), static_cast<float*>(rgba_device), 0, x, y, w, false,
-                        nullptr);
+                        nullptr, nframes, (long long)w * h * 4);
         }
         *ticket = fs->ticket;
     });
 }
 }  // namespace
+
+int pgrt_render_frames_device_async(pgrt_ctx* ctx, const pgrt_render_params* p, int nframes, void* rgba_device,
+                                    unsigned long long* ticket) {
+    return submit_async(ctx, p, rgba_device, ticket, false, nframes);
+}
+
+int pgrt_render_frames_distributed_device_async(pgrt_ctx* ctx, const pgrt_render_params* p, int nframes,
+                                                void* rgba_device, unsigned long long* ticket) {
+    return submit_async(ctx, p, rgba_device, ticket, true, nframes);
+}
 
 int pgrt_render_device_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device,
                              unsigned long long* ticket) {

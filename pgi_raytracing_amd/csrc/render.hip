@@ -64,6 +64,7 @@ __global__ __launch_bounds__(kBlock) void k_raygen(CameraView cam, FrameParams f
     int px, py;
     bool valid;
     tile_pixel(slot_pix, tiles, px, py, valid);
+    const uint32_t frame = fp.frame + (uint32_t)frame_of_tile(fp, slot_pix / (kTile * kTile));
     if (!valid) {
         q.ro[i] = make_float4(0, 0, 0, 0);
         q.rd[i] = make_float4(0, 0, 0, -1.0f);  // padding slot: tfar < 0, never hits
@@ -78,11 +79,11 @@ __global__ __launch_bounds__(kBlock) void k_raygen(CameraView cam, FrameParams f
         const float Sf = (float)S;
         const float ja = -0.5f / Sf, jb = 0.5f / Sf;
         const float la = -fp.aperture / 2.0f, lb = fp.aperture / 2.0f;
-        const float u0 = pg_jitter_u01(fp.seed, fp.frame, pixel, (uint32_t)s, 0);
-        const float u1 = pg_jitter_u01(fp.seed, fp.frame, pixel, (uint32_t)s, 1);
+        const float u0 = pg_jitter_u01(fp.seed, frame, pixel, (uint32_t)s, 0);
+        const float u1 = pg_jitter_u01(fp.seed, frame, pixel, (uint32_t)s, 1);
         const bool corr = fp.jitter == PGRT_JITTER_HASH_CORRELATED;
-        const float u2 = corr ? u0 : pg_jitter_u01(fp.seed, fp.frame, pixel, (uint32_t)s, 2);
-        const float u3 = corr ? u1 : pg_jitter_u01(fp.seed, fp.frame, pixel, (uint32_t)s, 3);
+        const float u2 = corr ? u0 : pg_jitter_u01(fp.seed, frame, pixel, (uint32_t)s, 2);
+        const float u3 = corr ? u1 : pg_jitter_u01(fp.seed, frame, pixel, (uint32_t)s, 3);
         j0 = u0 * (jb - ja) + ja;
         j1 = u1 * (jb - ja) + ja;
         j2 = u2 * (lb - la) + la;
@@ -435,13 +436,18 @@ __global__ __launch_bounds__(kBlock) void k_finish(SceneView s, FrameParams fp, 
     // gamma(Color4f{final.b/area, final.g/area, final.r/area}) (raytracer.cpp:431-435)
     const float4 o = gamma_rgba(acc.z / (float)area, acc.y / (float)area, acc.x / (float)area, fp.gamma);
     if (out_mode == 0) {
-        float* dst = out + ((size_t)(py - oy) * (size_t)pitch + (size_t)(px - ox)) * 4;
+        float* dst = out + (size_t)frame_of_tile(fp, p / (kTile * kTile)) * fp.frame_stride +
+                     ((size_t)(py - oy) * (size_t)pitch + (size_t)(px - ox)) * 4;
         *reinterpret_cast<float4*>(dst) = o;
         return;
     }
     const int tile = p / (kTile * kTile);
     const int4 tr = tiles[tile];
-    const size_t gtile = (size_t)tile * K + j;  // position in the caller's tile list
+    size_t gtile = (size_t)tile * K + j;  // position in the caller's tile list
+    if (fp.frame_tiles > 0) {  // multi-frame call: frame f's tiles start at f * frame_out_tiles
+        const size_t f = gtile / fp.frame_tiles;
+        gtile += f * (size_t)(fp.frame_out_tiles - fp.frame_tiles);
+    }
     const size_t q = gtile * kTile * kTile + (size_t)(py - tr.y) * kTile + (size_t)(px - tr.x);
     if (out_mode == 1) {
         *reinterpret_cast<float4*>(out + q * 4) = o;
@@ -462,8 +468,11 @@ void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles,
 
 // ------------------------------------------------------------------ multi-GPU unpack
 
+// g holds, per rank, `frames` frames of tiles_per_rank tiles each (frame-major); frame `frame` of
+// every rank is unpacked into rgba
 __global__ __launch_bounds__(kBlock) void k_unpack(const float* __restrict__ g, float4* __restrict__ rgba, int width,
-                                                   int height, int world, int tiles_per_rank, int channels) {
+                                                   int height, int world, int tiles_per_rank, int channels,
+                                                   int frames, int frame) {
     const long long idx = (long long)blockIdx.x * kBlock + threadIdx.x;
     const long long per_rank = (long long)tiles_per_rank * kTile * kTile;
     if (idx >= per_rank * world) return;
@@ -478,16 +487,17 @@ __global__ __launch_bounds__(kBlock) void k_unpack(const float* __restrict__ g, 
     const int x = (t % tiles_x) * kTile + (p % kTile);
     const int y = (t / tiles_x) * kTile + (p / kTile);
     if (x >= width || y >= height) return;
-    rgba[(size_t)y * width + x] = channels == 4 ? reinterpret_cast<const float4*>(g)[idx]
-                                                 : make_float4(g[idx * 3], g[idx * 3 + 1], g[idx * 3 + 2], 1.0f);
+    const long long src = ((long long)rank * frames + frame) * per_rank + r;
+    rgba[(size_t)y * width + x] = channels == 4 ? reinterpret_cast<const float4*>(g)[src]
+                                                 : make_float4(g[src * 3], g[src * 3 + 1], g[src * 3 + 2], 1.0f);
 }
 
 void launch_unpack_tiles(const float* gathered, float* rgba, int width, int height, int world, int tiles_per_rank,
-                         int channels, hipStream_t stream) {
+                         int channels, hipStream_t stream, int frames, int frame) {
     const long long total = (long long)world * tiles_per_rank * kTile * kTile;
     if (total <= 0) return;
     hipLaunchKernelGGL(k_unpack, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, gathered,
-                       reinterpret_cast<float4*>(rgba), width, height, world, tiles_per_rank, channels);
+                       reinterpret_cast<float4*>(rgba), width, height, world, tiles_per_rank, channels, frames, frame);
 }
 
 // ------------------------------------------------------------------ progressive accumulation

@@ -35,7 +35,17 @@ struct FrameParams {
     unsigned seed, frame;
     int s0, nsb;   // first sample and samples in this batch
     int ntiles;
+    // multi-frame calls: the caller's tile list is nframes copies of one frame's tiles
+    // (frame-major); a slot's tile q is the caller's tile q * slots + slot, its frame that index
+    // / frame_tiles (frame_tiles 0: one frame).  Frame f jitters with frame index frame + f and
+    // writes a framebuffer at out + f * frame_stride floats (tile-compact outputs are frame-major).
+    int slots, slot, frame_tiles, frame_out_tiles;  // frame_out_tiles: tiles per frame in a tile-compact output
+    long long frame_stride;
 };
+
+__host__ __device__ inline int frame_of_tile(const FrameParams& fp, int tile) {
+    return fp.frame_tiles > 0 ? (tile * fp.slots + fp.slot) / fp.frame_tiles : 0;
+}
 
 // level-L queue view
 struct Queue {
@@ -99,7 +109,7 @@ void launch_accumulate_frame(const float* frame, float* sum, float* mean, long l
 void launch_export_counters(FrameCounters* dev, FrameCounters* host, int n, hipStream_t stream);
 // gathered: rank-major tile-compact buffers, `channels` floats per pixel (4: RGBA, 3: RGB + alpha 1)
 void launch_unpack_tiles(const float* gathered, float* rgba, int width, int height, int world, int tiles_per_rank,
-                         int channels, hipStream_t stream);
+                         int channels, hipStream_t stream, int frames = 1, int frame = 0);
 
 // scene / BVH build
 constexpr int kBuilderLbvh = 0;  // Karras 2012 over 63-bit Morton codes

@@ -62,6 +62,11 @@ def lib():
         "pgrt_render_distributed_device_async": (ip, [vp, C.POINTER(abi.RenderParams), vp,
                                                       C.POINTER(C.c_ulonglong)]),
         "pgrt_render_wait": (ip, [vp, C.c_ulonglong, C.POINTER(abi.Stats)]),
+        "pgrt_render_frames_device_async": (ip, [vp, C.POINTER(abi.RenderParams), ip, vp,
+                                                 C.POINTER(C.c_ulonglong)]),
+        "pgrt_render_frames_device": (ip, [vp, C.POINTER(abi.RenderParams), ip, vp, C.POINTER(abi.Stats)]),
+        "pgrt_render_frames_distributed_device_async": (ip, [vp, C.POINTER(abi.RenderParams), ip, vp,
+                                                             C.POINTER(C.c_ulonglong)]),
         "pgrt_tile_count": (ip, [ip, ip, ip, ip, ip]),
         "pgrt_tile_rect": (ip, [ip, ip, ip, ip, C.POINTER(C.c_int)]),
         "pgrt_unpack_tiles_host": (ip, [ip, ip, ip, ip, fp, fp]),
@@ -225,6 +230,26 @@ class Context:
         t = C.c_ulonglong()
         _check(self.h, self.L.pgrt_render_distributed_device_async(self.h, C.byref(params), C.c_void_p(dev_ptr or 0),
                                                                    C.byref(t)))
+        return t.value
+
+    def render_frames_device_async(self, params, nframes: int, dev_ptr: int) -> int:
+        """Enqueue nframes consecutive frames in one pass (pgrt_render_frames_device_async)."""
+        t = C.c_ulonglong()
+        _check(self.h, self.L.pgrt_render_frames_device_async(self.h, C.byref(params), nframes, C.c_void_p(dev_ptr),
+                                                              C.byref(t)))
+        return t.value
+
+    def render_frames_device(self, params, nframes: int, dev_ptr: int):
+        """nframes consecutive frames in one synchronous pass (pgrt_render_frames_device)."""
+        st = abi.Stats()
+        _check(self.h, self.L.pgrt_render_frames_device(self.h, C.byref(params), nframes, C.c_void_p(dev_ptr),
+                                                        C.byref(st)))
+        return st
+
+    def render_frames_distributed_device_async(self, params, nframes: int, dev_ptr: int | None) -> int:
+        t = C.c_ulonglong()
+        _check(self.h, self.L.pgrt_render_frames_distributed_device_async(self.h, C.byref(params), nframes,
+                                                                          C.c_void_p(dev_ptr or 0), C.byref(t)))
         return t.value
 
     def render_wait(self, ticket: int):

@@ -261,6 +261,55 @@ def test_progressive_accumulation_is_mean_of_frames(gpu_ctx, avenger_scene):
     assert n1 == 1 and ((m1 == frames[0]) | (np.isnan(m1) & np.isnan(frames[0]))).all()
 
 
+def test_batched_frames_match_single(gpu_ctx, avenger_scene):
+    """pgrt_render_frames_device_async: nframes frames in one pass (ragged 200x120 frame, so
+    padded edge tiles repeat per frame) are bit-identical to single renders with frame index
+    base + f; the distributed form (world 1) unpacks every frame; nframes outside [1, 16] is
+    refused."""
+    from pgi_raytracing_amd.raytracer import PgrtError
+
+    gpu_ctx.set_scene(avenger_scene)
+    W, H = 200, 120
+    gpu_ctx.set_camera(abi.default_camera(W, H))
+    for spp_side, dof, F, rect in ((1, 0, 3, (0, 0, 0, 0)), (2, 1, 5, (0, 0, 0, 0)), (1, 1, 2, (30, 20, 100, 70))):
+        def params(frame):
+            return abi.make_params(max_level=5, spp_side=spp_side, dof=dof, jitter=abi.PGRT_JITTER_HASH,
+                                   frame=frame, rect=rect)
+
+        p = params(11)
+        w, h = (rect[2], rect[3]) if rect[2] else (W, H)
+        frame_bytes = w * h * 16
+        refs = [gpu_ctx.render(params(11 + f)) for f in range(F)]
+        buf = gpu_ctx.alloc(F * frame_bytes)
+        dbuf = gpu_ctx.alloc(F * frame_bytes)
+        try:
+            gpu_ctx.set_frames_in_flight(2)
+            t0 = gpu_ctx.render_frames_device_async(p, F, buf)
+            st0 = gpu_ctx.render_wait(t0)
+            assert st0.rays() == sum(st.rays() for _, st in refs)
+            out = gpu_ctx.to_host(buf, (F, h, w, 4))
+            checks = [("frames", out)]
+            st1 = gpu_ctx.render_frames_device(params(11), F, dbuf)  # synchronous form
+            assert st1.rays() == st0.rays()
+            checks.append(("synchronous frames", gpu_ctx.to_host(dbuf, (F, h, w, 4))))
+            if not rect[2]:  # the distributed form renders the whole camera image
+                gpu_ctx.render_wait(gpu_ctx.render_frames_distributed_device_async(p, F, dbuf))
+                checks.append(("distributed frames", gpu_ctx.to_host(dbuf, (F, H, W, 4))))
+            for f, (ref, _) in enumerate(refs):
+                for name, o in ((n, a[f]) for n, a in checks):
+                    same = (o == ref) | (np.isnan(o) & np.isnan(ref))
+                    assert same.all(), f"{name} S={spp_side} frame {f}: {(~same).sum()} pixels differ"
+            if F > 1:
+                assert not np.array_equal(out[0], out[1])  # the frames really differ (jitter)
+            for bad in (0, 17):
+                with pytest.raises(PgrtError):
+                    gpu_ctx.render_frames_device_async(p, bad, buf)
+        finally:
+            gpu_ctx.set_frames_in_flight(1)
+            gpu_ctx.free(buf)
+            gpu_ctx.free(dbuf)
+
+
 def test_frames_in_flight_match_synchronous(gpu_ctx, avenger_scene):
     """Asynchronous frames (3 in flight, different depth / spp / DoF / seed per frame, the
     distributed form included) are bit-identical to synchronous renders; a recycled ticket is
