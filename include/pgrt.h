@@ -202,7 +202,7 @@ int pgrt_set_frames_in_flight(pgrt_ctx* ctx, int n);
 int pgrt_render_device_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device,
                              unsigned long long* ticket);
 int pgrt_render_wait(pgrt_ctx* ctx, unsigned long long ticket, pgrt_stats* st);
-/* Batched frames: one call renders nframes (1..16) consecutive frames of the same camera and
+/* Batched frames: one call renders nframes (1..64) consecutive frames of the same camera and
  * params, frame f with jitter frame index p->frame + f, into rgba_device + f * (frame floats)
  * (W*H*4 floats per frame, or the rect's w*h*4).  Every launch covers all nframes frames, so
  * small frames fill the GPU and pay the per-launch latency once per call instead of once per

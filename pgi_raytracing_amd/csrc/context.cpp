@@ -29,7 +29,7 @@ constexpr int kMaxFramesInFlight = 8;
 // frames = ~3800 launches queued at once and ran clean with 2 (r1d); frames of one or a few
 // batches (C2, C3) are unaffected.
 constexpr int kMaxBatchesInFlight = 64;
-constexpr int kMaxFramesPerCall = 16;
+constexpr int kMaxFramesPerCall = 64;
 
 struct StageTimer {
     struct Rec {
@@ -1018,7 +1018,7 @@ void start_frame(pgrt_ctx* ctx, FrameSet* fs, const pgrt_render_params* p, std::
                  long long frame_stride = 0) {
     check_frame(ctx, p);
     PGRT_REQUIRE(nframes >= 1 && nframes <= kMaxFramesPerCall, PGRT_ERR_INVALID_ARGUMENT,
-                 "frames per call must be in [1, 16]");
+                 "frames per call must be in [1, 64]");
     fs->t0 = std::chrono::steady_clock::now();
     fs->params = *p;
     fs->nframes = nframes;

@@ -175,6 +175,21 @@ def test_distributed_world1_equals_render(gpu_ctx, avenger_scene):
     a, _ = gpu_ctx.render(p)
     b, _ = gpu_ctx.render_distributed(p)
     assert (np.nan_to_num(a, nan=5) == np.nan_to_num(b, nan=5)).all()
+    # batched frames through the RCCL gather: one ncclGather for all frames of the call
+    F = 3
+    refs = [gpu_ctx.render(abi.make_params(max_level=5, spp_side=2, jitter=abi.PGRT_JITTER_HASH, frame=4 + f))[0]
+            for f in range(F)]
+    buf = gpu_ctx.alloc(F * 150 * 100 * 16)
+    try:
+        gpu_ctx.set_frames_in_flight(2)
+        q = abi.make_params(max_level=5, spp_side=2, jitter=abi.PGRT_JITTER_HASH, frame=4)
+        gpu_ctx.render_wait(gpu_ctx.render_frames_distributed_device_async(q, F, buf))
+        out = gpu_ctx.to_host(buf, (F, 100, 150, 4))
+        for f in range(F):
+            assert (np.nan_to_num(out[f], nan=5) == np.nan_to_num(refs[f], nan=5)).all(), f"frame {f}"
+    finally:
+        gpu_ctx.set_frames_in_flight(1)
+        gpu_ctx.free(buf)
 
 
 @pytest.mark.parametrize("builder,width,split,group", [
@@ -264,7 +279,7 @@ def test_progressive_accumulation_is_mean_of_frames(gpu_ctx, avenger_scene):
 def test_batched_frames_match_single(gpu_ctx, avenger_scene):
     """pgrt_render_frames_device_async: nframes frames in one pass (ragged 200x120 frame, so
     padded edge tiles repeat per frame) are bit-identical to single renders with frame index
-    base + f; the distributed form (world 1) unpacks every frame; nframes outside [1, 16] is
+    base + f; the distributed form (world 1) unpacks every frame; nframes outside [1, 64] is
     refused."""
     from pgi_raytracing_amd.raytracer import PgrtError
 
@@ -301,7 +316,7 @@ def test_batched_frames_match_single(gpu_ctx, avenger_scene):
                     assert same.all(), f"{name} S={spp_side} frame {f}: {(~same).sum()} pixels differ"
             if F > 1:
                 assert not np.array_equal(out[0], out[1])  # the frames really differ (jitter)
-            for bad in (0, 17):
+            for bad in (0, 65):
                 with pytest.raises(PgrtError):
                     gpu_ctx.render_frames_device_async(p, bad, buf)
         finally:
