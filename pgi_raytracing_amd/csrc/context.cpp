@@ -570,10 +570,10 @@ void grow_after_overflow(FrameSlot* sl, int levels) {
     int shadow_need = 0;
     for (auto& h : sl->host_fc) {
         int sc = 0;
-        for (int L = 0; L < kMaxLevels; ++L) sc += h.shadow_count[L];
+        for (int L = 0; L < kMaxLevels; ++L) sc += fc_shadow(h, L);
         shadow_need = std::max(shadow_need, sc);
         for (int L = 1; L < levels; ++L) {
-            const int need = h.count[L] * 2;
+            const int need = fc_count(h, L) * 2;
             if (need > sl->level_cap[L]) sl->level_cap[L] = need;
             if (need > sl->q_cap) {
                 for (int b = 0; b < 2; ++b) {
@@ -777,7 +777,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 const int ex = L == 0 ? n0 : sl->expect_count[L];
                 id = ctx->timer.begin_kernel(CAT_TRACE, CAT_LTRACE + L);
                 const bool launched =
-                    launch_trace(view, qc.ro, qc.rd, qc.hit, &fcd->count[L], 0, maxc, &fcd->fetch[L], sl->gstack.p,
+                    launch_trace(view, qc.ro, qc.rd, qc.hit, fc_count_ptr(fcd, L), 0, maxc, &fcd->fetch[L], sl->gstack.p,
                                  kTraceGridThreads, fcd->trav[L], p->profile >= 2, s, ex, 1, true,
                                  L <= packet_levels);  // coherent 8x8-pixel waves -> packet traversal
                 ctx->timer.end_kernel(s, id, launched);
@@ -795,7 +795,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             if (view.nlight > 0 && p->max_level > 0) {  // every level's shadow rays, one launch
                 id = ctx->timer.begin_kernel(CAT_TRACE, CAT_SHADOW);
                 const bool launched = launch_trace(
-                    view, sq.ro, sq.rd, sq.hit, &fcd->shadow_count[0], 0, sq.cap, &fcd->fetch[kMaxLevels],
+                    view, sq.ro, sq.rd, sq.hit, fc_shadow_counts(fcd), 0, sq.cap, &fcd->fetch[kMaxLevels],
                     sl->gstack.p, kTraceGridThreads, fcd->trav[kMaxLevels], p->profile >= 2, s,
                     sl->expect_shadow_total, levels, false, packet_shadow);  // shadow rays: no 8-lane groups
                 ctx->timer.end_kernel(s, id, launched);
@@ -877,7 +877,7 @@ void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
             int shadow_need = 0;
             for (auto& h : sl->host_fc) {
                 int sc = 0;
-                for (int L = 0; L < kMaxLevels; ++L) sc += h.shadow_count[L];
+                for (int L = 0; L < kMaxLevels; ++L) sc += fc_shadow(h, L);
                 shadow_need = std::max(shadow_need, sc);
             }
             // grid hints for the next frame: kept while the count stays within [hint/2, hint]
@@ -887,7 +887,7 @@ void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
             };
             for (int L = 0; L < kMaxLevels; ++L) {
                 int c = 0;
-                for (auto& h : sl->host_fc) c = std::max(c, h.count[L]);
+                for (auto& h : sl->host_fc) c = std::max(c, fc_count(h, L));
                 hint(sl->expect_count[L], c);
             }
             hint(sl->expect_shadow_total, shadow_need);
@@ -903,10 +903,10 @@ void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
         }
         for (auto& h : ctx->last_fc) {
             for (int L = 0; L < levels; ++L) {
-                rays_shadow += (uint64_t)h.shadow_count[L];
+                rays_shadow += (uint64_t)fc_shadow(h, L);
                 if (L >= 1) {
                     rays_refract += (uint64_t)h.refract[L];
-                    rays_reflect += (uint64_t)(h.count[L] - h.refract[L]);
+                    rays_reflect += (uint64_t)(fc_count(h, L) - h.refract[L]);
                 }
             }
             for (int k = 0; k < 2 * kMaxLevels; ++k) {
@@ -1549,8 +1549,8 @@ int pgrt_frame_diag(const pgrt_ctx* ctx, pgrt_level_diag* out, int max_levels) {
     for (const FrameCounters& h : ctx->last_fc)
         for (int L = 0; L < n; ++L) {
             pgrt_level_diag& d = out[L];
-            d.rays += (uint64_t)h.count[L];
-            d.shadow_rays += (uint64_t)h.shadow_count[L];
+            d.rays += (uint64_t)fc_count(h, L);
+            d.shadow_rays += (uint64_t)fc_shadow(h, L);
             d.visits += h.trav[L][0] + h.trav[L][14];
             d.wide_visits += h.trav[L][14];
             d.tests += h.trav[L][1];

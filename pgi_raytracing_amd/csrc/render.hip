@@ -57,7 +57,7 @@ __device__ __forceinline__ void tile_pixel(int slot_pix, const int4* tiles, int&
 __global__ __launch_bounds__(kBlock) void k_raygen(CameraView cam, FrameParams fp, const int4* __restrict__ tiles,
                                                    Queue q, int n0, FrameCounters* fc) {
     const int i = blockIdx.x * kBlock + threadIdx.x;
-    if (i == 0) fc->count[0] = n0;
+    if (i == 0) fc->count0 = n0;
     if (i >= n0) return;
     const int slot_pix = i / fp.nsb;
     const int s = fp.s0 + (i - slot_pix * fp.nsb);
@@ -127,32 +127,49 @@ void launch_raygen(const CameraView& cam, const FrameParams& fp, const int4* til
 // hit -> attributes -> material -> texture chain has one global round trip fewer per hop
 constexpr int kLdsMats = 64, kLdsTex = 32;
 
+// queue allocation in k_shade: 0 two 32-bit atomics per wave, 1 one packed 64-bit atomic per
+// wave, 2 one packed 64-bit atomic per block and grid-stride iteration
+// k_shade block size: mode 2 issues one allocation atomic per block and iteration
+#ifndef PGRT_SHADE_BLOCK
+#define PGRT_SHADE_BLOCK 256
+#endif
+constexpr int kShadeBlock = PGRT_SHADE_BLOCK;
+static_assert(kShadeBlock % kBlock == 0, "k_shade blocks are whole multiples of kBlock");
+#ifndef PGRT_ALLOC_MODE
+#define PGRT_ALLOC_MODE 2
+#endif
+
 template <bool LDS_TABLES>
-__global__ __launch_bounds__(kBlock) void k_shade(SceneView s, FrameParams fp, int level, Queue q, Queue next,
+__global__ __launch_bounds__(kShadeBlock) void k_shade(SceneView s, FrameParams fp, int level, Queue q, Queue next,
                                                   LevelNodes nodes, ShadowQueue sq, FrameCounters* fc) {
     __shared__ float lut255[256];
     __shared__ DevMaterial smat[LDS_TABLES ? kLdsMats : 1];
     __shared__ DevTexture stex[LDS_TABLES ? kLdsTex : 1];
     if constexpr (LDS_TABLES) {
-        for (int k = threadIdx.x; k < s.nmat; k += kBlock) smat[k] = s.mats[k];
-        for (int k = threadIdx.x; k < s.ntex; k += kBlock) stex[k] = s.tex[k];
+        for (int k = threadIdx.x; k < s.nmat; k += kShadeBlock) smat[k] = s.mats[k];
+        for (int k = threadIdx.x; k < s.ntex; k += kShadeBlock) stex[k] = s.tex[k];
         s.tex = stex;  // env_texel / tex_texel read descriptors through s.tex
     }
+#if PGRT_ALLOC_MODE == 2
+    __shared__ unsigned long long s_wtot[2][kShadeBlock / 64];
+    __shared__ unsigned long long s_bbase;
+    int it_par = 0;
+#endif
     const DevMaterial* mats = LDS_TABLES ? smat : s.mats;
     fill_byte_lut(lut255);  // ends with __syncthreads: the tables above are visible too
-    const int n = min(fc->count[level], q.cap);
+    const int n = min(fc_count(*fc, level), q.cap);
     const int tid = threadIdx.x;
     // one shadow queue for the whole batch: level L's rays follow those of levels < L (final by now)
     int sq_base = 0;
-    for (int l = 0; l < level; ++l) sq_base += fc->shadow_count[l];
+    for (int l = 0; l < level; ++l) sq_base += fc_shadow(*fc, l);
     const int sbits = s.nlight > 0 ? 32 - __clz(s.nlight) : 0;  // bits of a lane's shadow-ray count
     // software pipeline over the grid-stride loop: the next ray's record and hit are loaded
     // while this one is shaded (big queues give every thread several rays)
-    const int stride = gridDim.x * kBlock;
+    const int stride = gridDim.x * kShadeBlock;
     float4 nx_o = make_float4(0, 0, 0, 0), nx_d = make_float4(0, 0, 0, 0), nx_h = make_float4(0, 0, 0, 0);
     float nx_t = 0.0f;
     {
-        const int i0 = blockIdx.x * kBlock + tid;
+        const int i0 = blockIdx.x * kShadeBlock + tid;
         if (i0 < n) {
             nx_o = q.ro[i0];
             nx_d = q.rd[i0];
@@ -160,7 +177,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(SceneView s, FrameParams fp, i
             nx_h = q.hit[i0];
         }
     }
-    for (int base_i = blockIdx.x * kBlock; base_i < n; base_i += stride) {
+    for (int base_i = blockIdx.x * kShadeBlock; base_i < n; base_i += stride) {
         const int i = base_i + tid;
         const bool active = i < n;
         const float4 cur_o = nx_o, cur_d = nx_d, cur_h = nx_h;
@@ -268,15 +285,49 @@ __global__ __launch_bounds__(kBlock) void k_shade(SceneView s, FrameParams fp, i
         wave_prefix_small(nchild, 2, cpre, ctot);
         wave_prefix_small(nshadow, sbits, spre, stot);
         const int rtot = (int)__popcll(__ballot(nchild == 2));
-        int cb = 0, sb = 0;
-        if (__lane_id() == 0) {
-            const int ln = level + 1 < kMaxLevels ? level + 1 : level;
-            if (ctot) cb = atomicAdd(&fc->count[ln], ctot);
-            if (stot) sb = atomicAdd(&fc->shadow_count[level], stot);
-            if (rtot) atomicAdd(&fc->refract[ln], rtot);  // statistics only: no return
+        const unsigned long long wtot = ((unsigned long long)(unsigned)stot << 32) | (unsigned)ctot;
+        unsigned long long old = 0;
+#if PGRT_ALLOC_MODE == 2
+        // one returning atomic per BLOCK and iteration reserves both ranges (children | shadow
+        // rays << 32) for its 4 waves: a quarter of the same-address atomics of a per-wave
+        // allocation; wave totals double-buffered by iteration parity (a slow wave may still read
+        // the previous iteration's entries when a fast one writes the next)
+        {
+            const int w = tid >> 6;
+            if (__lane_id() == 0) {
+                s_wtot[it_par][w] = wtot;
+                if (rtot && level + 1 < kMaxLevels) atomicAdd(&fc->refract[level + 1], rtot);  // statistics
+            }
+            __syncthreads();
+            if (tid == 0) {
+                unsigned long long btot = 0;
+                for (int k = 0; k < kShadeBlock / 64; ++k) btot += s_wtot[it_par][k];
+                s_bbase = btot ? atomicAdd(&fc->alloc[level], btot) : 0ull;
+            }
+            __syncthreads();
+            old = s_bbase;
+            for (int k = 0; k < w; ++k) old += s_wtot[it_par][k];
+            it_par ^= 1;
         }
-        const int cbase = __builtin_amdgcn_readfirstlane(cb) + cpre;
-        const int sbase = sq_base + __builtin_amdgcn_readfirstlane(sb) + spre;
+#else
+        if (__lane_id() == 0) {
+#if PGRT_ALLOC_MODE == 1
+            // one returning atomic per wave reserves both ranges (children | shadow rays << 32)
+            if (wtot) old = atomicAdd(&fc->alloc[level], wtot);
+#else
+            // two 32-bit atomics per wave on the halves of the same word
+            unsigned lo = 0, hi = 0;
+            if (ctot) lo = atomicAdd(reinterpret_cast<unsigned*>(&fc->alloc[level]), (unsigned)ctot);
+            if (stot) hi = atomicAdd(reinterpret_cast<unsigned*>(&fc->alloc[level]) + 1, (unsigned)stot);
+            old = ((unsigned long long)hi << 32) | lo;
+#endif
+            if (rtot && level + 1 < kMaxLevels) atomicAdd(&fc->refract[level + 1], rtot);  // statistics: no return
+        }
+#endif
+        const int cb = __builtin_amdgcn_readfirstlane((int)(unsigned)(old & 0xffffffffull));
+        const int sb = __builtin_amdgcn_readfirstlane((int)(unsigned)(old >> 32));
+        const int cbase = cb + cpre;
+        const int sbase = sq_base + sb + spre;
         if (!active) continue;
         int4 link = make_int4(-1, -1, -1, 0);
         if (kind == 1) {
@@ -338,11 +389,14 @@ __global__ __launch_bounds__(kBlock) void k_shade(SceneView s, FrameParams fp, i
 void launch_shade(const SceneView& s, const FrameParams& fp, int level, Queue q, Queue next, LevelNodes nodes,
                   ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect) {
     if (max_count <= 0) return;
-    const int grid = grid_for(max_count, expect);
+    const int per_block = kShadeBlock / kBlock;  // grid_for counts kBlock-thread blocks
+    const int grid = std::max(1, grid_for(max_count, expect) / per_block);
     if (s.nmat <= kLdsMats && s.ntex <= kLdsTex)
-        hipLaunchKernelGGL(k_shade<true>, dim3(grid), dim3(kBlock), 0, stream, s, fp, level, q, next, nodes, sq, fc);
+        hipLaunchKernelGGL(k_shade<true>, dim3(grid), dim3(kShadeBlock), 0, stream, s, fp, level, q, next, nodes, sq,
+                           fc);
     else
-        hipLaunchKernelGGL(k_shade<false>, dim3(grid), dim3(kBlock), 0, stream, s, fp, level, q, next, nodes, sq, fc);
+        hipLaunchKernelGGL(k_shade<false>, dim3(grid), dim3(kShadeBlock), 0, stream, s, fp, level, q, next, nodes, sq,
+                           fc);
 }
 
 // ------------------------------------------------------------------ combine + finish
@@ -393,7 +447,7 @@ __device__ __forceinline__ float4 node_color(const SceneView& s, const ShadowQue
 __global__ __launch_bounds__(kBlock) void k_combine(SceneView s, int level, LevelNodes nodes,
                                                     const float4* __restrict__ child, ShadowQueue sq,
                                                     const FrameCounters* fc, int cap) {
-    const int n = min(fc->count[level], cap);
+    const int n = min(fc_count(*fc, level), cap);
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
         const int4 lk = nodes.link[i];
         if (lk.x < 0 && lk.z < 0) continue;  // colour written by k_shade

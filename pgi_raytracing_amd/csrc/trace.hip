@@ -76,7 +76,7 @@ __device__ __forceinline__ void tri_test(float4 q0, float4 q1, float4 q2, float 
 __device__ __forceinline__ int ray_count(const int* count_dev, int count_terms, int count_host, int cap) {
     if (!count_dev) return count_host;
     int n = 0;
-    for (int k = 0; k < count_terms; ++k) n += count_dev[k];
+    for (int k = 0; k < count_terms; ++k) n += count_dev[2 * k];  // stride 2: FrameCounters::alloc words
     return min(n, cap);
 }
 

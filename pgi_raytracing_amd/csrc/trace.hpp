@@ -15,16 +15,33 @@ constexpr int kMaxLevels = 16;    // max_level + 1 <= kMaxLevels
 
 // Per-frame device counters (zeroed by one hipMemsetAsync per batch).
 struct FrameCounters {
-    int count[kMaxLevels];         // rays queued per level
-    int shadow_count[kMaxLevels];  // shadow rays emitted per level
-    int refract[kMaxLevels];       // refraction rays among count[L]
-    int overflow;                  // set when an emit exceeded a queue capacity
-    int pad[3];
-    int fetch[2 * kMaxLevels];     // work counters of the closest-hit launches (level, shadow)
+    // queue allocation: shade(L) reserves its children (level L+1 rays) and its shadow rays with
+    // ONE 64-bit atomic per wave on alloc[L] = shadow rays of L << 32 | rays of level L+1 (the low
+    // word never carries: counts stay below 2^31); level 0's count is written by raygen.  Read
+    // them through fc_count / fc_shadow.
+    int count0;
+    int overflow;                        // set when an emit exceeded a queue capacity
+    int pad0[2];
+    unsigned long long alloc[kMaxLevels];
+    // statistics only (fire-and-forget atomics), on cache lines of their own so they never
+    // serialise with the allocation atomics
+    alignas(128) int refract[kMaxLevels];  // refraction rays among the rays of level L
+    alignas(128) int fetch[2 * kMaxLevels];  // work counters of the closest-hit launches (level, shadow)
     // profile == 2: per closest-hit launch {sum node visits, sum triangle tests, max visits of
     // one ray, max tests of one ray}; [0, kMaxLevels) level queues, [kMaxLevels, 2k) shadows
-    unsigned long long trav[2 * kMaxLevels][16];  // visits, tests, max visits, max tests, max wave iterations
+    alignas(128) unsigned long long trav[2 * kMaxLevels][16];  // visits, tests, max visits, max tests, max wave iterations
 };
+
+__host__ __device__ inline int fc_count(const FrameCounters& f, int L) {
+    return L == 0 ? f.count0 : (int)(unsigned)(f.alloc[L - 1] & 0xffffffffull);
+}
+__host__ __device__ inline int fc_shadow(const FrameCounters& f, int L) { return (int)(unsigned)(f.alloc[L] >> 32); }
+// device address of level L's ray count (a trace launch reads it); shadow counts are the high
+// words of alloc[0..levels), stride 2 ints (fc_shadow_counts)
+inline int* fc_count_ptr(FrameCounters* f, int L) {
+    return L == 0 ? &f->count0 : reinterpret_cast<int*>(&f->alloc[L - 1]);
+}
+inline int* fc_shadow_counts(FrameCounters* f) { return reinterpret_cast<int*>(&f->alloc[0]) + 1; }
 
 struct FrameParams {
     int spp_side;
