@@ -15,6 +15,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "trace.hpp"
+#include "shade_ops.hpp"
 
 namespace pgrt {
 
@@ -202,7 +203,18 @@ __global__ __launch_bounds__(kB) void k_depth(int n, const int* __restrict__ par
     atomicMax(max_depth, depth);
 }
 
+__global__ void k_tri_normals(const float4* __restrict__ tri, int m, float4* __restrict__ ng) {
+    const int k = blockIdx.x * kB + threadIdx.x;
+    if (k < m) ng[k] = tri_normal(tri[3 * k + 1], tri[3 * k + 2]);
+}
+
 }  // namespace
+
+void compute_tri_normals(const float4* tri, int m, float4* ng, hipStream_t stream) {
+    if (m <= 0) return;
+    hipLaunchKernelGGL(k_tri_normals, dim3(ceil_div(m, kB)), dim3(kB), 0, stream, tri, m, ng);
+    PGRT_HIP(hipGetLastError());
+}
 
 size_t lbvh_sort_temp_bytes(int ntri) {
     size_t bytes = 0;

@@ -1,0 +1,99 @@
+// camera_ops.hpp -- primary ray of a sample-batch slot, shared by k_raygen, the level-0 packet
+// traversal and the level-0 shade (which regenerate the ray in registers instead of reading a
+// ray queue, see DESIGN.md "fused primary rays").  Same float operation order everywhere, so a
+// regenerated ray is bit-identical to the one k_raygen stores.
+#pragma once
+
+#include "shade_ops.hpp"
+#include "trace.hpp"
+
+namespace pgrt {
+
+// slot pixel -> image pixel: 64x64 tiles, 8x8-pixel blocks inside (one wave = one block)
+__device__ __forceinline__ void tile_pixel(int slot_pix, const int4* tiles, int& px, int& py, bool& valid) {
+    const int tile = slot_pix / (kTile * kTile);
+    const int p = slot_pix - tile * kTile * kTile;
+    const int blk = p >> 6, w = p & 63;
+    const int lx = ((blk & 7) << 3) + (w & 7);
+    const int ly = ((blk >> 3) << 3) + (w >> 3);
+    const int4 tr = tiles[tile];
+    valid = lx < tr.z && ly < tr.w;
+    px = tr.x + lx;
+    py = tr.y + ly;
+}
+
+// Ray i of the batch (samples innermost): get_pixel's stratified sample position + jitter
+// (APP/raytracer.cpp:396-416) through Camera::GenerateRay, pinhole (PinHoleCamera.cpp:31-63) or
+// thin lens (:65-105).  ro = (org, tnear), rd = (dir, tfar).  Returns false for a padding slot
+// of a partial tile: ro = 0, rd = (0, 0, 0, -1) (tfar < 0 never hits).
+__device__ __forceinline__ bool primary_ray(const CameraView& cam, const FrameParams& fp, const int4* tiles, int i,
+                                            float4& ro, float4& rd) {
+    const int slot_pix = i / fp.nsb;
+    const int s = fp.s0 + (i - slot_pix * fp.nsb);
+    int px, py;
+    bool valid;
+    tile_pixel(slot_pix, tiles, px, py, valid);
+    if (!valid) {
+        ro = make_float4(0, 0, 0, 0);
+        rd = make_float4(0, 0, 0, -1.0f);
+        return false;
+    }
+    const uint32_t frame = fp.frame + (uint32_t)frame_of_tile(fp, slot_pix / (kTile * kTile));
+    const int S = fp.spp_side;
+    const int sx = s / S, sy = s - (s / S) * S;
+    const uint32_t pixel = (uint32_t)py * (uint32_t)cam.width + (uint32_t)px;
+    float j0 = 0.0f, j1 = 0.0f, j2 = 0.0f, j3 = 0.0f;
+    if (fp.jitter != PGRT_JITTER_NONE) {
+        const float Sf = (float)S;
+        const float ja = -0.5f / Sf, jb = 0.5f / Sf;
+        const float la = -fp.aperture / 2.0f, lb = fp.aperture / 2.0f;
+        const float u0 = pg_jitter_u01(fp.seed, frame, pixel, (uint32_t)s, 0);
+        const float u1 = pg_jitter_u01(fp.seed, frame, pixel, (uint32_t)s, 1);
+        const bool corr = fp.jitter == PGRT_JITTER_HASH_CORRELATED;
+        const float u2 = corr ? u0 : pg_jitter_u01(fp.seed, frame, pixel, (uint32_t)s, 2);
+        const float u3 = corr ? u1 : pg_jitter_u01(fp.seed, frame, pixel, (uint32_t)s, 3);
+        j0 = u0 * (jb - ja) + ja;
+        j1 = u1 * (jb - ja) + ja;
+        j2 = u2 * (lb - la) + la;
+        j3 = u3 * (lb - la) + la;
+    }
+    // get_pixel sample position (raytracer.cpp:412-413)
+    const float nx = (float)px + ((float)sx * (1.0f / (float)S)) + j0;
+    const float ny = (float)py + ((float)sy * (1.0f / (float)S)) + j1;
+    // camera-space direction with integer W/2, H/2 (PinHoleCamera.cpp:41-42, :67)
+    V3 crd = v3(nx - (float)(cam.width / 2), (float)(cam.height / 2) - ny, -cam.fy);
+    crd = normalize(crd);
+    V3 org, dir;
+    float tnear;
+    if (!fp.dof) {  // generate_ray(x, y) (PinHoleCamera.cpp:31-63)
+        org = v3(cam.from[0], cam.from[1], cam.from[2]);
+        dir = mat_mul(cam.m, crd);
+        tnear = 0.001f;
+    } else {  // generate_ray(x, y, focal, aperture) (PinHoleCamera.cpp:65-105)
+        V3 dws = normalize(mat_mul(cam.m, crd));
+        const V3 fpnt = v3(cam.from[0] + dws.x * fp.focal, cam.from[1] + dws.y * fp.focal,
+                           cam.from[2] + dws.z * fp.focal);
+        const V3 shift = mat_mul(cam.m, v3(j2, j3, 0));
+        org = v3(cam.from[0] + shift.x, cam.from[1] + shift.y, cam.from[2] + shift.z);
+        dir = normalize(v3(fpnt.x - org.x, fpnt.y - org.y, fpnt.z - org.z));
+        tnear = 0.01f;
+    }
+    ro = make_float4(org.x, org.y, org.z, tnear);
+    rd = make_float4(dir.x, dir.y, dir.z, 3.402823466e+38f);
+    return true;
+}
+
+// level-0 rays regenerated in registers (no ray queue): the launch's camera, batch and tiles
+struct PrimaryGen {
+    CameraView cam;
+    FrameParams fp;
+    const int4* tiles;
+    // when set, the packet traversal stores the rays it generated (k_raygen's queue layout) for a
+    // level-0 shade that reads them instead of regenerating
+    float4* store_ro;
+    float4* store_rd;
+    float* store_time;
+    int* store_count;  // the level-0 ray count (FrameCounters::count0), k_raygen's other output
+};
+
+}  // namespace pgrt

@@ -120,6 +120,7 @@ __host__ __device__ inline unsigned wide_leaf_bits(unsigned meta) {  // the leaf
 
 struct SceneView {  // kernel-argument view of the device scene
     const float4* tri;     // 3 x float4 per sorted triangle: (v0, orig id bits) (e1) (e2)
+    const float4* tri_ng;  // per sorted triangle: its Ng = e2 x e1 (tri_normal), w = 0
     const BvhNode* nodes;
     int root;              // node index, or a leaf code for tiny scenes
     const Bvh8Node* nodes8;  // 8-wide BVH (root = node 0)

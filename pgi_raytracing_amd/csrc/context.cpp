@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "trace.hpp"
+#include "camera_ops.hpp"
 
 using namespace pgrt;
 
@@ -252,6 +253,7 @@ struct pgrt_ctx {
     DevBuf<BvhNode> nodes;
     DevBuf<Bvh8Node> nodes8;
     DevBuf<float4> tri8;  // triangles in 8-wide leaf order
+    DevBuf<float4> tri_ng;  // Ng per binary-order reference (packet traversal)
     DevBuf<float> attr;
     DevBuf<DevMaterial> mats;
     DevBuf<DevTexture> texd;
@@ -478,12 +480,15 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
         build_bvh8(ctx->nodes.p, ctx->tri.p, bo.root, m, rlo, rhi, ctx->nodes8.p, ctx->tri8.p, &wide_nodes,
                    &wide_depth, st);
     }
+    ctx->tri_ng.alloc((size_t)std::max(1, m));
+    compute_tri_normals(ctx->tri.p, m, ctx->tri_ng.p, st);
     auto te = std::chrono::steady_clock::now();
     PGRT_REQUIRE(bo.max_depth <= kLdsStack + kGlobalStack - 2, PGRT_ERR_INVALID_ARGUMENT,
                  "BVH depth " + std::to_string(bo.max_depth) + " exceeds the traversal stack");
 
     SceneView& v = ctx->view;
     v.tri = ctx->tri.p;
+    v.tri_ng = ctx->tri_ng.p;
     v.nodes = ctx->nodes.p;
     v.root = bo.root;
     v.nodes8 = ctx->nodes8.p;
@@ -519,7 +524,7 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
         bi.scene_lo[k] = lo[k];
         bi.scene_hi[k] = hi[k];
     }
-    bi.device_bytes = ctx->tri.bytes() + ctx->tri8.bytes() + ctx->nodes8.bytes() + ctx->nodes.bytes() +
+    bi.device_bytes = ctx->tri.bytes() + ctx->tri_ng.bytes() + ctx->tri8.bytes() + ctx->nodes8.bytes() + ctx->nodes.bytes() +
                       ctx->attr.bytes() + ctx->texels.bytes();
     (void)t0;
 }
@@ -647,6 +652,12 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
         const char* e = getenv("PGRT_PACKET_LEVELS");
         return e ? atoi(e) : 0;
     }();
+    // PGRT_FUSED_RAYGEN: 0 k_raygen writes the level-0 ray queue; 1 the packet traversal and the
+    // level-0 shade both regenerate the rays; 2 the traversal generates and stores them
+    static const int fused_raygen = [] {
+        const char* e = getenv("PGRT_FUSED_RAYGEN");
+        return e ? atoi(e) : 2;
+    }();
     static const bool packet_shadow = [] {  // shadow queue as wave packets (A/B knob)
         const char* e = getenv("PGRT_PACKET_SHADOW");
         return e ? atoi(e) != 0 : false;
@@ -763,8 +774,15 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             for (int b = 0; b < 2; ++b)
                 q[b] = Queue{sl->q_ro[b].p, sl->q_rd[b].p, sl->q_time[b].p, sl->q_hit[b].p, sl->q_cap};
             ShadowQueue sq{sl->s_ro.p, sl->s_rd.p, sl->s_hit.p, sl->s_contrib.p, sl->s_cap};
+            // fused primary rays: the level-0 packet traversal and shade regenerate each ray from
+            // the camera in registers instead of k_raygen writing (and both reading) a 36-B/ray queue
+            // (mode 2: the traversal also stores them and the shade reads the queue)
+            const bool fuse = fused_raygen > 0 && packet_levels >= 0 && trace_packets_available(view, true);
+            const bool store = fused_raygen == 2;
+            const PrimaryGen gen{ctx->cam, fp, sl->tiles.p, store ? q[0].ro : nullptr, store ? q[0].rd : nullptr,
+                                 store ? q[0].time : nullptr, store ? &fcd->count0 : nullptr};
             int id = ctx->timer.begin(s, CAT_RAYGEN);
-            launch_raygen(ctx->cam, fp, sl->tiles.p, q[0], n0, fcd, s);
+            if (!fuse) launch_raygen(ctx->cam, fp, sl->tiles.p, q[0], n0, fcd, s);
             debug_sync(s, "raygen", 0, bi);
             ctx->timer.end(s, id);
             for (int L = 0; L < levels; ++L) {
@@ -777,14 +795,17 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 const int ex = L == 0 ? n0 : sl->expect_count[L];
                 id = ctx->timer.begin_kernel(CAT_TRACE, CAT_LTRACE + L);
                 const bool launched =
-                    launch_trace(view, qc.ro, qc.rd, qc.hit, fc_count_ptr(fcd, L), 0, maxc, &fcd->fetch[L], sl->gstack.p,
-                                 kTraceGridThreads, fcd->trav[L], p->profile >= 2, s, ex, 1, true,
-                                 L <= packet_levels);  // coherent 8x8-pixel waves -> packet traversal
+                    launch_trace(view, qc.ro, qc.rd, qc.hit, L == 0 && fuse ? nullptr : fc_count_ptr(fcd, L),
+                                 L == 0 && fuse ? n0 : 0, maxc, &fcd->fetch[L], sl->gstack.p, kTraceGridThreads,
+                                 fcd->trav[L], p->profile >= 2, s, ex, 1, true,
+                                 L <= packet_levels,  // coherent 8x8-pixel waves -> packet traversal
+                                 L == 0 && fuse ? &gen : nullptr);
                 ctx->timer.end_kernel(s, id, launched);
                 debug_sync(s, "trace", L, bi);
                 ++trace_launches;
                 id = ctx->timer.begin(s, CAT_SHADE, CAT_LSHADE + L);
-                launch_shade(view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex);
+                launch_shade(view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex,
+                             L == 0 && fuse && !store ? &gen : nullptr);
                 debug_sync(s, "shade", L, bi);
                 ctx->timer.end(s, id);
                 if (!staggered && (L == std::min(stagger_level, levels - 1))) {

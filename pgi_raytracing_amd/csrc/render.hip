@@ -12,6 +12,7 @@
 // once every level is traced.
 #include "shade_ops.hpp"
 #include "trace.hpp"
+#include "camera_ops.hpp"
 
 namespace pgrt {
 
@@ -42,77 +43,16 @@ __device__ __forceinline__ void wave_prefix_small(int x, int bits, int& prefix, 
 
 // ------------------------------------------------------------------ ray generation
 
-__device__ __forceinline__ void tile_pixel(int slot_pix, const int4* tiles, int& px, int& py, bool& valid) {
-    const int tile = slot_pix / (kTile * kTile);
-    const int p = slot_pix - tile * kTile * kTile;
-    const int blk = p >> 6, w = p & 63;
-    const int lx = ((blk & 7) << 3) + (w & 7);
-    const int ly = ((blk >> 3) << 3) + (w >> 3);
-    const int4 tr = tiles[tile];
-    valid = lx < tr.z && ly < tr.w;
-    px = tr.x + lx;
-    py = tr.y + ly;
-}
-
 __global__ __launch_bounds__(kBlock) void k_raygen(CameraView cam, FrameParams fp, const int4* __restrict__ tiles,
                                                    Queue q, int n0, FrameCounters* fc) {
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (i == 0) fc->count0 = n0;
     if (i >= n0) return;
-    const int slot_pix = i / fp.nsb;
-    const int s = fp.s0 + (i - slot_pix * fp.nsb);
-    int px, py;
-    bool valid;
-    tile_pixel(slot_pix, tiles, px, py, valid);
-    const uint32_t frame = fp.frame + (uint32_t)frame_of_tile(fp, slot_pix / (kTile * kTile));
-    if (!valid) {
-        q.ro[i] = make_float4(0, 0, 0, 0);
-        q.rd[i] = make_float4(0, 0, 0, -1.0f);  // padding slot: tfar < 0, never hits
-        q.time[i] = 0.0f;
-        return;
-    }
-    const int S = fp.spp_side;
-    const int sx = s / S, sy = s - (s / S) * S;
-    const uint32_t pixel = (uint32_t)py * (uint32_t)cam.width + (uint32_t)px;
-    float j0 = 0.0f, j1 = 0.0f, j2 = 0.0f, j3 = 0.0f;
-    if (fp.jitter != PGRT_JITTER_NONE) {
-        const float Sf = (float)S;
-        const float ja = -0.5f / Sf, jb = 0.5f / Sf;
-        const float la = -fp.aperture / 2.0f, lb = fp.aperture / 2.0f;
-        const float u0 = pg_jitter_u01(fp.seed, frame, pixel, (uint32_t)s, 0);
-        const float u1 = pg_jitter_u01(fp.seed, frame, pixel, (uint32_t)s, 1);
-        const bool corr = fp.jitter == PGRT_JITTER_HASH_CORRELATED;
-        const float u2 = corr ? u0 : pg_jitter_u01(fp.seed, frame, pixel, (uint32_t)s, 2);
-        const float u3 = corr ? u1 : pg_jitter_u01(fp.seed, frame, pixel, (uint32_t)s, 3);
-        j0 = u0 * (jb - ja) + ja;
-        j1 = u1 * (jb - ja) + ja;
-        j2 = u2 * (lb - la) + la;
-        j3 = u3 * (lb - la) + la;
-    }
-    // get_pixel sample position (raytracer.cpp:412-413)
-    const float nx = (float)px + ((float)sx * (1.0f / (float)S)) + j0;
-    const float ny = (float)py + ((float)sy * (1.0f / (float)S)) + j1;
-    // camera-space direction with integer W/2, H/2 (PinHoleCamera.cpp:41-42, :67)
-    V3 crd = v3(nx - (float)(cam.width / 2), (float)(cam.height / 2) - ny, -cam.fy);
-    crd = normalize(crd);
-    V3 org, dir;
-    float tnear;
-    if (!fp.dof) {  // generate_ray(x, y) (PinHoleCamera.cpp:31-63)
-        org = v3(cam.from[0], cam.from[1], cam.from[2]);
-        dir = mat_mul(cam.m, crd);
-        tnear = 0.001f;
-    } else {  // generate_ray(x, y, focal, aperture) (PinHoleCamera.cpp:65-105)
-        V3 dws = normalize(mat_mul(cam.m, crd));
-        const V3 fpnt = v3(cam.from[0] + dws.x * fp.focal, cam.from[1] + dws.y * fp.focal,
-                           cam.from[2] + dws.z * fp.focal);
-        const V3 shift = mat_mul(cam.m, v3(j2, j3, 0));
-        org = v3(cam.from[0] + shift.x, cam.from[1] + shift.y, cam.from[2] + shift.z);
-        dir = normalize(v3(fpnt.x - org.x, fpnt.y - org.y, fpnt.z - org.z));
-        tnear = 0.01f;
-    }
-    q.ro[i] = make_float4(org.x, org.y, org.z, tnear);
-    q.rd[i] = make_float4(dir.x, dir.y, dir.z, 3.402823466e+38f);
-    q.time[i] = PGRT_IOR_AIR;  // raytracer.cpp:416
+    float4 o, d;
+    const bool valid = primary_ray(cam, fp, tiles, i, o, d);
+    q.ro[i] = o;
+    q.rd[i] = d;
+    q.time[i] = valid ? PGRT_IOR_AIR : 0.0f;  // raytracer.cpp:416
 }
 
 void launch_raygen(const CameraView& cam, const FrameParams& fp, const int4* tiles, Queue q, int n0,
@@ -139,9 +79,10 @@ static_assert(kShadeBlock % kBlock == 0, "k_shade blocks are whole multiples of 
 #define PGRT_ALLOC_MODE 2
 #endif
 
-template <bool LDS_TABLES>
+template <bool LDS_TABLES, bool GEN>
 __global__ __launch_bounds__(kShadeBlock) void k_shade(SceneView s, FrameParams fp, int level, Queue q, Queue next,
-                                                  LevelNodes nodes, ShadowQueue sq, FrameCounters* fc) {
+                                                  LevelNodes nodes, ShadowQueue sq, FrameCounters* fc, PrimaryGen gen,
+                                                  int n_gen) {
     __shared__ float lut255[256];
     __shared__ DevMaterial smat[LDS_TABLES ? kLdsMats : 1];
     __shared__ DevTexture stex[LDS_TABLES ? kLdsTex : 1];
@@ -157,8 +98,11 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(SceneView s, FrameParams 
 #endif
     const DevMaterial* mats = LDS_TABLES ? smat : s.mats;
     fill_byte_lut(lut255);  // ends with __syncthreads: the tables above are visible too
-    const int n = min(fc_count(*fc, level), q.cap);
+    // GEN (level 0, fused primary rays): n_gen rays regenerated from the camera, no ray queue
+    // was written; this launch publishes the level-0 count in raygen's place
+    const int n = GEN ? n_gen : min(fc_count(*fc, level), q.cap);
     const int tid = threadIdx.x;
+    if (GEN && blockIdx.x == 0 && tid == 0) fc->count0 = n_gen;
     // one shadow queue for the whole batch: level L's rays follow those of levels < L (final by now)
     int sq_base = 0;
     for (int l = 0; l < level; ++l) sq_base += fc_shadow(*fc, l);
@@ -171,22 +115,30 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(SceneView s, FrameParams 
     {
         const int i0 = blockIdx.x * kShadeBlock + tid;
         if (i0 < n) {
-            nx_o = q.ro[i0];
-            nx_d = q.rd[i0];
-            nx_t = q.time[i0];
+            if constexpr (!GEN) {
+                nx_o = q.ro[i0];
+                nx_d = q.rd[i0];
+                nx_t = q.time[i0];
+            }
             nx_h = q.hit[i0];
         }
     }
     for (int base_i = blockIdx.x * kShadeBlock; base_i < n; base_i += stride) {
         const int i = base_i + tid;
         const bool active = i < n;
-        const float4 cur_o = nx_o, cur_d = nx_d, cur_h = nx_h;
-        const float cur_t = nx_t;
+        float4 cur_o = nx_o, cur_d = nx_d;
+        const float4 cur_h = nx_h;
+        float cur_t = nx_t;
         if (i + stride < n) {
-            nx_o = q.ro[i + stride];
-            nx_d = q.rd[i + stride];
-            nx_t = q.time[i + stride];
+            if constexpr (!GEN) {
+                nx_o = q.ro[i + stride];
+                nx_d = q.rd[i + stride];
+                nx_t = q.time[i + stride];
+            }
             nx_h = q.hit[i + stride];
+        }
+        if constexpr (GEN) {
+            if (active) cur_t = primary_ray(gen.cam, gen.fp, gen.tiles, i, cur_o, cur_d) ? PGRT_IOR_AIR : 0.0f;
         }
         int kind = 0;  // 0 final colour, 1 dielectric, 2 opaque (shadow rays pending)
         float4 color = make_float4(0, 0, 0, 1);
@@ -387,16 +339,22 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(SceneView s, FrameParams 
 }
 
 void launch_shade(const SceneView& s, const FrameParams& fp, int level, Queue q, Queue next, LevelNodes nodes,
-                  ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect) {
+                  ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect,
+                  const PrimaryGen* gen) {
     if (max_count <= 0) return;
     const int per_block = kShadeBlock / kBlock;  // grid_for counts kBlock-thread blocks
     const int grid = std::max(1, grid_for(max_count, expect) / per_block);
-    if (s.nmat <= kLdsMats && s.ntex <= kLdsTex)
-        hipLaunchKernelGGL(k_shade<true>, dim3(grid), dim3(kShadeBlock), 0, stream, s, fp, level, q, next, nodes, sq,
-                           fc);
-    else
-        hipLaunchKernelGGL(k_shade<false>, dim3(grid), dim3(kShadeBlock), 0, stream, s, fp, level, q, next, nodes, sq,
-                           fc);
+    const PrimaryGen g = gen ? *gen : PrimaryGen{};
+    const bool lds = s.nmat <= kLdsMats && s.ntex <= kLdsTex;
+#define PGRT_LAUNCH_S(L, G)                                                                                    \
+    hipLaunchKernelGGL((k_shade<L, G>), dim3(grid), dim3(kShadeBlock), 0, stream, s, fp, level, q, next, nodes, sq, \
+                       fc, g, max_count)
+    if (lds) {
+        if (gen) PGRT_LAUNCH_S(true, true); else PGRT_LAUNCH_S(true, false);
+    } else {
+        if (gen) PGRT_LAUNCH_S(false, true); else PGRT_LAUNCH_S(false, false);
+    }
+#undef PGRT_LAUNCH_S
 }
 
 // ------------------------------------------------------------------ combine + finish

@@ -133,6 +133,14 @@ __device__ inline float4 gamma_rgba(float in_r, float in_g, float in_b, float g)
     return make_float4(b, gg, r, 1.0f);
 }
 
+// Ng = e2 x e1 of a triangle record (v0|id, e1, e2): the first step of tri_test, also
+// precomputed per BVH reference (SceneView::tri_ng) with the same float operations
+__host__ __device__ __forceinline__ float4 tri_normal(float4 q1, float4 q2) {
+    const float e1x = q1.x, e1y = q1.y, e1z = q1.z;
+    const float e2x = q2.x, e2y = q2.y, e2z = q2.z;
+    return make_float4(e2y * e1z - e2z * e1y, e2z * e1x - e2x * e1z, e2x * e1y - e2y * e1x, 0.0f);
+}
+
 // Embree's Moeller-Trumbore triangle test (restated; see oracle.c tri_hit).
 __device__ __forceinline__ float xorsign(float a, float s) {
     return __uint_as_float(__float_as_uint(a) ^ (__float_as_uint(s) & 0x80000000u));

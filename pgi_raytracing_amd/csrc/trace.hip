@@ -21,11 +21,21 @@
 #include <hip/hip_ext.h>
 
 #include "trace.hpp"
+#include "camera_ops.hpp"
 
 namespace pgrt {
 
 constexpr int kTraceBlock = 256;
 constexpr int kSentinel = 0x7fffffff;  // bottom of every stack: "traversal finished"
+
+// packet traversal A/B switches: packed-pair child box tests (r1f: 507 vs 485 us per L0 launch,
+// off), precomputed triangle normals (r1f: 503 vs 511 us, on)
+#ifndef PGRT_PK_BOX
+#define PGRT_PK_BOX 0
+#endif
+#ifndef PGRT_TRI_NG
+#define PGRT_TRI_NG 1
+#endif
 
 __device__ __forceinline__ bool box_hit(float lox, float hix, float loy, float hiy, float loz,
                                         float hiz, float idx, float idy, float idz, float oix,
@@ -42,14 +52,13 @@ __device__ __forceinline__ bool box_hit(float lox, float hix, float loy, float h
 // Moeller-Trumbore as Embree's closest-hit path evaluates it (see oracle/oracle.c): e1 = v0 - v1,
 // e2 = v2 - v0 (precomputed), Ng = e2 x e1, scaled edge tests, IEEE divisions.  Closest hit in
 // (tnear, tfar]; ties in t go to the smaller original triangle index.
-__device__ __forceinline__ void tri_test(float4 q0, float4 q1, float4 q2, float ox, float oy, float oz, float dx,
-                                         float dy, float dz, float tnear, float tfar, float& best_t, float& best_u,
-                                         float& best_v, int& best_prim) {
+// ng: the triangle's Ng = e2 x e1 (tri_normal, precomputed per reference with the same float ops)
+__device__ __forceinline__ void tri_test_ng(float4 q0, float4 q1, float4 q2, float4 ng, float ox, float oy, float oz,
+                                            float dx, float dy, float dz, float tnear, float tfar, float& best_t,
+                                            float& best_u, float& best_v, int& best_prim) {
     const float e1x = q1.x, e1y = q1.y, e1z = q1.z;
     const float e2x = q2.x, e2y = q2.y, e2z = q2.z;
-    const float ngx = e2y * e1z - e2z * e1y;
-    const float ngy = e2z * e1x - e2x * e1z;
-    const float ngz = e2x * e1y - e2y * e1x;
+    const float ngx = ng.x, ngy = ng.y, ngz = ng.z;
     const float cx = q0.x - ox, cy = q0.y - oy, cz = q0.z - oz;
     const float rx = cy * dz - cz * dy;
     const float ry = cz * dx - cx * dz;
@@ -71,6 +80,36 @@ __device__ __forceinline__ void tri_test(float4 q0, float4 q1, float4 q2, float 
             }
         }
     }
+}
+
+__device__ __forceinline__ void tri_test(float4 q0, float4 q1, float4 q2, float ox, float oy, float oz, float dx,
+                                         float dy, float dz, float tnear, float tfar, float& best_t, float& best_u,
+                                         float& best_v, int& best_prim) {
+    tri_test_ng(q0, q1, q2, tri_normal(q1, q2), ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v,
+                best_prim);
+}
+
+// both child boxes of a binary node at once: the slab fmas as packed pairs (v_pk_fma_f32);
+// conservative like box_hit (the boxes are padded, the exit distance scaled by 1 + 1e-6)
+typedef float pgrt_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void box_hit2(float4 a, float4 b, float4 c, float idx, float idy, float idz, float oix,
+                                         float oiy, float oiz, float tmax, bool& h0, bool& h1, float& t0,
+                                         float& t1) {
+    const pgrt_f2 vidx = {idx, idx}, vidy = {idy, idy}, vidz = {idz, idz};
+    const pgrt_f2 voix = {-oix, -oix}, voiy = {-oiy, -oiy}, voiz = {-oiz, -oiz};
+    const pgrt_f2 lx = {a.x, b.x}, hx = {a.y, b.y}, ly = {a.z, b.z}, hy = {a.w, b.w}, lz = {c.x, c.z},
+                  hz = {c.y, c.w};
+    const pgrt_f2 tx0 = __builtin_elementwise_fma(lx, vidx, voix), tx1 = __builtin_elementwise_fma(hx, vidx, voix);
+    const pgrt_f2 ty0 = __builtin_elementwise_fma(ly, vidy, voiy), ty1 = __builtin_elementwise_fma(hy, vidy, voiy);
+    const pgrt_f2 tz0 = __builtin_elementwise_fma(lz, vidz, voiz), tz1 = __builtin_elementwise_fma(hz, vidz, voiz);
+    const float e0 = fmaxf(fmaxf(fminf(tx0.x, tx1.x), fminf(ty0.x, ty1.x)), fmaxf(fminf(tz0.x, tz1.x), 0.0f));
+    const float x0 = fminf(fminf(fmaxf(tx0.x, tx1.x), fmaxf(ty0.x, ty1.x)), fminf(fmaxf(tz0.x, tz1.x), tmax));
+    const float e1 = fmaxf(fmaxf(fminf(tx0.y, tx1.y), fminf(ty0.y, ty1.y)), fmaxf(fminf(tz0.y, tz1.y), 0.0f));
+    const float x1 = fminf(fminf(fmaxf(tx0.y, tx1.y), fmaxf(ty0.y, ty1.y)), fminf(fmaxf(tz0.y, tz1.y), tmax));
+    t0 = e0;
+    t1 = e1;
+    h0 = e0 <= x0 * 1.000001f;
+    h1 = e1 <= x1 * 1.000001f;
 }
 
 __device__ __forceinline__ int ray_count(const int* count_dev, int count_terms, int count_host, int cap) {
@@ -624,16 +663,19 @@ typedef const __attribute__((address_space(4))) float* cfloat_ptr;
 __device__ __forceinline__ float4 cload4(cfloat_ptr p) { return make_float4(p[0], p[1], p[2], p[3]); }
 constexpr int kPktStack = 64;  // wave-uniform stack entries (>= BVH depth + 2)
 
-template <bool COUNT>
+template <bool COUNT, bool GEN>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const float4* __restrict__ ro,
                                                            const float4* __restrict__ rd, float4* __restrict__ hits,
                                                            const int* __restrict__ count_dev, int count_terms,
                                                            int count_host, int cap,
-                                                           unsigned long long* __restrict__ counters) {
+                                                           unsigned long long* __restrict__ counters, PrimaryGen gen) {
     __shared__ int wstack[kTraceBlock / 64][kPktStack];
     const int wib = threadIdx.x >> 6;
     const int lane = __lane_id();
     const int n = ray_count(count_dev, count_terms, count_host, cap);
+    if constexpr (GEN) {
+        if (gen.store_count && blockIdx.x == 0 && threadIdx.x == 0) *gen.store_count = n;
+    }
     const cfloat_ptr nodes = (cfloat_ptr)(const void*)s.nodes;  // 16 floats per node
     const cfloat_ptr tris = (cfloat_ptr)(const void*)s.tri;     // 12 floats per triangle
     unsigned long long nvis = 0, ntest = 0;
@@ -643,8 +685,17 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const fl
         const bool valid = i < n;
         float4 o4 = make_float4(0, 0, 0, 0), d4 = make_float4(0, 0, 1, -1.0f);
         if (valid) {
-            o4 = ro[i];
-            d4 = rd[i];
+            if constexpr (GEN) {
+                const bool pv = primary_ray(gen.cam, gen.fp, gen.tiles, i, o4, d4);  // level 0: no ray queue read
+                if (gen.store_ro) {
+                    gen.store_ro[i] = o4;
+                    gen.store_rd[i] = d4;
+                    gen.store_time[i] = pv ? PGRT_IOR_AIR : 0.0f;
+                }
+            } else {
+                o4 = ro[i];
+                d4 = rd[i];
+            }
         }
         const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
         const float dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
@@ -672,8 +723,13 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const fl
                                          __float_as_int(nd[15]));
                 if (COUNT) ++rvis;
                 float t0, t1;
+#if PGRT_PK_BOX
+                bool h0, h1;
+                box_hit2(a, b, c, idx, idy, idz, oix, oiy, oiz, best_t, h0, h1, t0, t1);
+#else
                 const bool h0 = box_hit(a.x, a.y, a.z, a.w, c.x, c.y, idx, idy, idz, oix, oiy, oiz, best_t, t0);
                 const bool h1 = box_hit(b.x, b.y, b.z, b.w, c.z, c.w, idx, idy, idz, oix, oiy, oiz, best_t, t1);
+#endif
                 const unsigned long long b0 = __ballot(h0), b1 = __ballot(h1);
                 if (b0 == 0ull && b1 == 0ull) {
                     node = sp > 0 ? wstack[wib][--sp] : kSentinel;
@@ -693,7 +749,14 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const fl
                     const cfloat_ptr q = tris + 12 * k;
                     const float4 q0 = cload4(q), q1 = cload4(q + 4), q2 = cload4(q + 8);
                     if (COUNT) ++rtest;
+#if PGRT_TRI_NG
+                    const float4 ng = cload4((cfloat_ptr)(const void*)s.tri_ng + 4 * k);  // precomputed Ng
+                    if (live)
+                        tri_test_ng(q0, q1, q2, ng, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v,
+                                    best_prim);
+#else
                     if (live) tri_test(q0, q1, q2, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v, best_prim);
+#endif
                 }
                 node = sp > 0 ? wstack[wib][--sp] : kSentinel;
             }
@@ -723,11 +786,20 @@ void set_trace_events(hipEvent_t start, hipEvent_t stop) {
 #define PGRT_TLAUNCH(kernel, grid, block, lds, stream, ...) \
     hipExtLaunchKernelGGL(kernel, grid, block, lds, stream, t_ev_start, t_ev_stop, 0, __VA_ARGS__)
 
+bool trace_packets_available(const SceneView& s, bool coherent) {
+    static const bool packets = [] {  // PGRT_PACKETS=0: level 0 on the one-lane kernel too
+        const char* e = getenv("PGRT_PACKETS");
+        return !(e && atoi(e) == 0);
+    }();
+    return coherent && packets && !s.wide && s.root >= 0 && s.depth + 2 <= kPktStack;
+}
+
 bool launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4* hits, const int* count_dev,
                   int count_host, int max_count, int* fetch, int* gstack, int gstack_threads,
                   unsigned long long* counters, bool count, hipStream_t stream, int expect, int count_terms,
-                  bool allow_group, bool coherent) {
+                  bool allow_group, bool coherent, const PrimaryGen* gen) {
     if (max_count <= 0) return false;
+    // gen (fused primary rays) is only passed when trace_packets_available(s, coherent) holds
     static const bool force_spill = getenv("PGRT_FORCE_SPILL") != nullptr;  // A/B of the stack layout
     if (s.wide) {
         int grid = ceil_div(expect > 0 && expect < max_count ? expect : max_count, kTraceBlock);
@@ -740,21 +812,21 @@ bool launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4
                                count_dev, count_terms, count_host, max_count, gstack, counters);
         return true;
     }
-    // small queues: 8 lanes per ray over the 8-wide BVH (PGRT_GROUP_MAX: largest queue, rays)
-    static const bool packets = [] {  // PGRT_PACKETS=0: level 0 on the one-lane kernel too
-        const char* e = getenv("PGRT_PACKETS");
-        return !(e && atoi(e) == 0);
-    }();
-    if (coherent && packets && !s.wide && s.root >= 0 && s.depth + 2 <= kPktStack) {
+    // coherent level-0 waves: packet traversal
+    if (trace_packets_available(s, coherent)) {
         const int exg = expect > 0 && expect < max_count ? expect : max_count;
         int grid = ceil_div(exg, kTraceBlock);
         if (grid > 16384) grid = 16384;
-        if (count)
-            PGRT_TLAUNCH((k_trace_pkt<true>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
-                               count_dev, count_terms, count_host, max_count, counters);
-        else
-            PGRT_TLAUNCH((k_trace_pkt<false>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
-                               count_dev, count_terms, count_host, max_count, counters);
+        const PrimaryGen g = gen ? *gen : PrimaryGen{};
+#define PGRT_LAUNCH_P(C, G)                                                                                  \
+    PGRT_TLAUNCH((k_trace_pkt<C, G>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits, count_dev, \
+                 count_terms, count_host, max_count, counters, g)
+        if (count) {
+            if (gen) PGRT_LAUNCH_P(true, true); else PGRT_LAUNCH_P(true, false);
+        } else {
+            if (gen) PGRT_LAUNCH_P(false, true); else PGRT_LAUNCH_P(false, false);
+        }
+#undef PGRT_LAUNCH_P
         return true;
     }
     const int group_max = s.group_max;

@@ -90,10 +90,14 @@ struct ShadowQueue {  // one per batch: the shadow rays of every level, level-ma
 // fetch: a zeroed device int per launch (persistent waves pull 64 rays per atomic).
 // Ray count: sum of count_dev[0 .. count_terms) when count_dev is set, else count_host.
 // returns false when nothing was launched (max_count <= 0)
+struct PrimaryGen;  // camera_ops.hpp
+// the level-0 packet traversal is used for coherent queues (and can regenerate primary rays)
+bool trace_packets_available(const SceneView& s, bool coherent);
 bool launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4* hits, const int* count_dev,
                   int count_host, int max_count, int* fetch, int* gstack, int gstack_threads,
                   unsigned long long* counters, bool count, hipStream_t stream, int expect = 0,
-                  int count_terms = 1, bool allow_group = true, bool coherent = false);
+                  int count_terms = 1, bool allow_group = true, bool coherent = false,
+                  const PrimaryGen* gen = nullptr);
 // events the next launch_trace records at its kernel's start / end (nullptr: none)
 void set_trace_events(hipEvent_t start, hipEvent_t stop);
 int trace_block_size();
@@ -106,7 +110,8 @@ void launch_occluded(const SceneView& s, const float4* ro, const float4* rd, int
 void launch_raygen(const CameraView& cam, const FrameParams& fp, const int4* tiles, Queue q, int n0,
                    FrameCounters* fc, hipStream_t stream);
 void launch_shade(const SceneView& s, const FrameParams& fp, int level, Queue q, Queue next, LevelNodes nodes,
-                  ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect = 0);
+                  ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect = 0,
+                  const PrimaryGen* gen = nullptr);  // gen: level 0 regenerates its rays (max_count of them)
 // level L's final colours from its shadow hits and level L+1's colours (child)
 void launch_combine(const SceneView& s, int level, LevelNodes nodes, const float4* child, ShadowQueue sq,
                     const FrameCounters* fc, int max_count, hipStream_t stream, int expect = 0);
@@ -157,6 +162,8 @@ void build_lbvh(const float* pos_dev, int ntri, float4* tri_out, BvhNode* nodes_
                 void* sort_tmp, size_t sort_tmp_bytes, float pad, BuildOut* out, hipStream_t stream);
 // collapse the binary BVH (root: node index or leaf code; root box used for a leaf root) into
 // the 8-wide quantized layout; tri_out receives the triangles in wide-leaf order
+// Ng = e2 x e1 per BVH reference (SceneView::tri_ng), same float operations as tri_test
+void compute_tri_normals(const float4* tri, int m, float4* ng, hipStream_t stream);
 void build_bvh8(const BvhNode* bin, const float4* tri_in, int root, int n, float4 root_lo, float4 root_hi,
                 Bvh8Node* out, float4* tri_out, int* num_nodes, int* depth, hipStream_t stream);
 size_t lbvh_sort_temp_bytes(int ntri);
