@@ -131,6 +131,7 @@ struct SceneView {  // kernel-argument view of the device scene
     int ntri;
     int depth;             // binary BVH depth (bounds the traversal stack)
     const float* attr;     // 16 floats per ORIGINAL triangle: n0 n1 n2 uv0 uv1 uv2, mat (bits)
+    const unsigned char* prim_glass;  // per ORIGINAL triangle: 1 when its material is dielectric
     const DevMaterial* mats;
     const DevTexture* tex;
     int nmat, ntex;

@@ -255,6 +255,7 @@ struct pgrt_ctx {
     DevBuf<float4> tri8;  // triangles in 8-wide leaf order
     DevBuf<float4> tri_ng;  // Ng per binary-order reference (packet traversal)
     DevBuf<float> attr;
+    DevBuf<unsigned char> prim_glass;
     DevBuf<DevMaterial> mats;
     DevBuf<DevTexture> texd;
     DevBuf<unsigned char> texels;
@@ -426,6 +427,16 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
 
     ctx->attr.alloc(attr.size());
     PGRT_HIP(hipMemcpyAsync(ctx->attr.p, attr.data(), attr.size() * sizeof(float), hipMemcpyHostToDevice, st));
+    // per-triangle "dielectric" byte: the shadow resolve's is_illuminated test reads one byte
+    // instead of the attribute line + the material table (two dependent loads fewer)
+    std::vector<unsigned char> glass((size_t)std::max(1, n), 0);
+    for (int i = 0; i < n; ++i) {
+        int mid;
+        std::memcpy(&mid, &attr[(size_t)i * 16 + 15], sizeof(int));
+        glass[i] = mats[mid].type == PGRT_MATERIAL_DIELECTRIC ? 1 : 0;
+    }
+    ctx->prim_glass.alloc(glass.size());
+    PGRT_HIP(hipMemcpyAsync(ctx->prim_glass.p, glass.data(), glass.size(), hipMemcpyHostToDevice, st));
     ctx->mats.alloc(mats.size());
     PGRT_HIP(hipMemcpyAsync(ctx->mats.p, mats.data(), mats.size() * sizeof(DevMaterial), hipMemcpyHostToDevice, st));
     ctx->texd.alloc(texs.size());
@@ -501,6 +512,7 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
     v.ntri = n;
     v.depth = bo.max_depth;
     v.attr = ctx->attr.p;
+    v.prim_glass = ctx->prim_glass.p;
     v.mats = ctx->mats.p;
     v.tex = ctx->texd.p;
     v.nmat = (int)mats.size();

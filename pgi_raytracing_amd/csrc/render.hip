@@ -373,10 +373,7 @@ __device__ __forceinline__ float4 opaque_color(const SceneView& s, const ShadowQ
         const int k = base + j;
         const int prim = __float_as_int(sq.hit[k].w);
         bool lit = true;  // is_illuminated (raytracer.cpp:163-173): closest hit decides
-        if (prim >= 0) {
-            const int mid = __float_as_int(s.attr[16 * (size_t)prim + 15]);
-            lit = s.mats[mid].type == PGRT_MATERIAL_DIELECTRIC;
-        }
+        if (prim >= 0) lit = s.prim_glass[prim] != 0;  // the occluder's material is dielectric
         if (lit) {
             const float4 c = sq.contrib[k];
             blue += c.x;
@@ -446,7 +443,9 @@ __global__ __launch_bounds__(kBlock) void k_finish(SceneView s, FrameParams fp, 
     if (!valid) return;
     const int area = fp.spp_side * fp.spp_side;
     // gamma(Color4f{final.b/area, final.g/area, final.r/area}) (raytracer.cpp:431-435)
-    const float4 o = gamma_rgba(acc.z / (float)area, acc.y / (float)area, acc.x / (float)area, fp.gamma);
+    // x / 1 == x exactly: the (correctly rounded, ~10-instruction) divisions only for S > 1
+    const float4 o = area == 1 ? gamma_rgba(acc.z, acc.y, acc.x, fp.gamma)
+                               : gamma_rgba(acc.z / (float)area, acc.y / (float)area, acc.x / (float)area, fp.gamma);
     if (out_mode == 0) {
         float* dst = out + (size_t)frame_of_tile(fp, p / (kTile * kTile)) * fp.frame_stride +
                      ((size_t)(py - oy) * (size_t)pitch + (size_t)(px - ox)) * 4;

@@ -125,12 +125,22 @@ __device__ inline float4 mix_srgb(float4 c0, float4 c1, float a) {
     return make_float4(srgb_compress(m.z), srgb_compress(m.y), srgb_compress(m.x), 0.1f);
 }
 
+// pg_powf(x, g) with the gamma slider's default g = 0.5 (wave-uniform) decided once: pg_powf's
+// y = 0.5 result is sqrtf(x) except at its earlier special cases that sqrtf does not share
+// (+0 for x = -0, +inf for x = -inf); NaN / negative x give NaN either way
+__device__ __forceinline__ float gamma_pow(float x, float g) {
+    if (g == 0.5f) {
+        if (x == 0.0f) return 0.0f;
+        if (x == -__builtin_inff()) return __builtin_inff();
+        return sqrtf(x);
+    }
+    return pg_powf(x, g);
+}
+
 // Raytracer::gamma (APP/raytracer.cpp:439-446) on Color4f{b,g,r} input: returns r,g,b order.
 __device__ inline float4 gamma_rgba(float in_r, float in_g, float in_b, float g) {
-    const float b = pg_powf(in_b, g) * pg_powf(in_b, g);
-    const float gg = pg_powf(in_g, g) * pg_powf(in_g, g);
-    const float r = pg_powf(in_r, g) * pg_powf(in_r, g);
-    return make_float4(b, gg, r, 1.0f);
+    const float pb = gamma_pow(in_b, g), pg = gamma_pow(in_g, g), pr = gamma_pow(in_r, g);
+    return make_float4(pb * pb, pg * pg, pr * pr, 1.0f);
 }
 
 // Ng = e2 x e1 of a triangle record (v0|id, e1, e2): the first step of tri_test, also
