@@ -45,7 +45,7 @@ CONFIGS = {
     "C2": dict(width=1920, height=1080, max_level=5, spp_side=1, dof=0, scene="avenger"),
     "C3": dict(width=1920, height=1080, max_level=5, spp_side=8, dof=1, scene="avenger"),
     "C4": dict(width=3840, height=2160, max_level=5, spp_side=8, dof=1, scene="avenger"),
-    "C5": dict(width=4096, height=4096, max_level=8, spp_side=1, dof=0, scene="random1m"),
+    "C5": dict(width=4096, height=4096, max_level=8, spp_side=1, dof=0, scene="random1m", in_flight=2),
 }
 
 
@@ -67,7 +67,7 @@ def parse():
     ap.add_argument("--in-flight", type=int, default=None,
                     help="frames in flight (pgrt_set_frames_in_flight); default 6 (r1 scan, tools/inflight_scan.py)")
     ap.add_argument("--frames-per-call", type=int, default=None,
-                    help="frames per submission (pgrt_render_frames_*_async, 1..64); default 8 x world (r1e scans)")
+                    help="frames per submission (pgrt_render_frames_*_async, 1..64); default 8 x world for C2, 1 otherwise (r1e scans)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (multi-thread leg)")
     a = ap.parse_args()
@@ -112,7 +112,8 @@ def main():
     # frames per call: ~22 M rays per call per rank (8 C2 frames on 1 GPU, 8 x world frames of a
     # rank's 1/world share at N GPUs); r1e scans: N=1 F=8 0.255 ms/frame (F=16 with 6 in flight
     # 0.39), emulated N=8 rank F=64 0.040 ms/frame (F=16 0.045)
-    F = max(1, min(64, args.frames_per_call or 8 * world))
+    # (C3/C4/C5 frames are 15-80x heavier than C2's and fill the GPU on their own: 1 per call)
+    F = max(1, min(64, args.frames_per_call or (8 * world if args.config == "C2" else 1)))
     fb = ctx.alloc(F * args.width * args.height * 16) if rank == 0 or world == 1 else None
     if world > 1:
         uid = [Context.comm_unique_id() if rank == 0 else None]
@@ -127,7 +128,9 @@ def main():
     # frames in flight: a step is one whole frame (every rank's tiles rendered, gathered and
     # unpacked on rank 0); up to `in_flight` consecutive frames overlap on the device, so one
     # frame's latency-bound deep levels share the CUs with the next frame's wide levels
-    in_flight = args.in_flight or 6
+    # (C5: 2 -- r1g scan 26.1 / 23.5 / 25.2 ms at 1 / 2 / 3, and 175 ms at 6: its 16.7 M-ray
+    # frames with 9 levels of queues per frame set thrash the memory system)
+    in_flight = args.in_flight or CONFIGS[args.config].get("in_flight", 6)
     ctx.set_frames_in_flight(in_flight)
 
     def run_frames(n):

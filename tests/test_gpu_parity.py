@@ -32,6 +32,10 @@ def test_device_math_bit_exact(gpu_ctx):
                         np.array([0.0, -0.0, 1.0, 0.5, 1e-38, 3e38])]).astype(np.float32)
     b = np.concatenate([rng.uniform(-3, 40, 4000), rng.uniform(0.1, 3, 2000), rng.uniform(1, 2, 500),
                         np.array([2.0, 3.0, 0.0, 32.0, 2.4, 0.5])]).astype(np.float32)
+    # k_finish's gamma fast path (column 2 is gamma_pow == pg_powf): y = 0.5 on special and random x
+    sp = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, -1.0, 1.0, 1e-45, 3.4e38], np.float32)
+    a = np.concatenate([a, sp, rng.uniform(0, 4, 1000).astype(np.float32)]).astype(np.float32)
+    b = np.concatenate([b, np.full(len(sp) + 1000, 0.5, np.float32)]).astype(np.float32)
     pairs = np.stack([a, b], 1)
     dev = gpu_ctx.selftest_math(pairs)
     host = np.zeros_like(dev)
