@@ -45,7 +45,10 @@ CONFIGS = {
     "C2": dict(width=1920, height=1080, max_level=5, spp_side=1, dof=0, scene="avenger"),
     "C3": dict(width=1920, height=1080, max_level=5, spp_side=8, dof=1, scene="avenger"),
     "C4": dict(width=3840, height=2160, max_level=5, spp_side=8, dof=1, scene="avenger"),
-    "C5": dict(width=4096, height=4096, max_level=8, spp_side=1, dof=0, scene="random1m", in_flight=2),
+    # C5: secondary rays in a triangle soup are incoherent, wave packets only at level 0
+    # (r1g: packet levels 0 / 2 -> 23.1 / 26.2 ms/frame)
+    "C5": dict(width=4096, height=4096, max_level=8, spp_side=1, dof=0, scene="random1m", in_flight=2,
+               env={"PGRT_PACKET_LEVELS": "0"}),
 }
 
 
@@ -91,6 +94,8 @@ def main():
     from pgi_raytracing_amd import abi
     from pgi_raytracing_amd.raytracer import Context, load_obj
 
+    for k, v in CONFIGS[args.config].get("env", {}).items():  # per-workload libpgrt knobs
+        os.environ.setdefault(k, v)
     env = os.path.join(ROOT, "assets", "spherical_map_windows.jpg")
     if args.scene == "avenger":
         if rank == 0 and not os.path.exists(scenes.AVENGER_OBJ):

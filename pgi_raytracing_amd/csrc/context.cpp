@@ -660,9 +660,13 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
         const char* e = getenv("PGRT_STAGGER_LEVEL");
         return e ? atoi(e) : -1;
     }();
-    static const int packet_levels = [] {  // levels traced as wave packets (A/B knob)
+    // levels 0..packet_levels traced as wave packets: level 0 is coherent by construction (8x8
+    // pixel blocks), levels 1-2 since k_shade queues each wave's reflections and refractions as
+    // separate pixel-ordered groups (r1g C2: 0 / 1 / 2 / 3 / all levels 0.206 / 0.197 / 0.194 /
+    // 0.196 / 0.202 ms/frame)
+    static const int packet_levels = [] {
         const char* e = getenv("PGRT_PACKET_LEVELS");
-        return e ? atoi(e) : 0;
+        return e ? atoi(e) : 2;
     }();
     // PGRT_FUSED_RAYGEN: 0 k_raygen writes the level-0 ray queue; 1 the packet traversal and the
     // level-0 shade both regenerate the rays; 2 the traversal generates and stores them

@@ -69,6 +69,10 @@ constexpr int kLdsMats = 64, kLdsTex = 32;
 
 // queue allocation in k_shade: 0 two 32-bit atomics per wave, 1 one packed 64-bit atomic per
 // wave, 2 one packed 64-bit atomic per block and grid-stride iteration
+// child order in the next level's queue: 1 = per wave, its reflections then its refractions
+#ifndef PGRT_CHILD_SPLIT
+#define PGRT_CHILD_SPLIT 1
+#endif
 // k_shade block size: mode 2 issues one allocation atomic per block and iteration
 #ifndef PGRT_SHADE_BLOCK
 #define PGRT_SHADE_BLOCK 256
@@ -278,23 +282,35 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(SceneView s, FrameParams 
 #endif
         const int cb = __builtin_amdgcn_readfirstlane((int)(unsigned)(old & 0xffffffffull));
         const int sb = __builtin_amdgcn_readfirstlane((int)(unsigned)(old >> 32));
-        const int cbase = cb + cpre;
+#if PGRT_CHILD_SPLIT
+        // the wave's reflection rays first, then its refraction rays, each group in pixel order:
+        // the next level's waves are coherent bundles instead of alternating reflect / refract
+        const unsigned long long mrefl = __ballot(nchild >= 1), mrefr = __ballot(nchild == 2);
+        const int refl_slot = cb + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mrefl >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((unsigned)mrefl, 0u));
+        const int refr_slot = cb + (int)__popcll(mrefl) +
+                              (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mrefr >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((unsigned)mrefr, 0u));
+        (void)cpre;
+#else
+        const int refl_slot = cb + cpre, refr_slot = refl_slot + 1;
+#endif
         const int sbase = sq_base + sb + spre;
         if (!active) continue;
         int4 link = make_int4(-1, -1, -1, 0);
         if (kind == 1) {
-            if (cbase + nchild > next.cap || level + 1 >= kMaxLevels) {
+            if ((nchild == 2 ? max(refl_slot, refr_slot) : refl_slot) >= next.cap || level + 1 >= kMaxLevels) {
                 atomicOr(&fc->overflow, 1);
             } else {
-                next.ro[cbase] = make_float4(hitp.x, hitp.y, hitp.z, 0.01f);
-                next.rd[cbase] = make_float4(refl_dir.x, refl_dir.y, refl_dir.z, 3.402823466e+38f);
-                next.time[cbase] = n1;
-                link.x = cbase;
+                next.ro[refl_slot] = make_float4(hitp.x, hitp.y, hitp.z, 0.01f);
+                next.rd[refl_slot] = make_float4(refl_dir.x, refl_dir.y, refl_dir.z, 3.402823466e+38f);
+                next.time[refl_slot] = n1;
+                link.x = refl_slot;
                 if (nchild == 2) {
-                    next.ro[cbase + 1] = make_float4(hitp.x, hitp.y, hitp.z, 0.01f);
-                    next.rd[cbase + 1] = make_float4(refr_dir.x, refr_dir.y, refr_dir.z, 3.402823466e+38f);
-                    next.time[cbase + 1] = n2;
-                    link.y = cbase + 1;
+                    next.ro[refr_slot] = make_float4(hitp.x, hitp.y, hitp.z, 0.01f);
+                    next.rd[refr_slot] = make_float4(refr_dir.x, refr_dir.y, refr_dir.z, 3.402823466e+38f);
+                    next.time[refr_slot] = n2;
+                    link.y = refr_slot;
                 }
             }
             nodes.att[i] = att;
