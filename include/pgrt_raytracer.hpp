@@ -217,6 +217,16 @@ public:
         ++params_.frame;
         return t;
     }
+    // Batched frames (pgrt_render_frames_device_async): nframes consecutive frames (frame indices
+    // params.frame .. + nframes - 1) in one launch sequence, frame f at rgba_device + f*W*H*4.
+    unsigned long long SubmitFrames(int nframes, void* rgba_device) {
+        params_.gamma_level = gamma_level;
+        unsigned long long t = 0;
+        check(ctx_, pgrt_render_frames_device_async(ctx_, &params_, nframes, rgba_device, &t),
+              "pgrt_render_frames_device_async");
+        params_.frame += (unsigned)nframes;
+        return t;
+    }
     pgrt_stats Wait(unsigned long long ticket) {
         pgrt_stats st{};
         check(ctx_, pgrt_render_wait(ctx_, ticket, &st), "pgrt_render_wait");
