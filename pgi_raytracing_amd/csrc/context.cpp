@@ -16,6 +16,7 @@
 
 #include "trace.hpp"
 #include "camera_ops.hpp"
+#include "shade_ray.hpp"
 
 using namespace pgrt;
 
@@ -264,6 +265,16 @@ struct pgrt_ctx {
     bool has_scene = false;
     unsigned long long scene_gen = 0;  // bumped by every pgrt_set_scene
     bool group_max_env = false;        // PGRT_GROUP_MAX given (else the default follows the mode)
+    // levels 0..packet_levels traced as wave packets (PGRT_PACKET_LEVELS): level 0 is coherent by
+    // construction (8x8 pixel blocks), levels 1-2 since k_shade queues each wave's reflections and
+    // refractions as separate pixel-ordered groups (r1g C2: 0 / 1 / 2 / 3 / all levels 0.206 /
+    // 0.197 / 0.194 / 0.196 / 0.202 ms/frame)
+    int packet_levels = 2;
+    // level-0 rays (PGRT_FUSED_RAYGEN): 0 k_raygen writes the ray queue; 1 the packet traversal
+    // and the level-0 shade both regenerate them; 2 (default) the traversal generates and stores
+    // them; 3 the traversal also shades its packets (one level-0 kernel; r1g: 938 us vs 486 + 457,
+    // throughput 0.201 vs 0.197 ms/frame -- the shading is latency-bound, not HBM-bound)
+    int fused_raygen = 2;
     pgrt_bvh_info info{};
 
     CameraView cam{};
@@ -505,6 +516,10 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
     v.nodes8 = ctx->nodes8.p;
     v.tri8 = ctx->tri8.p;
     v.depth8 = wide_depth;
+    const char* epl = getenv("PGRT_PACKET_LEVELS");  // read per set_scene (tests compare settings)
+    ctx->packet_levels = epl ? atoi(epl) : 2;
+    const char* efr = getenv("PGRT_FUSED_RAYGEN");
+    ctx->fused_raygen = efr ? atoi(efr) : 2;
     const char* eg = getenv("PGRT_GROUP_MAX");  // read per set_scene (tests compare settings)
     v.group_max = eg ? atoi(eg) : kDefaultGroupMax;
     ctx->group_max_env = eg != nullptr;
@@ -660,20 +675,9 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
         const char* e = getenv("PGRT_STAGGER_LEVEL");
         return e ? atoi(e) : -1;
     }();
-    // levels 0..packet_levels traced as wave packets: level 0 is coherent by construction (8x8
-    // pixel blocks), levels 1-2 since k_shade queues each wave's reflections and refractions as
-    // separate pixel-ordered groups (r1g C2: 0 / 1 / 2 / 3 / all levels 0.206 / 0.197 / 0.194 /
-    // 0.196 / 0.202 ms/frame)
-    static const int packet_levels = [] {
-        const char* e = getenv("PGRT_PACKET_LEVELS");
-        return e ? atoi(e) : 2;
-    }();
-    // PGRT_FUSED_RAYGEN: 0 k_raygen writes the level-0 ray queue; 1 the packet traversal and the
-    // level-0 shade both regenerate the rays; 2 the traversal generates and stores them
-    static const int fused_raygen = [] {
-        const char* e = getenv("PGRT_FUSED_RAYGEN");
-        return e ? atoi(e) : 2;
-    }();
+    // pipeline knobs read per set_scene (ctx->packet_levels, ctx->fused_raygen; see there)
+    const int packet_levels = ctx->packet_levels;
+    const int fused_raygen = ctx->fused_raygen;
     static const bool packet_shadow = [] {  // shadow queue as wave packets (A/B knob)
         const char* e = getenv("PGRT_PACKET_SHADOW");
         return e ? atoi(e) != 0 : false;
@@ -792,11 +796,13 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             ShadowQueue sq{sl->s_ro.p, sl->s_rd.p, sl->s_hit.p, sl->s_contrib.p, sl->s_cap};
             // fused primary rays: the level-0 packet traversal and shade regenerate each ray from
             // the camera in registers instead of k_raygen writing (and both reading) a 36-B/ray queue
-            // (mode 2: the traversal also stores them and the shade reads the queue)
+            // (mode 2: the traversal also stores them and the shade reads the queue; mode 3: the
+            // traversal shades its packets itself -- no level-0 hit / ray queue, no k_shade launch)
             const bool fuse = fused_raygen > 0 && packet_levels >= 0 && trace_packets_available(view, true);
-            const bool store = fused_raygen == 2;
+            const bool shade0 = fuse && fused_raygen == 3 && view.nmat <= kLdsMats && view.ntex <= kLdsTex;
+            const bool store = fuse && (fused_raygen == 2 || (fused_raygen == 3 && !shade0));
             const PrimaryGen gen{ctx->cam, fp, sl->tiles.p, store ? q[0].ro : nullptr, store ? q[0].rd : nullptr,
-                                 store ? q[0].time : nullptr, store ? &fcd->count0 : nullptr};
+                                 store ? q[0].time : nullptr, &fcd->count0};
             int id = ctx->timer.begin(s, CAT_RAYGEN);
             if (!fuse) launch_raygen(ctx->cam, fp, sl->tiles.p, q[0], n0, fcd, s);
             debug_sync(s, "raygen", 0, bi);
@@ -809,19 +815,21 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 LevelNodes ln{sl->n_color[L]->p, sl->n_link[L]->p, sl->n_att[L]->p};
                 // grid hints: last frame's per-level counts (+25 %); level 0 is exact
                 const int ex = L == 0 ? n0 : sl->expect_count[L];
+                const ShadeArgs shade_args{qn, ln, sq, fcd};
                 id = ctx->timer.begin_kernel(CAT_TRACE, CAT_LTRACE + L);
                 const bool launched =
                     launch_trace(view, qc.ro, qc.rd, qc.hit, L == 0 && fuse ? nullptr : fc_count_ptr(fcd, L),
                                  L == 0 && fuse ? n0 : 0, maxc, &fcd->fetch[L], sl->gstack.p, kTraceGridThreads,
                                  fcd->trav[L], p->profile >= 2, s, ex, 1, true,
                                  L <= packet_levels,  // coherent 8x8-pixel waves -> packet traversal
-                                 L == 0 && fuse ? &gen : nullptr);
+                                 L == 0 && fuse ? &gen : nullptr, L == 0 && shade0 ? &shade_args : nullptr);
                 ctx->timer.end_kernel(s, id, launched);
                 debug_sync(s, "trace", L, bi);
                 ++trace_launches;
                 id = ctx->timer.begin(s, CAT_SHADE, CAT_LSHADE + L);
-                launch_shade(view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex,
-                             L == 0 && fuse && !store ? &gen : nullptr);
+                if (!(L == 0 && shade0))
+                    launch_shade(view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex,
+                                 L == 0 && fuse && !store ? &gen : nullptr);
                 debug_sync(s, "shade", L, bi);
                 ctx->timer.end(s, id);
                 if (!staggered && (L == std::min(stagger_level, levels - 1))) {

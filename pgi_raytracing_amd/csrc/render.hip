@@ -13,6 +13,7 @@
 #include "shade_ops.hpp"
 #include "trace.hpp"
 #include "camera_ops.hpp"
+#include "shade_ray.hpp"
 
 namespace pgrt {
 
@@ -23,22 +24,6 @@ static int grid_for(int max_count, int expect) {
     const int n = (expect > 0 && expect < max_count) ? expect : max_count;
     const int g = ceil_div(n, kBlock);
     return g < 1 ? 1 : (g > 4096 ? 4096 : g);
-}
-
-// Wave-level slot allocation for small per-lane counts (children <= 2, shadow rays <= lights):
-// the exclusive prefix is sum_b 2^b * (lanes below with bit b set), one ballot + mbcnt per bit,
-// and lane 0 issues the queue atomics together (one round trip).  Every lane of the wave must
-// be active (k_shade keeps whole waves in its loop).
-__device__ __forceinline__ void wave_prefix_small(int x, int bits, int& prefix, int& total) {
-    prefix = 0;
-    total = 0;
-    for (int b = 0; b < bits; ++b) {
-        const unsigned long long m = __ballot((x >> b) & 1);
-        const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-        prefix += below << b;
-        total += __popcll(m) << b;
-    }
 }
 
 // ------------------------------------------------------------------ ray generation
@@ -63,25 +48,16 @@ void launch_raygen(const CameraView& cam, const FrameParams& fp, const int4* til
 
 // ------------------------------------------------------------------ shading (trace body)
 
-// LDS_TABLES: the material and texture-descriptor tables are copied to LDS per block, so the
-// hit -> attributes -> material -> texture chain has one global round trip fewer per hop
-constexpr int kLdsMats = 64, kLdsTex = 32;
+// LDS_TABLES: the material and texture-descriptor tables are copied to LDS per block
+// (kLdsMats / kLdsTex, shade_ray.hpp)
 
-// queue allocation in k_shade: 0 two 32-bit atomics per wave, 1 one packed 64-bit atomic per
-// wave, 2 one packed 64-bit atomic per block and grid-stride iteration
-// child order in the next level's queue: 1 = per wave, its reflections then its refractions
-#ifndef PGRT_CHILD_SPLIT
-#define PGRT_CHILD_SPLIT 1
-#endif
-// k_shade block size: mode 2 issues one allocation atomic per block and iteration
+// k_shade block size (one allocation atomic per block and iteration, shade_ray.hpp; r1f A/B:
+// 256 beat 512 and 1024)
 #ifndef PGRT_SHADE_BLOCK
 #define PGRT_SHADE_BLOCK 256
 #endif
 constexpr int kShadeBlock = PGRT_SHADE_BLOCK;
 static_assert(kShadeBlock % kBlock == 0, "k_shade blocks are whole multiples of kBlock");
-#ifndef PGRT_ALLOC_MODE
-#define PGRT_ALLOC_MODE 2
-#endif
 
 template <bool LDS_TABLES, bool GEN>
 __global__ __launch_bounds__(kShadeBlock) void k_shade(SceneView s, FrameParams fp, int level, Queue q, Queue next,
@@ -90,16 +66,13 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(SceneView s, FrameParams 
     __shared__ float lut255[256];
     __shared__ DevMaterial smat[LDS_TABLES ? kLdsMats : 1];
     __shared__ DevTexture stex[LDS_TABLES ? kLdsTex : 1];
+    __shared__ ShadeAllocLds<kShadeBlock> alds;
     if constexpr (LDS_TABLES) {
         for (int k = threadIdx.x; k < s.nmat; k += kShadeBlock) smat[k] = s.mats[k];
         for (int k = threadIdx.x; k < s.ntex; k += kShadeBlock) stex[k] = s.tex[k];
         s.tex = stex;  // env_texel / tex_texel read descriptors through s.tex
     }
-#if PGRT_ALLOC_MODE == 2
-    __shared__ unsigned long long s_wtot[2][kShadeBlock / 64];
-    __shared__ unsigned long long s_bbase;
     int it_par = 0;
-#endif
     const DevMaterial* mats = LDS_TABLES ? smat : s.mats;
     fill_byte_lut(lut255);  // ends with __syncthreads: the tables above are visible too
     // GEN (level 0, fused primary rays): n_gen rays regenerated from the camera, no ray queue
@@ -144,213 +117,10 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(SceneView s, FrameParams 
         if constexpr (GEN) {
             if (active) cur_t = primary_ray(gen.cam, gen.fp, gen.tiles, i, cur_o, cur_d) ? PGRT_IOR_AIR : 0.0f;
         }
-        int kind = 0;  // 0 final colour, 1 dielectric, 2 opaque (shadow rays pending)
-        float4 color = make_float4(0, 0, 0, 1);
-        int nshadow = 0, nchild = 0;
-        V3 org = v3(0, 0, 0), dirraw = v3(0, 0, 0), d = v3(0, 0, 0), nrm = v3(0, 0, 0), hitp = v3(0, 0, 0);
-        V3 refl_dir = v3(0, 0, 0), refr_dir = v3(0, 0, 0);
-        float n1 = 0, n2 = 0, t = 0;
-        float4 att = make_float4(0, 0, 0, 0);
-        float m_d_r = 0, m_d_g = 0, m_d_b = 0;
-        int mid = 0;
-        if (active) {
-            const float4 o4 = cur_o;
-            const float4 d4 = cur_d;
-            const float rtime = cur_t;
-            const float4 h = cur_h;
-            org = v3(o4.x, o4.y, o4.z);
-            dirraw = v3(d4.x, d4.y, d4.z);
-            if (d4.w < 0.0f) {
-                color = make_float4(0, 0, 0, 0);  // padding slot
-            } else {
-                d = normalize(dirraw);
-                const int prim = __float_as_int(h.w);
-                if (prim < 0) {
-                    color = env_texel(s, lut255, d);  // miss (raytracer.cpp:390-393)
-                } else {
-                    t = h.x;
-                    const float* a = s.attr + 16 * (size_t)prim;
-                    const float u = h.y, v = h.z;
-                    V3 nn = v3(interp1(a[0], a[3], a[6], u, v), interp1(a[1], a[4], a[7], u, v),
-                               interp1(a[2], a[5], a[8], u, v));
-                    mid = __float_as_int(a[15]);
-                    const DevMaterial& m = mats[mid];
-                    nn = normalize(nn);
-                    hitp = org + scale(t, dirraw);
-                    if (rtime == PGRT_IOR_AIR) {
-                        n1 = PGRT_IOR_AIR;
-                        n2 = m.ior;
-                    } else {
-                        n1 = m.ior;
-                        n2 = PGRT_IOR_AIR;
-                    }
-                    if (dot(nn, d) > 0) nn = -nn;
-                    nrm = nn;
-                    if (level >= fp.max_level) {
-                        color = make_float4(0, 0, 0, 1);  // raytracer.cpp:282-283
-                    } else if (m.type == PGRT_MATERIAL_DIELECTRIC) {
-                        kind = 1;
-                        {  // get_reflection_ray (raytracer.cpp:209-235)
-                            const V3 dd = normalize(d), rn = normalize(nn);
-                            refl_dir = dd - scale(2, scale(dot(dd, rn), rn));
-                        }
-                        att.x = pg_expf(-(1 - m.kd[0]) * t);  // raytracer.cpp:303-305
-                        att.y = pg_expf(-(1 - m.kd[1]) * t);
-                        att.z = pg_expf(-(1 - m.kd[2]) * t);
-                        {  // get_refraction_ray (raytracer.cpp:178-207)
-                            const V3 dd = normalize(d), rn = normalize(nn);
-                            const float n1_n2 = n1 / n2;
-                            const float d_n = dot(dd, rn);
-                            const V3 sd = v3(dd.x * n1_n2, dd.y * n1_n2, dd.z * n1_n2);
-                            const float kk = n1_n2 * d_n + sqrtf(1 - ((n1_n2 * n1_n2) * (1 - (d_n * d_n))));
-                            refr_dir = sd - scale(kk, rn);
-                        }
-                        nchild = 1;
-                        if (refr_dir.x == refr_dir.x) {  // no total internal reflection
-                            nchild = 2;
-                            const float cos1 = fabsf(dot(nn, -d));
-                            const float alpha = (n1 - n2) / (n1 + n2);
-                            att.w = (float)((double)(alpha * alpha + (1 - (alpha * alpha))) *
-                                            pg_pow_d((double)(1 - cos1), 5.0));
-                        }
-                    } else {
-                        kind = 2;
-                        if (m.tex < 0) {
-                            m_d_r = m.kd[2];
-                            m_d_g = m.kd[1];
-                            m_d_b = m.kd[0];
-                        } else {
-                            const float tu = interp1(a[9], a[11], a[13], u, v);
-                            const float tv = interp1(a[10], a[12], a[14], u, v);
-                            const V3 tx = tex_texel(s.tex[m.tex], s.texels, lut255, tu, 1.0f - tv);
-                            m_d_r = tx.x;
-                            m_d_g = tx.y;
-                            m_d_b = tx.z;
-                        }
-                        for (int li = 0; li < s.nlight; ++li) {
-                            const DevLight& L = s.lights[li];
-                            if (!(dot(nn, v3(L.pos[0], L.pos[1], L.pos[2])) < 0)) ++nshadow;
-                        }
-                        color = make_float4(0, 0, 0, 1);
-                    }
-                }
-            }
-        }
-        // ---- queue allocation (wave-uniform control flow) ----
-        int cpre, ctot, spre, stot;
-        wave_prefix_small(nchild, 2, cpre, ctot);
-        wave_prefix_small(nshadow, sbits, spre, stot);
-        const int rtot = (int)__popcll(__ballot(nchild == 2));
-        const unsigned long long wtot = ((unsigned long long)(unsigned)stot << 32) | (unsigned)ctot;
-        unsigned long long old = 0;
-#if PGRT_ALLOC_MODE == 2
-        // one returning atomic per BLOCK and iteration reserves both ranges (children | shadow
-        // rays << 32) for its 4 waves: a quarter of the same-address atomics of a per-wave
-        // allocation; wave totals double-buffered by iteration parity (a slow wave may still read
-        // the previous iteration's entries when a fast one writes the next)
-        {
-            const int w = tid >> 6;
-            if (__lane_id() == 0) {
-                s_wtot[it_par][w] = wtot;
-                if (rtot && level + 1 < kMaxLevels) atomicAdd(&fc->refract[level + 1], rtot);  // statistics
-            }
-            __syncthreads();
-            if (tid == 0) {
-                unsigned long long btot = 0;
-                for (int k = 0; k < kShadeBlock / 64; ++k) btot += s_wtot[it_par][k];
-                s_bbase = btot ? atomicAdd(&fc->alloc[level], btot) : 0ull;
-            }
-            __syncthreads();
-            old = s_bbase;
-            for (int k = 0; k < w; ++k) old += s_wtot[it_par][k];
-            it_par ^= 1;
-        }
-#else
-        if (__lane_id() == 0) {
-#if PGRT_ALLOC_MODE == 1
-            // one returning atomic per wave reserves both ranges (children | shadow rays << 32)
-            if (wtot) old = atomicAdd(&fc->alloc[level], wtot);
-#else
-            // two 32-bit atomics per wave on the halves of the same word
-            unsigned lo = 0, hi = 0;
-            if (ctot) lo = atomicAdd(reinterpret_cast<unsigned*>(&fc->alloc[level]), (unsigned)ctot);
-            if (stot) hi = atomicAdd(reinterpret_cast<unsigned*>(&fc->alloc[level]) + 1, (unsigned)stot);
-            old = ((unsigned long long)hi << 32) | lo;
-#endif
-            if (rtot && level + 1 < kMaxLevels) atomicAdd(&fc->refract[level + 1], rtot);  // statistics: no return
-        }
-#endif
-        const int cb = __builtin_amdgcn_readfirstlane((int)(unsigned)(old & 0xffffffffull));
-        const int sb = __builtin_amdgcn_readfirstlane((int)(unsigned)(old >> 32));
-#if PGRT_CHILD_SPLIT
-        // the wave's reflection rays first, then its refraction rays, each group in pixel order:
-        // the next level's waves are coherent bundles instead of alternating reflect / refract
-        const unsigned long long mrefl = __ballot(nchild >= 1), mrefr = __ballot(nchild == 2);
-        const int refl_slot = cb + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mrefl >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((unsigned)mrefl, 0u));
-        const int refr_slot = cb + (int)__popcll(mrefl) +
-                              (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mrefr >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((unsigned)mrefr, 0u));
-        (void)cpre;
-#else
-        const int refl_slot = cb + cpre, refr_slot = refl_slot + 1;
-#endif
-        const int sbase = sq_base + sb + spre;
-        if (!active) continue;
-        int4 link = make_int4(-1, -1, -1, 0);
-        if (kind == 1) {
-            if ((nchild == 2 ? max(refl_slot, refr_slot) : refl_slot) >= next.cap || level + 1 >= kMaxLevels) {
-                atomicOr(&fc->overflow, 1);
-            } else {
-                next.ro[refl_slot] = make_float4(hitp.x, hitp.y, hitp.z, 0.01f);
-                next.rd[refl_slot] = make_float4(refl_dir.x, refl_dir.y, refl_dir.z, 3.402823466e+38f);
-                next.time[refl_slot] = n1;
-                link.x = refl_slot;
-                if (nchild == 2) {
-                    next.ro[refr_slot] = make_float4(hitp.x, hitp.y, hitp.z, 0.01f);
-                    next.rd[refr_slot] = make_float4(refr_dir.x, refr_dir.y, refr_dir.z, 3.402823466e+38f);
-                    next.time[refr_slot] = n2;
-                    link.y = refr_slot;
-                }
-            }
-            nodes.att[i] = att;
-        } else if (kind == 2 && nshadow > 0) {
-            if (sbase + nshadow > sq.cap) {
-                atomicOr(&fc->overflow, 1);
-            } else {
-                const DevMaterial& m = mats[mid];
-                int k = sbase;
-                for (int li = 0; li < s.nlight; ++li) {
-                    const DevLight& L = s.lights[li];
-                    const V3 lp = v3(L.pos[0], L.pos[1], L.pos[2]);
-                    if (dot(nrm, lp) < 0) continue;  // is_illuminated's N.L test (raytracer.cpp:155)
-                    // LightSource::GenerateRay(hit): org = light, dir = hit position vector
-                    sq.ro[k] = make_float4(lp.x, lp.y, lp.z, 0.01f);
-                    sq.rd[k] = make_float4(hitp.x, hitp.y, hitp.z,
-                                           length(v3(lp.x - hitp.x, lp.y - hitp.y, lp.z - hitp.z)));
-                    // Phong term for this light (raytracer.cpp:355-382)
-                    const V3 lv = normalize(v3(lp.x - hitp.x, lp.y - hitp.y, lp.z - hitp.z));
-                    const V3 cv = normalize(v3(org.x - dirraw.x, org.y - dirraw.y, org.z - dirraw.z));
-                    const float gam = m.ns;
-                    const float i_d_r = L.kd[2], i_d_g = L.kd[1], i_d_b = L.kd[0];
-                    const float i_s_r = L.ks[2], i_s_g = L.ks[1], i_s_b = L.ks[0];
-                    const float m_s_r = m.ks[2], m_s_g = m.ks[1], m_s_b = m.ks[0];
-                    const float nl = dot(nrm, lv);
-                    V3 l_r = scale(2 * nl, nrm) - lv;
-                    l_r = normalize(l_r);
-                    const float spec = pg_powf(dot(cv, l_r), gam);
-                    const float tb = i_d_b * m_d_b * dot(nrm, lv) + i_s_b * m_s_b * spec;
-                    const float tg = i_d_g * m_d_g * dot(nrm, lv) + i_s_g * m_s_g * spec;
-                    const float tr = i_d_r * m_d_r * dot(nrm, lv) + i_s_r * m_s_r * spec;
-                    sq.contrib[k] = make_float4(tb, tg, tr, 0.0f);
-                    ++k;
-                }
-                link.z = sbase;
-                link.w = nshadow;
-            }
-        }
-        nodes.link[i] = link;
-        if (link.x < 0 && link.z < 0) nodes.color[i] = color;  // else derived by k_finish
+        ShadeOut r;
+        shade_eval(s, mats, lut255, level, fp.max_level, active, cur_o, cur_d, cur_t, cur_h, r);
+        const ShadeSlots sl = shade_alloc<kShadeBlock>(alds, it_par, fc, level, sq_base, sbits, r);
+        if (active) shade_emit(s, mats, level, i, r, sl, next, nodes, sq, fc);
     }
 }
 

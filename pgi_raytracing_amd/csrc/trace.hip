@@ -22,6 +22,7 @@
 
 #include "trace.hpp"
 #include "camera_ops.hpp"
+#include "shade_ray.hpp"
 
 namespace pgrt {
 
@@ -663,13 +664,30 @@ typedef const __attribute__((address_space(4))) float* cfloat_ptr;
 __device__ __forceinline__ float4 cload4(cfloat_ptr p) { return make_float4(p[0], p[1], p[2], p[3]); }
 constexpr int kPktStack = 64;  // wave-uniform stack entries (>= BVH depth + 2)
 
-template <bool COUNT, bool GEN>
+// SHADE (level 0 with GEN): the wave shades its packet right after the traversal (shade_ray.hpp)
+// -- ray and hit stay in registers, no hit record or ray queue goes through HBM, and the level-0
+// k_shade launch disappears.  The loop is then block-uniform (shade_alloc has barriers).
+template <bool COUNT, bool GEN, bool SHADE>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const float4* __restrict__ ro,
                                                            const float4* __restrict__ rd, float4* __restrict__ hits,
                                                            const int* __restrict__ count_dev, int count_terms,
                                                            int count_host, int cap,
-                                                           unsigned long long* __restrict__ counters, PrimaryGen gen) {
+                                                           unsigned long long* __restrict__ counters, PrimaryGen gen,
+                                                           ShadeArgs sh) {
     __shared__ int wstack[kTraceBlock / 64][kPktStack];
+    __shared__ float lut255[SHADE ? 256 : 1];
+    __shared__ DevMaterial smat[SHADE ? kLdsMats : 1];
+    __shared__ DevTexture stex[SHADE ? kLdsTex : 1];
+    __shared__ ShadeAllocLds<kTraceBlock> alds;
+    int it_par = 0;
+    SceneView ss = s;  // shading view: descriptors from LDS
+    if constexpr (SHADE) {
+        for (int k = threadIdx.x; k < s.nmat; k += kTraceBlock) smat[k] = s.mats[k];
+        for (int k = threadIdx.x; k < s.ntex; k += kTraceBlock) stex[k] = s.tex[k];
+        ss.tex = stex;
+        fill_byte_lut(lut255);  // ends with __syncthreads
+    }
+    const int sbits = s.nlight > 0 ? 32 - __clz(s.nlight) : 0;
     const int wib = threadIdx.x >> 6;
     const int lane = __lane_id();
     const int n = ray_count(count_dev, count_terms, count_host, cap);
@@ -679,14 +697,15 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const fl
     const cfloat_ptr nodes = (cfloat_ptr)(const void*)s.nodes;  // 16 floats per node
     const cfloat_ptr tris = (cfloat_ptr)(const void*)s.tri;     // 12 floats per triangle
     unsigned long long nvis = 0, ntest = 0;
-    for (int base = (blockIdx.x * (kTraceBlock / 64) + wib) * 64; base < n;
-         base += gridDim.x * kTraceBlock) {
+    for (int bbase = blockIdx.x * kTraceBlock; bbase < n; bbase += gridDim.x * kTraceBlock) {
+        const int base = bbase + wib * 64;  // waves past n run no traversal but join the barriers
         const int i = base + lane;
         const bool valid = i < n;
         float4 o4 = make_float4(0, 0, 0, 0), d4 = make_float4(0, 0, 1, -1.0f);
+        bool pv = false;
         if (valid) {
             if constexpr (GEN) {
-                const bool pv = primary_ray(gen.cam, gen.fp, gen.tiles, i, o4, d4);  // level 0: no ray queue read
+                pv = primary_ray(gen.cam, gen.fp, gen.tiles, i, o4, d4);  // level 0: no ray queue read
                 if (gen.store_ro) {
                     gen.store_ro[i] = o4;
                     gen.store_rd[i] = d4;
@@ -761,7 +780,15 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const fl
                 node = sp > 0 ? wstack[wib][--sp] : kSentinel;
             }
         }
-        if (valid) hits[i] = make_float4(live ? best_t : tfar, best_u, best_v, __int_as_float(best_prim));
+        const float4 hit = make_float4(live ? best_t : tfar, best_u, best_v, __int_as_float(best_prim));
+        if constexpr (SHADE) {
+            ShadeOut r;
+            shade_eval(ss, smat, lut255, 0, gen.fp.max_level, valid, o4, d4, pv ? PGRT_IOR_AIR : 0.0f, hit, r);
+            const ShadeSlots sl = shade_alloc<kTraceBlock>(alds, it_par, sh.fc, 0, 0, sbits, r);
+            if (valid) shade_emit(ss, smat, 0, i, r, sl, sh.next, sh.nodes, sh.sq, sh.fc);
+        } else {
+            if (valid) hits[i] = hit;
+        }
         if (COUNT && lane == 0) {
             nvis += rvis;
             ntest += rtest;
@@ -797,7 +824,7 @@ bool trace_packets_available(const SceneView& s, bool coherent) {
 bool launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4* hits, const int* count_dev,
                   int count_host, int max_count, int* fetch, int* gstack, int gstack_threads,
                   unsigned long long* counters, bool count, hipStream_t stream, int expect, int count_terms,
-                  bool allow_group, bool coherent, const PrimaryGen* gen) {
+                  bool allow_group, bool coherent, const PrimaryGen* gen, const ShadeArgs* shade) {
     if (max_count <= 0) return false;
     // gen (fused primary rays) is only passed when trace_packets_available(s, coherent) holds
     static const bool force_spill = getenv("PGRT_FORCE_SPILL") != nullptr;  // A/B of the stack layout
@@ -818,13 +845,18 @@ bool launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4
         int grid = ceil_div(exg, kTraceBlock);
         if (grid > 16384) grid = 16384;
         const PrimaryGen g = gen ? *gen : PrimaryGen{};
-#define PGRT_LAUNCH_P(C, G)                                                                                  \
-    PGRT_TLAUNCH((k_trace_pkt<C, G>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits, count_dev, \
-                 count_terms, count_host, max_count, counters, g)
+        const ShadeArgs sa = shade ? *shade : ShadeArgs{};
+#define PGRT_LAUNCH_P(C, G, SH)                                                                                  \
+    PGRT_TLAUNCH((k_trace_pkt<C, G, SH>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits, count_dev, \
+                 count_terms, count_host, max_count, counters, g, sa)
         if (count) {
-            if (gen) PGRT_LAUNCH_P(true, true); else PGRT_LAUNCH_P(true, false);
+            if (gen && shade) PGRT_LAUNCH_P(true, true, true);
+            else if (gen) PGRT_LAUNCH_P(true, true, false);
+            else PGRT_LAUNCH_P(true, false, false);
         } else {
-            if (gen) PGRT_LAUNCH_P(false, true); else PGRT_LAUNCH_P(false, false);
+            if (gen && shade) PGRT_LAUNCH_P(false, true, true);
+            else if (gen) PGRT_LAUNCH_P(false, true, false);
+            else PGRT_LAUNCH_P(false, false, false);
         }
 #undef PGRT_LAUNCH_P
         return true;

@@ -91,13 +91,14 @@ struct ShadowQueue {  // one per batch: the shadow rays of every level, level-ma
 // Ray count: sum of count_dev[0 .. count_terms) when count_dev is set, else count_host.
 // returns false when nothing was launched (max_count <= 0)
 struct PrimaryGen;  // camera_ops.hpp
+struct ShadeArgs;   // shade_ray.hpp
 // the level-0 packet traversal is used for coherent queues (and can regenerate primary rays)
 bool trace_packets_available(const SceneView& s, bool coherent);
 bool launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4* hits, const int* count_dev,
                   int count_host, int max_count, int* fetch, int* gstack, int gstack_threads,
                   unsigned long long* counters, bool count, hipStream_t stream, int expect = 0,
                   int count_terms = 1, bool allow_group = true, bool coherent = false,
-                  const PrimaryGen* gen = nullptr);
+                  const PrimaryGen* gen = nullptr, const ShadeArgs* shade = nullptr);
 // events the next launch_trace records at its kernel's start / end (nullptr: none)
 void set_trace_events(hipEvent_t start, hipEvent_t stop);
 int trace_block_size();

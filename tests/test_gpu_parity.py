@@ -236,6 +236,45 @@ def test_bvh_layouts_bit_exact(gpu_ctx, avenger_scene, monkeypatch, builder, wid
         gpu_ctx.set_scene(avenger_scene)
 
 
+@pytest.mark.parametrize("fused,packets", [("0", "0"), ("1", "0"), ("2", "0"), ("2", "2"), ("3", "2"), ("3", "9"),
+                                            ("2", "-1")])
+def test_pipeline_modes_bit_exact(gpu_ctx, avenger_scene, monkeypatch, fused, packets):
+    """Every level-0 ray mode (k_raygen queue / regenerated in trace + shade / stored by the
+    packet traversal / traversal + shade fused) and every packet-traversal depth renders the
+    oracle's frame bit for bit, frames in flight and batched frames included."""
+    monkeypatch.setenv("PGRT_FUSED_RAYGEN", fused)
+    monkeypatch.setenv("PGRT_PACKET_LEVELS", packets)
+    try:
+        gpu_ctx.set_scene(avenger_scene)
+        W, H = 96, 64
+        cam = abi.default_camera(W, H)
+        gpu_ctx.set_camera(cam)
+        for p in (abi.make_params(spp_side=1, max_level=5),
+                  abi.make_params(spp_side=2, max_level=5, dof=1, jitter=abi.PGRT_JITTER_HASH, frame=3)):
+            img, _ = gpu_ctx.render(p)
+            ref, _ = _oracle(avenger_scene).render(cam, p)
+            _, exact = assert_frames_match(img, ref)
+            assert exact == 1.0
+        buf = gpu_ctx.alloc(3 * W * H * 16)
+        try:
+            gpu_ctx.set_frames_in_flight(2)
+            p = abi.make_params(spp_side=1, max_level=5, jitter=abi.PGRT_JITTER_HASH, frame=7)
+            gpu_ctx.render_wait(gpu_ctx.render_frames_device_async(p, 3, buf))
+            out = gpu_ctx.to_host(buf, (3, H, W, 4))
+            for f in range(3):
+                ref, _ = _oracle(avenger_scene).render(
+                    cam, abi.make_params(spp_side=1, max_level=5, jitter=abi.PGRT_JITTER_HASH, frame=7 + f))
+                _, exact = assert_frames_match(out[f], ref)
+                assert exact == 1.0, f"batched frame {f}"
+        finally:
+            gpu_ctx.set_frames_in_flight(1)
+            gpu_ctx.free(buf)
+    finally:
+        monkeypatch.delenv("PGRT_FUSED_RAYGEN")
+        monkeypatch.delenv("PGRT_PACKET_LEVELS")
+        gpu_ctx.set_scene(avenger_scene)
+
+
 def test_occluded_matches_closest_hit(gpu_ctx, avenger_scene):
     """rtcOccluded1 analogue: any hit in (tnear, tfar] exactly when the closest-hit query (oracle)
     finds one -- including finite-tfar shadow-style rays that stop short of the geometry."""
