@@ -43,8 +43,11 @@ RAY_BYTES, NODE_BYTES, WIDE_NODE_BYTES, TRI_BYTES = 48, 64, 80, 48
 # others are measured with --config and recorded in DESIGN.md / profiles/
 CONFIGS = {
     "C2": dict(width=1920, height=1080, max_level=5, spp_side=1, dof=0, scene="avenger"),
-    "C3": dict(width=1920, height=1080, max_level=5, spp_side=8, dof=1, scene="avenger"),
-    "C4": dict(width=3840, height=2160, max_level=5, spp_side=8, dof=1, scene="avenger"),
+    # heavy frames: rank 0's unpack is negligible next to its render share -> round-robin deal
+    "C3": dict(width=1920, height=1080, max_level=5, spp_side=8, dof=1, scene="avenger",
+               env={"PGRT_RANK0_SHARE": "8/8"}),
+    "C4": dict(width=3840, height=2160, max_level=5, spp_side=8, dof=1, scene="avenger",
+               env={"PGRT_RANK0_SHARE": "8/8"}),
     # C5: secondary rays in a triangle soup are incoherent, wave packets only at level 0
     # (r1g: packet levels 0 / 2 -> 23.1 / 26.2 ms/frame)
     "C5": dict(width=4096, height=4096, max_level=8, spp_side=1, dof=0, scene="random1m", in_flight=2,

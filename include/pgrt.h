@@ -226,11 +226,19 @@ int pgrt_intersect_closest(pgrt_ctx* ctx, const float* rays, int n, float* hits)
 int pgrt_occluded(pgrt_ctx* ctx, const float* rays, int n, int* occluded);
 
 /* ---- multi-GPU image tiles (one process per GPU, RCCL over xGMI) ----
- * Tiles are tile_size x tile_size, numbered row-major; tile t belongs to rank t % world. */
+ * Tiles are tile_size x tile_size, numbered row-major and dealt to ranks in rounds of
+ * a + b*(world-1) tiles: b sub-rounds of one tile per rank, rank 0 in only the first a of them
+ * (rank 0 also unpacks every gathered frame, so it renders a/b of another rank's share).
+ * pgrt_tile_share reports (a, b) for a world size (PGRT_RANK0_SHARE="a/b" overrides; a == b is
+ * the round-robin deal t -> rank t % world).  pgrt_tile_index maps local tile j of rank to its
+ * tile index (error past the rank's last tile); pgrt_tile_count is the rank's tile count. */
 int pgrt_tile_count(int width, int height, int tile_size, int rank, int world);
+int pgrt_tile_index(int width, int height, int tile_size, int rank, int world, int j);
+int pgrt_tile_share(int world, int* a, int* b);
 int pgrt_tile_rect(int width, int height, int tile_size, int tile_index, int rect[4]);
-/* Unpack a rank-major gathered tile buffer (every rank's tiles, each tile tile_size^2 * 4
- * floats, padded) into a W x H RGBA framebuffer.  Host reference of the device unpack. */
+/* Unpack a rank-major gathered tile buffer (every rank's tiles in its local order, each tile
+ * tile_size^2 * 4 floats, each rank's block padded to the longest rank list) into a W x H RGBA
+ * framebuffer.  Host reference of the device unpack. */
 int pgrt_unpack_tiles_host(int width, int height, int tile_size, int world,
                            const float* gathered, float* rgba);
 int pgrt_comm_unique_id(char id[128]);
@@ -238,7 +246,7 @@ int pgrt_comm_init(pgrt_ctx* ctx, int world, int rank, const char id[128]);
 /* Rank-local half of the distributed render, for callers that gather with their own
  * communicator: render the tiles of `rank` (of `world`) of the camera image into a tile-compact
  * device buffer of pgrt_tile_count(W, H, 64, rank, world) * 64 * 64 * 4 floats (local tile j is
- * global tile j * world + rank; edge tiles are padded). */
+ * tile pgrt_tile_index(W, H, 64, rank, world, j); edge tiles are padded). */
 int pgrt_render_tiles_device(pgrt_ctx* ctx, const pgrt_render_params* p, int rank, int world,
                              void* tiles_device, pgrt_stats* st);
 /* Render this rank's tiles, gather them on rank 0 with one ncclGather, unpack on device.

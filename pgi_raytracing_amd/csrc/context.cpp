@@ -17,6 +17,7 @@
 #include "trace.hpp"
 #include "camera_ops.hpp"
 #include "shade_ray.hpp"
+#include "tiles.hpp"
 
 using namespace pgrt;
 
@@ -995,11 +996,10 @@ void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
 void gather_frame(pgrt_ctx* ctx, FrameSet* fs) {
     const int W = fs->cam_w, H = fs->cam_h;
     const int total = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
-    const int per_rank = (total + ctx->world - 1) / ctx->world;
+    const int per_rank = deal_max_count(tile_deal(ctx->world), total);
     const int F = fs->nframes;
     const size_t tile_floats = (size_t)kTile * kTile * 3;  // RGB tiles (out_mode 2)
     const size_t block = (size_t)F * per_rank * tile_floats;  // one rank's frames, frame-major
-    const size_t frame_px = (size_t)W * H * 4;
     const float* src = nullptr;
     if (ctx->emulated) {
         ctx->gathered.alloc(block * ctx->world);
@@ -1017,10 +1017,8 @@ void gather_frame(pgrt_ctx* ctx, FrameSet* fs) {
         if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string("ncclGather: ") + ncclGetErrorString(r));
         src = ctx->rank == 0 ? ctx->gathered.p : nullptr;
     }
-    if (src)
-        for (int f = 0; f < F; ++f)
-            launch_unpack_tiles(src, fs->dist_fb + (size_t)f * frame_px, W, H, ctx->world, per_rank, 3, ctx->stream, F,
-                                f);
+    if (src)  // every frame of the call in one launch (grid.y = frame)
+        launch_unpack_tiles(src, fs->dist_fb, W, H, ctx->world, per_rank, 3, ctx->stream, F, 0, F);
     PGRT_HIP(hipGetLastError());
 }
 
@@ -1079,7 +1077,7 @@ void start_frame(pgrt_ctx* ctx, FrameSet* fs, const pgrt_render_params* p, std::
     if (distributed) {
         const int W = fs->cam_w, H = fs->cam_h;
         const int total = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
-        const int per_rank = (total + ctx->world - 1) / ctx->world;
+        const int per_rank = deal_max_count(tile_deal(ctx->world), total);
         // padded slots of the tile-compact buffer are never unpacked (t >= total); frame-major
         fs->tilebuf.alloc((size_t)nframes * per_rank * kTile * kTile * 3);
         fs->frame_out_tiles = per_rank;
@@ -1133,10 +1131,15 @@ void frame_rect(const pgrt_ctx* ctx, const pgrt_render_params* p, int& x, int& y
                  "render rect outside the camera image");
 }
 
+// rank's tiles in its local order (tiles.hpp deal)
 std::vector<int4> rank_tiles(int W, int H, int rank, int world) {
     std::vector<int4> all = rect_tiles(0, 0, W, H), mine;
-    for (size_t t = 0; t < all.size(); ++t)
-        if ((int)(t % world) == rank) mine.push_back(all[t]);
+    const TileDeal d = tile_deal(world);
+    for (int j = 0;; ++j) {
+        const int t = deal_tile(d, rank, j);
+        if (t >= (int)all.size()) break;
+        mine.push_back(all[t]);
+    }
     return mine;
 }
 
@@ -1382,7 +1385,23 @@ int pgrt_tile_count(int width, int height, int tile_size, int rank, int world) {
     if (width <= 0 || height <= 0 || tile_size <= 0 || world <= 0 || rank < 0 || rank >= world)
         return PGRT_ERR_INVALID_ARGUMENT;
     const long long total = (long long)((width + tile_size - 1) / tile_size) * ((height + tile_size - 1) / tile_size);
-    return (int)(total / world + (rank < total % world ? 1 : 0));
+    return deal_count(tile_deal(world), (int)total, rank);
+}
+
+int pgrt_tile_index(int width, int height, int tile_size, int rank, int world, int j) {
+    if (width <= 0 || height <= 0 || tile_size <= 0 || world <= 0 || rank < 0 || rank >= world || j < 0)
+        return PGRT_ERR_INVALID_ARGUMENT;
+    const int total = ((width + tile_size - 1) / tile_size) * ((height + tile_size - 1) / tile_size);
+    const int t = deal_tile(tile_deal(world), rank, j);
+    return t < total ? t : PGRT_ERR_INVALID_ARGUMENT;
+}
+
+int pgrt_tile_share(int world, int* a, int* b) {
+    if (world <= 0 || !a || !b) return PGRT_ERR_INVALID_ARGUMENT;
+    const TileDeal d = tile_deal(world);
+    *a = d.a;
+    *b = d.b;
+    return PGRT_OK;
 }
 
 int pgrt_tile_rect(int width, int height, int tile_size, int t, int rect[4]) {
@@ -1400,11 +1419,12 @@ int pgrt_unpack_tiles_host(int width, int height, int tile_size, int world, cons
     if (width <= 0 || height <= 0 || tile_size <= 0 || world <= 0 || !g || !rgba) return PGRT_ERR_INVALID_ARGUMENT;
     const int tx = (width + tile_size - 1) / tile_size, ty = (height + tile_size - 1) / tile_size;
     const int total = tx * ty;
-    const int per_rank = (total + world - 1) / world;
+    const TileDeal d = tile_deal(world);
+    const int per_rank = deal_max_count(d, total);
     const size_t tile_floats = (size_t)tile_size * tile_size * 4;
     for (int r = 0; r < world; ++r)
         for (int j = 0; j < per_rank; ++j) {
-            const int t = j * world + r;
+            const int t = deal_tile(d, r, j);
             if (t >= total) continue;
             const float* src = g + ((size_t)r * per_rank + j) * tile_floats;
             const int x0 = (t % tx) * tile_size, y0 = (t / tx) * tile_size;

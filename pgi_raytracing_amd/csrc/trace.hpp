@@ -132,7 +132,7 @@ void launch_accumulate_frame(const float* frame, float* sum, float* mean, long l
 void launch_export_counters(FrameCounters* dev, FrameCounters* host, int n, hipStream_t stream);
 // gathered: rank-major tile-compact buffers, `channels` floats per pixel (4: RGBA, 3: RGB + alpha 1)
 void launch_unpack_tiles(const float* gathered, float* rgba, int width, int height, int world, int tiles_per_rank,
-                         int channels, hipStream_t stream, int frames = 1, int frame = 0);
+                         int channels, hipStream_t stream, int frames = 1, int frame0 = 0, int nframes = 1);
 
 // scene / BVH build
 constexpr int kBuilderLbvh = 0;  // Karras 2012 over 63-bit Morton codes

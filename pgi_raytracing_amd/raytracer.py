@@ -68,6 +68,8 @@ def lib():
         "pgrt_render_frames_distributed_device_async": (ip, [vp, C.POINTER(abi.RenderParams), ip, vp,
                                                              C.POINTER(C.c_ulonglong)]),
         "pgrt_tile_count": (ip, [ip, ip, ip, ip, ip]),
+        "pgrt_tile_index": (ip, [ip, ip, ip, ip, ip, ip]),
+        "pgrt_tile_share": (ip, [ip, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "pgrt_tile_rect": (ip, [ip, ip, ip, ip, C.POINTER(C.c_int)]),
         "pgrt_unpack_tiles_host": (ip, [ip, ip, ip, ip, fp, fp]),
         "pgrt_comm_unique_id": (ip, [C.c_char_p]),

@@ -49,13 +49,49 @@ def test_argument_validation():
     assert L.pgrt_tile_count(100, 100, 64, 2, 2) == -1
 
 
-@pytest.mark.parametrize("W,H,world", [(1920, 1080, 8), (640, 480, 3), (100, 70, 2), (64, 64, 4)])
+def _deal_owner(world, a, b, t):
+    """Python restatement of the tile deal (pgi_raytracing_amd/csrc/tiles.hpp deal_owner)."""
+    if world <= 1:
+        return 0, t
+    R = a + b * (world - 1)
+    rnd, pos = divmod(t, R)
+    if pos < a * world:
+        sub, r = divmod(pos, world)
+        return r, rnd * (a if r == 0 else b) + sub
+    p2 = pos - a * world
+    return 1 + p2 % (world - 1), rnd * b + a + p2 // (world - 1)
+
+
+def _share(L, world):
+    a, b = C.c_int(), C.c_int()
+    assert L.pgrt_tile_share(world, C.byref(a), C.byref(b)) == 0
+    return a.value, b.value
+
+
+@pytest.mark.parametrize("W,H,world", [(1920, 1080, 8), (640, 480, 3), (100, 70, 2), (64, 64, 4), (1920, 1080, 1),
+                                       (3840, 2160, 8), (1920, 1080, 6)])
 def test_tile_plan_partitions_the_frame(W, H, world):
+    """Every tile has exactly one (rank, local index); pgrt_tile_index is the deal's inverse;
+    rank 0 holds about a/b of another rank's share, the other ranks within one tile of each other."""
     L = lib()
     tiles_x, tiles_y = -(-W // 64), -(-H // 64)
+    total = tiles_x * tiles_y
+    a, b = _share(L, world)
+    assert 1 <= a <= b
     counts = [L.pgrt_tile_count(W, H, 64, r, world) for r in range(world)]
-    assert sum(counts) == tiles_x * tiles_y
-    assert max(counts) - min(counts) <= 1
+    assert sum(counts) == total
+    if world > 1:
+        assert max(counts[1:]) - min(counts[1:]) <= 1
+        assert abs(counts[0] - counts[1] * a / b) <= b
+    owner = {}
+    for r in range(world):
+        for j in range(counts[r]):
+            t = L.pgrt_tile_index(W, H, 64, r, world, j)
+            assert 0 <= t < total and t not in owner
+            owner[t] = (r, j)
+            assert _deal_owner(world, a, b, t) == (r, j)
+        assert L.pgrt_tile_index(W, H, 64, r, world, counts[r]) < 0  # past the rank's last tile
+    assert len(owner) == total
     cover = np.zeros((H, W), np.int32)
     rect = (C.c_int * 4)()
     for t in range(tiles_x * tiles_y):
@@ -65,18 +101,20 @@ def test_tile_plan_partitions_the_frame(W, H, world):
     assert (cover == 1).all()
 
 
-@pytest.mark.parametrize("W,H,world", [(200, 130, 3), (64, 64, 1), (130, 70, 4)])
+@pytest.mark.parametrize("W,H,world", [(200, 130, 3), (64, 64, 1), (130, 70, 4), (700, 500, 8)])
 def test_unpack_tiles_host(W, H, world):
-    """Rank-major gathered tiles (tile t on rank t % world) reassemble into the frame."""
+    """Rank-major gathered tiles (the deal's local order, blocks padded to the longest rank list)
+    reassemble into the frame."""
     L = lib()
     T = 64
     tx, ty = -(-W // T), -(-H // T)
     total = tx * ty
-    per_rank = -(-total // world)
+    a, b = _share(L, world)
+    per_rank = max(L.pgrt_tile_count(W, H, T, r, world) for r in range(world))
     frame = np.random.default_rng(0).random((H, W, 4), dtype=np.float32)
     g = np.zeros((world, per_rank, T, T, 4), np.float32)
     for t in range(total):
-        r, j = t % world, t // world
+        r, j = _deal_owner(world, a, b, t)
         x0, y0 = (t % tx) * T, (t // tx) * T
         blk = frame[y0:y0 + T, x0:x0 + T]
         g[r, j, :blk.shape[0], :blk.shape[1]] = blk

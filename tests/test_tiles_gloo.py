@@ -1,7 +1,7 @@
 """Multi-GPU path on CPU: world_size 2 over gloo.
 
-Each rank renders the 64x64 tiles it owns (tile t -> rank t % world, the plan of
-pgrt_tile_count / pgrt_tile_rect) into a tile-compact buffer, the buffers are gathered on rank 0
+Each rank renders the 64x64 tiles it owns (the deal of pgrt_tile_count / pgrt_tile_index /
+pgrt_tile_rect: rank 0 takes a smaller share, it also unpacks) into a tile-compact buffer, the buffers are gathered on rank 0
 (gloo standing in for libpgrt's ncclGather) and unpacked with pgrt_unpack_tiles_host; the result
 must equal a single-process full-frame render bit for bit.  The per-tile renders use the CPU
 restatement (no GPU here); the device path runs the same plan (tests/test_gpu_parity.py)."""
@@ -44,12 +44,11 @@ def _worker(rank, world, port, obj, env, q):
     sc.set_environment(env)
     osc = pyoracle.OracleScene(sc)
     cam = abi.default_camera(W, H)
-    total = -(-W // T) * -(-H // T)
-    per_rank = -(-total // world)
-    assert L.pgrt_tile_count(W, H, T, rank, world) == len(range(rank, total, world))
+    per_rank = max(L.pgrt_tile_count(W, H, T, r, world) for r in range(world))
+    mine = [L.pgrt_tile_index(W, H, T, rank, world, j) for j in range(L.pgrt_tile_count(W, H, T, rank, world))]
     buf = np.zeros((per_rank, T, T, 4), np.float32)
     rect = (C.c_int * 4)()
-    for j, t in enumerate(range(rank, total, world)):
+    for j, t in enumerate(mine):
         L.pgrt_tile_rect(W, H, T, t, rect)
         x, y, w, h = rect
         img, _ = osc.render(cam, abi.make_params(max_level=5, spp_side=2, jitter=abi.PGRT_JITTER_HASH,
