@@ -44,9 +44,11 @@ RAY_BYTES, NODE_BYTES, WIDE_NODE_BYTES, TRI_BYTES = 48, 64, 80, 48
 CONFIGS = {
     "C2": dict(width=1920, height=1080, max_level=5, spp_side=1, dof=0, scene="avenger"),
     # heavy frames: rank 0's unpack is negligible next to its render share -> round-robin deal
-    "C3": dict(width=1920, height=1080, max_level=5, spp_side=8, dof=1, scene="avenger",
+    # (and 2 frames in flight: r1g/r1h C3 13.3-13.5 ms at 6 in flight but one run in three at 50 ms,
+    # 14.8 ms at 2, stable)
+    "C3": dict(width=1920, height=1080, max_level=5, spp_side=8, dof=1, scene="avenger", in_flight=2,
                env={"PGRT_RANK0_SHARE": "8/8"}),
-    "C4": dict(width=3840, height=2160, max_level=5, spp_side=8, dof=1, scene="avenger",
+    "C4": dict(width=3840, height=2160, max_level=5, spp_side=8, dof=1, scene="avenger", in_flight=2,
                env={"PGRT_RANK0_SHARE": "8/8"}),
     # C5: secondary rays in a triangle soup are incoherent, wave packets only at level 0
     # (r1g: packet levels 0 / 2 -> 23.1 / 26.2 ms/frame)

@@ -52,6 +52,11 @@ void launch_raygen(const CameraView& cam, const FrameParams& fp, const int4* til
 // LDS_TABLES: the material and texture-descriptor tables are copied to LDS per block
 // (kLdsMats / kLdsTex, shade_ray.hpp)
 
+// k_shade: the hit triangle's attributes loaded one ray ahead (A/B switch; r1h: 0.1982 vs
+// 0.2000 ms/frame without / with -- off)
+#ifndef PGRT_ATTR_PREFETCH
+#define PGRT_ATTR_PREFETCH 0
+#endif
 // k_shade block size (one allocation atomic per block and iteration, shade_ray.hpp; r1f A/B:
 // 256 beat 512 and 1024)
 #ifndef PGRT_SHADE_BLOCK
@@ -101,6 +106,9 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(SceneView s, FrameParams 
             nx_h = q.hit[i0];
         }
     }
+#if PGRT_ATTR_PREFETCH
+    HitAttr nx_a = load_attr(s, nx_h);
+#endif
     for (int base_i = blockIdx.x * kShadeBlock; base_i < n; base_i += stride) {
         const int i = base_i + tid;
         const bool active = i < n;
@@ -119,7 +127,15 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(SceneView s, FrameParams 
             if (active) cur_t = primary_ray(gen.cam, gen.fp, gen.tiles, i, cur_o, cur_d) ? PGRT_IOR_AIR : 0.0f;
         }
         ShadeOut r;
+#if PGRT_ATTR_PREFETCH
+        // the next ray's attributes are requested before this ray's allocation round trip (its
+        // hit arrived during this ray's shading), so the next hit -> attribute hop overlaps it
+        const HitAttr cur_a = nx_a;
+        shade_eval(s, mats, lut255, level, fp.max_level, active, cur_o, cur_d, cur_t, cur_h, r, &cur_a);
+        if (i + stride < n) nx_a = load_attr(s, nx_h);
+#else
         shade_eval(s, mats, lut255, level, fp.max_level, active, cur_o, cur_d, cur_t, cur_h, r);
+#endif
         const ShadeSlots sl = shade_alloc<kShadeBlock>(alds, it_par, fc, level, sq_base, sbits, r);
         if (active) shade_emit(s, mats, level, i, r, sl, next, nodes, sq, fc);
     }

@@ -59,10 +59,30 @@ struct ShadeOut {
     float m_d_r, m_d_g, m_d_b;
 };
 
-// Phase 1 for one ray (o4 = org|tnear, d4 = dir|tfar, rtime = medium IOR, h = t|u|v|prim).
+// the hit triangle's 16 shading floats (n0 n1 n2 uv0 uv1 uv2 material), 4 x 16 B
+struct HitAttr {
+    float4 q[4];
+};
+__device__ __forceinline__ HitAttr load_attr(const SceneView& s, float4 h) {
+    HitAttr a;
+    const int prim = __float_as_int(h.w);
+    if (prim >= 0) {
+        const float4* p = reinterpret_cast<const float4*>(s.attr + 16 * (size_t)prim);
+        a.q[0] = p[0];
+        a.q[1] = p[1];
+        a.q[2] = p[2];
+        a.q[3] = p[3];
+    } else {
+        a.q[0] = a.q[1] = a.q[2] = a.q[3] = make_float4(0, 0, 0, 0);
+    }
+    return a;
+}
+
+// Phase 1 for one ray (o4 = org|tnear, d4 = dir|tfar, rtime = medium IOR, h = t|u|v|prim); pa:
+// the hit's attributes when already loaded (k_shade prefetches them one ray ahead), else NULL.
 __device__ __forceinline__ void shade_eval(const SceneView& s, const DevMaterial* mats, const float* lut,
                                            int level, int max_level, bool active, float4 o4, float4 d4,
-                                           float rtime, float4 h, ShadeOut& r) {
+                                           float rtime, float4 h, ShadeOut& r, const HitAttr* pa = nullptr) {
     r.kind = 0;
     r.color = make_float4(0, 0, 0, 1);
     r.nshadow = 0;
@@ -86,7 +106,8 @@ __device__ __forceinline__ void shade_eval(const SceneView& s, const DevMaterial
         return;
     }
     const float t = h.x;
-    const float* a = s.attr + 16 * (size_t)prim;
+    const HitAttr ha = pa ? *pa : load_attr(s, h);
+    const float* a = reinterpret_cast<const float*>(ha.q);
     const float u = h.y, v = h.z;
     V3 nn = v3(interp1(a[0], a[3], a[6], u, v), interp1(a[1], a[4], a[7], u, v), interp1(a[2], a[5], a[8], u, v));
     r.mid = __float_as_int(a[15]);
