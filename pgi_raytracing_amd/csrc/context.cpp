@@ -593,7 +593,9 @@ void ensure_frame_buffers(FrameSlot* sl, int n0, int levels, int nlight, int bat
     }
     if (sl->fc.n < (size_t)batches) {  // zeroed once; every frame's export kernel re-zeroes them
         sl->fc.alloc((size_t)batches);
-        PGRT_HIP(hipMemset(sl->fc.p, 0, sizeof(FrameCounters) * batches));
+        // on the slot's own (non-blocking) stream, ahead of the frame's kernels: a NULL-stream
+        // hipMemset is not ordered with them and could zero a running frame's queue counters
+        PGRT_HIP(hipMemsetAsync(sl->fc.p, 0, sizeof(FrameCounters) * batches, sl->stream));
     }
     if (sl->gstack.n == 0) sl->gstack.alloc((size_t)kTraceGridThreads * kGlobalStack);
 }
