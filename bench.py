@@ -44,15 +44,14 @@ RAY_BYTES, NODE_BYTES, WIDE_NODE_BYTES, TRI_BYTES = 48, 64, 80, 48
 CONFIGS = {
     "C2": dict(width=1920, height=1080, max_level=5, spp_side=1, dof=0, scene="avenger"),
     # heavy frames: rank 0's unpack is negligible next to its render share -> round-robin deal
-    # (and 2 frames in flight: r1g/r1h C3 13.3-13.5 ms at 6 in flight but one run in three at 50 ms,
-    # 14.8 ms at 2, stable)
-    "C3": dict(width=1920, height=1080, max_level=5, spp_side=8, dof=1, scene="avenger", in_flight=2,
+    # (r1h after the counter-zeroing fix: C3 14.4 / 15.0 / 12.6 ms at 2 / 4 / 6 in flight)
+    "C3": dict(width=1920, height=1080, max_level=5, spp_side=8, dof=1, scene="avenger",
                env={"PGRT_RANK0_SHARE": "8/8"}),
     "C4": dict(width=3840, height=2160, max_level=5, spp_side=8, dof=1, scene="avenger", in_flight=2,
                env={"PGRT_RANK0_SHARE": "8/8"}),
     # C5: secondary rays in a triangle soup are incoherent, wave packets only at level 0
-    # (r1g: packet levels 0 / 2 -> 23.1 / 26.2 ms/frame)
-    "C5": dict(width=4096, height=4096, max_level=8, spp_side=1, dof=0, scene="random1m", in_flight=2,
+    # (r1g: packet levels 0 / 2 -> 23.1 / 26.2 ms/frame); r1h: 23.4 / 23.8 / 22.3 ms at 2 / 4 / 6 in flight
+    "C5": dict(width=4096, height=4096, max_level=8, spp_side=1, dof=0, scene="random1m",
                env={"PGRT_PACKET_LEVELS": "0"}),
 }
 
@@ -138,8 +137,8 @@ def main():
     # frames in flight: a step is one whole frame (every rank's tiles rendered, gathered and
     # unpacked on rank 0); up to `in_flight` consecutive frames overlap on the device, so one
     # frame's latency-bound deep levels share the CUs with the next frame's wide levels
-    # (C5: 2 -- r1g scan 26.1 / 23.5 / 25.2 ms at 1 / 2 / 3, and 175 ms at 6: its 16.7 M-ray
-    # frames with 9 levels of queues per frame set thrash the memory system)
+    # (r1g measured C5 at 175 ms/frame with 6 in flight: a new frame set's counters were zeroed
+    # by a NULL-stream hipMemset racing the slot streams, fixed in r1h)
     in_flight = args.in_flight or CONFIGS[args.config].get("in_flight", 6)
     ctx.set_frames_in_flight(in_flight)
 

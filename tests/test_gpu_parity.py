@@ -368,6 +368,30 @@ def test_batched_frames_match_single(gpu_ctx, avenger_scene):
             gpu_ctx.free(dbuf)
 
 
+def test_new_frame_sets_start_clean(avenger_scene):
+    """Regression (r1h): the first frame on each new frame set must see zeroed queue counters
+    -- they were zeroed by a NULL-stream hipMemset, unordered with the slot streams, and a set's
+    first frame could lose its secondary rays.  A fresh context, 6 sets, 720p frames."""
+    from pgi_raytracing_amd.raytracer import Context
+
+    ctx = Context(0)
+    try:
+        ctx.set_scene(avenger_scene)
+        W, H = 1280, 720
+        ctx.set_camera(abi.default_camera(W, H))
+        p = abi.make_params(max_level=5)
+        _, st_ref = ctx.render(p)
+        fb = ctx.alloc(W * H * 16)
+        ctx.set_frames_in_flight(6)
+        tickets = [ctx.render_device_async(p, fb) for _ in range(6)]
+        for t in tickets:
+            st = ctx.render_wait(t)
+            assert st.rays() == st_ref.rays() and st.rays_shadow == st_ref.rays_shadow
+        ctx.free(fb)
+    finally:
+        ctx.close()
+
+
 def test_frames_in_flight_match_synchronous(gpu_ctx, avenger_scene):
     """Asynchronous frames (3 in flight, different depth / spp / DoF / seed per frame, the
     distributed form included) are bit-identical to synchronous renders; a recycled ticket is
