@@ -59,7 +59,9 @@ CONFIGS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)  # ~0.15 s of frames: stable clocks, +-3 %
+    # frames timed; default 200 x world (N GPUs batch 8 x N frames per call: 25 calls either way,
+    # so the pipeline of calls in flight reaches steady state at every N)
+    ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--width", type=int, default=None)
@@ -88,6 +90,8 @@ def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if args.steps is None:
+        args.steps = 200 * world
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
