@@ -230,7 +230,8 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None,
-            "kernel": "closest hit: k_trace (binary BVH, big queues) + k_trace8g (8 lanes/ray, small queues)",
+            "kernel": "closest hit: k_trace_pkt (wave packets, levels 0-2; level 0 generates its rays) + k_trace "
+                      "(one lane per ray, levels 3-5 and the shadow queue)",
             "avg_launch_ms": round(avg_launch_ms, 4),
             "frames_per_launch": frames_per_prof,
             "launches_per_call": launches // reps,
