@@ -368,6 +368,35 @@ def test_batched_frames_match_single(gpu_ctx, avenger_scene):
             gpu_ctx.free(dbuf)
 
 
+def test_full_size_c2_batched_bit_exact(gpu_ctx, avenger_scene):
+    """BASELINE C2 at its full size through the bench's path (batched frames, frames in flight,
+    packets on levels 0-2, block-level queue allocation): every pixel of both frames of a
+    2-frame call equals the CPU restatement's frame bit for bit; plus a 2x2-spp DoF frame."""
+    gpu_ctx.set_scene(avenger_scene)
+    W, H = 1920, 1080
+    cam = abi.default_camera(W, H)
+    gpu_ctx.set_camera(cam)
+    p = abi.make_params(max_level=5)
+    ref, st_ref = _oracle(avenger_scene).render(cam, p, threads=16)
+    buf = gpu_ctx.alloc(2 * W * H * 16)
+    try:
+        gpu_ctx.set_frames_in_flight(6)
+        st = gpu_ctx.render_wait(gpu_ctx.render_frames_device_async(p, 2, buf))
+        assert st.rays() == 2 * st_ref.rays()
+        out = gpu_ctx.to_host(buf, (2, H, W, 4))
+        for f in range(2):
+            _, exact = assert_frames_match(out[f], ref)
+            assert exact == 1.0, f"frame {f}"
+    finally:
+        gpu_ctx.set_frames_in_flight(1)
+        gpu_ctx.free(buf)
+    q = abi.make_params(max_level=5, spp_side=2, dof=1, jitter=abi.PGRT_JITTER_HASH, frame=5)
+    img, _ = gpu_ctx.render(q)
+    ref2, _ = _oracle(avenger_scene).render(cam, q, threads=16)
+    _, exact = assert_frames_match(img, ref2)
+    assert exact == 1.0
+
+
 def test_new_frame_sets_start_clean(avenger_scene):
     """Regression (r1h): the first frame on each new frame set must see zeroed queue counters
     -- they were zeroed by a NULL-stream hipMemset, unordered with the slot streams, and a set's
