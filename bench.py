@@ -28,7 +28,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 # one hardware queue per frame in flight (+ the context stream): HIP's default of 4 would make
 # frames share queues; read by the HIP runtime at its initialisation, i.e. before libpgrt loads
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# (r1i C2, 8 frames per call: 8 queues / 6 in flight 0.197 ms; 12 / 6 0.191; 12 / 8 0.186;
+# 16 / 8-14 0.185-0.187)
+# (the GPU boxes export GPU_MAX_HW_QUEUES=4, HIP's default: raise it, a setdefault would not)
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 METRIC = "Mrays/sec + ms/frame, avenger 1920x1080 Whitted d=5, 1/2/4/8 GPU"
@@ -42,7 +46,7 @@ RAY_BYTES, NODE_BYTES, WIDE_NODE_BYTES, TRI_BYTES = 48, 64, 80, 48
 # BASELINE.json configs (SURVEY.md §8d "Concrete inputs"); C2 is the headline bench line, the
 # others are measured with --config and recorded in DESIGN.md / profiles/
 CONFIGS = {
-    "C2": dict(width=1920, height=1080, max_level=5, spp_side=1, dof=0, scene="avenger"),
+    "C2": dict(width=1920, height=1080, max_level=5, spp_side=1, dof=0, scene="avenger", in_flight=8),
     # heavy frames: rank 0's unpack is negligible next to its render share -> round-robin deal
     # (r1h after the counter-zeroing fix: C3 14.4 / 15.0 / 12.6 ms at 2 / 4 / 6 in flight)
     "C3": dict(width=1920, height=1080, max_level=5, spp_side=8, dof=1, scene="avenger",
@@ -59,8 +63,9 @@ CONFIGS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # frames timed; default 200 x world (N GPUs batch 8 x N frames per call: 25 calls either way,
-    # so the pipeline of calls in flight reaches steady state at every N)
+    # frames timed; default 600 x world (N GPUs batch 8 x N frames per call: 75 calls either way,
+    # ~10x the 8 calls in flight, so pipeline fill and drain stay a small part of the timed region
+    # at every N; r1i C2: 200 frames 0.207 ms/frame, 960 frames 0.186)
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
@@ -91,7 +96,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if args.steps is None:
-        args.steps = 200 * world
+        args.steps = 600 * world
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:

@@ -190,7 +190,7 @@ int pgrt_render_accumulate(pgrt_ctx* ctx, const pgrt_render_params* p, float* me
 
 /* ---- frames in flight (asynchronous frames) ----
  * pgrt_render_device_async enqueues a frame and returns at once with a ticket; up to n frames
- * (pgrt_set_frames_in_flight, 1..8, default 1) run concurrently, each on its own pipeline
+ * (pgrt_set_frames_in_flight, 1..16, default 1) run concurrently, each on its own pipeline
  * streams, so one frame's latency-bound deep Whitted levels overlap the next frame's wide levels.
  * Submitting when n frames are pending first completes the oldest.  pgrt_render_wait(ticket)
  * completes every frame up to that ticket and returns its statistics (ms_total = submit to

@@ -25,7 +25,7 @@ namespace {
 
 constexpr long long kMaxBatchRays = 16ll << 20;  // level-0 rays per sample batch
 constexpr int kTraceGridThreads = 2048 * 256;    // persistent trace grid (global overflow stacks)
-constexpr int kMaxFramesInFlight = 8;
+constexpr int kMaxFramesInFlight = 16;
 // sample batches queued on the device across all frames in flight (each batch is ~3 launches per
 // level): a frame is submitted only when the pending frames leave room for its batches (the
 // oldest pending frames complete first).  C4 on one GPU (32 batches per frame) faulted with 6

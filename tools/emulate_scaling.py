@@ -75,7 +75,7 @@ def main():
     t1 = None
     for n in worlds:
         for r in sorted({0, n - 1}):
-            env = dict(os.environ, EMU_CHILD="1", PGRT_EMULATE_RANK=f"{r}/{n}", GPU_MAX_HW_QUEUES="8")
+            env = dict(os.environ, EMU_CHILD="1", PGRT_EMULATE_RANK=f"{r}/{n}", GPU_MAX_HW_QUEUES="16")
             out = subprocess.run([sys.executable, __file__, str(frames), str(in_flight)], env=env, check=True,
                                  capture_output=True, text=True, timeout=300).stdout
             d = json.loads(out.strip().splitlines()[-1])

@@ -7,7 +7,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "tools")]
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+os.environ["GPU_MAX_HW_QUEUES"] = "16"
 import bench  # noqa: E402
 import scenes  # noqa: E402
 from pgi_raytracing_amd import abi  # noqa: E402
