@@ -15,7 +15,7 @@ all: $(LIBDIR)/libpgrt.so oracle $(BUILD)/pg1_pgrt
 $(BUILD) $(LIBDIR):
 	mkdir -p $@
 
-HDRS := include/pgrt.h include/pgrt_detmath.h $(SRC)/common.hpp $(SRC)/trace.hpp $(SRC)/shade_ops.hpp $(SRC)/camera_ops.hpp $(SRC)/shade_ray.hpp
+HDRS := include/pgrt.h include/pgrt_detmath.h $(SRC)/common.hpp $(SRC)/trace.hpp $(SRC)/shade_ops.hpp $(SRC)/camera_ops.hpp $(SRC)/shade_ray.hpp $(SRC)/tiles.hpp
 
 $(BUILD)/%.o: $(SRC)/%.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@

@@ -6,7 +6,7 @@
 // the framebuffer (≈ 10 µs per 1080p frame, ≈ 5 % of a C2 frame's render): with a < b the ranks
 // finish together.  a == b is the plain round-robin deal (tile t -> rank t % world).
 // The share is process-wide: PGRT_RANK0_SHARE="a/b" (1 <= a <= b <= 64), else a default by world
-// size from the C2 measurements.
+// size from the C2 measurements: 8/8 at 1-2 GPUs, 7/8 at 3-4, 6/8 at 5-7, 5/8 at 8+.
 #pragma once
 
 #include <cstdlib>
@@ -30,10 +30,14 @@ inline TileDeal tile_deal(int world) {
         d.a = env_a / 100;
         d.b = env_a % 100;
     } else if (world >= 8) {
-        d.a = 5;  // optimum share (1 - (W-1) u) / (1 + u), u = unpack / frame render = 0.046
+        // r1j emulated C2 ranks (tools/emulate_scaling.py, slowest rank ms/frame): 8 GPUs 5/8
+        // 0.025 vs 4/8 0.027 (a round of 60 tiles = two rows of 30 puts every rank on fixed
+        // columns, one of them over the canopy), 4 GPUs 7/8 0.054 vs 6/8 0.057, 2 GPUs 8/8
+        // 0.100 vs 7/8 0.105
+        d.a = 5;
     } else if (world >= 5) {
         d.a = 6;
-    } else if (world >= 2) {
+    } else if (world >= 3) {
         d.a = 7;
     }
     if (world <= 1) d.a = d.b = 1;
