@@ -47,16 +47,11 @@ RAY_BYTES, NODE_BYTES, WIDE_NODE_BYTES, TRI_BYTES = 48, 64, 80, 48
 # others are measured with --config and recorded in DESIGN.md / profiles/
 CONFIGS = {
     "C2": dict(width=1920, height=1080, max_level=5, spp_side=1, dof=0, scene="avenger", in_flight=8),
-    # heavy frames: rank 0's unpack is negligible next to its render share -> round-robin deal
     # (r1h after the counter-zeroing fix: C3 14.4 / 15.0 / 12.6 ms at 2 / 4 / 6 in flight)
-    "C3": dict(width=1920, height=1080, max_level=5, spp_side=8, dof=1, scene="avenger",
-               env={"PGRT_RANK0_SHARE": "8/8"}),
-    "C4": dict(width=3840, height=2160, max_level=5, spp_side=8, dof=1, scene="avenger", in_flight=2,
-               env={"PGRT_RANK0_SHARE": "8/8"}),
-    # C5: secondary rays in a triangle soup are incoherent, wave packets only at level 0
-    # (r1g: packet levels 0 / 2 -> 23.1 / 26.2 ms/frame); r1h: 23.4 / 23.8 / 22.3 ms at 2 / 4 / 6 in flight
-    "C5": dict(width=4096, height=4096, max_level=8, spp_side=1, dof=0, scene="random1m",
-               env={"PGRT_PACKET_LEVELS": "0"}),
+    "C3": dict(width=1920, height=1080, max_level=5, spp_side=8, dof=1, scene="avenger"),
+    "C4": dict(width=3840, height=2160, max_level=5, spp_side=8, dof=1, scene="avenger"),
+    # r1h: 23.4 / 23.8 / 22.3 ms at 2 / 4 / 6 in flight
+    "C5": dict(width=4096, height=4096, max_level=8, spp_side=1, dof=0, scene="random1m"),
 }
 
 
@@ -107,8 +102,6 @@ def main():
     from pgi_raytracing_amd import abi
     from pgi_raytracing_amd.raytracer import Context, load_obj
 
-    for k, v in CONFIGS[args.config].get("env", {}).items():  # per-workload libpgrt knobs
-        os.environ.setdefault(k, v)
     env = os.path.join(ROOT, "assets", "spherical_map_windows.jpg")
     if args.scene == "avenger":
         if rank == 0 and not os.path.exists(scenes.AVENGER_OBJ):

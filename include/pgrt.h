@@ -148,12 +148,34 @@ typedef struct pgrt_bvh_info {
     double build_ms;
     float scene_lo[3], scene_hi[3];
     size_t device_bytes;
-    int builder;          /* 0 Karras LBVH, 1 PLOC over the Morton order (default) */
+    int builder;          /* PGRT_BVH_LBVH or PGRT_BVH_PLOC (default) */
     int build_iterations; /* PLOC merge iterations */
     int width;            /* traversal layout: 2 (binary, default) or 8 (quantized 8-wide) */
     int num_references;   /* BVH leaf entries: triangles plus early-split-clipping duplicates */
     float split_beta;     /* split budget used (extra references / triangles), 0 = off */
 } pgrt_bvh_info;
+
+/* Context configuration (pgrt_get_config / pgrt_set_config).  Every choice here changes speed
+ * only: frames and hit records are bit-identical for every value (the closest hit is
+ * order-independent, tests/test_gpu_parity.py).  Zero-initialised fields mean "default". */
+#define PGRT_BVH_LBVH 1           /* Karras 2012 LBVH over 63-bit Morton codes */
+#define PGRT_BVH_PLOC 2           /* PLOC clustering over the Morton order + SAH leaf collapse */
+#define PGRT_PACKETS_AUTO 0       /* per level, from the measured packet efficiency (default) */
+#define PGRT_PACKETS_OFF (-1)     /* every level one lane per ray */
+typedef struct pgrt_config {
+    int bvh_builder;      /* 0 = PGRT_BVH_PLOC (default), PGRT_BVH_LBVH; applied by pgrt_set_scene */
+    int bvh_width;        /* 0 or 2: binary traversal layout (default); 8: quantized 8-wide for
+                             every queue.  The 8-wide layout is always built for small queues. */
+    float split_beta;     /* early split clipping budget (extra references / triangles), 0 off */
+    int packet_levels;    /* PGRT_PACKETS_AUTO, PGRT_PACKETS_OFF, or k >= 1: levels 0..k-1 traced
+                             as wave packets, deeper levels one lane per ray */
+    int group_max;        /* queues of <= group_max rays: 8 lanes per ray over the 8-wide BVH;
+                             0 = default (400k synchronous, 100k with frames in flight), -1 never */
+    long long max_batch_rays;  /* level-0 rays per sample batch (0 = 16M); smaller values split a
+                                  frame's samples into more batches (queue memory vs launches) */
+    int max_batches_in_flight; /* sample batches queued across frames in flight (0 = no bound) */
+    int reserved[5];
+} pgrt_config;
 
 /* ---- context ---- */
 const char* pgrt_version(void);
@@ -161,6 +183,10 @@ int pgrt_device_count(int* count);
 int pgrt_create(int hip_device, pgrt_ctx** out);
 void pgrt_destroy(pgrt_ctx* ctx);
 const char* pgrt_last_error(const pgrt_ctx* ctx);
+/* The BVH fields take effect at the next pgrt_set_scene, the others at the next frame
+ * (pending frames complete first). */
+int pgrt_get_config(const pgrt_ctx* ctx, pgrt_config* cfg);
+int pgrt_set_config(pgrt_ctx* ctx, const pgrt_config* cfg);
 
 /* ---- scene / camera (replaces Raytracer::LoadScene's Embree upload, raytracer.cpp:71-127,
  *      and the PinHoleCamera ctor, PinHoleCamera.cpp:5-29) ---- */

@@ -108,6 +108,24 @@ class RenderParams(C.Structure):
     ]
 
 
+PGRT_BVH_LBVH, PGRT_BVH_PLOC = 1, 2
+PGRT_PACKETS_AUTO, PGRT_PACKETS_OFF = 0, -1
+
+
+class Config(C.Structure):
+    """pgrt_config: speed-only choices (frames are bit-identical for every value)."""
+    _fields_ = [
+        ("bvh_builder", C.c_int),
+        ("bvh_width", C.c_int),
+        ("split_beta", C.c_float),
+        ("packet_levels", C.c_int),
+        ("group_max", C.c_int),
+        ("max_batch_rays", C.c_longlong),
+        ("max_batches_in_flight", C.c_int),
+        ("reserved", C.c_int * 5),
+    ]
+
+
 class Stats(C.Structure):
     _fields_ = [
         ("rays_primary", C.c_uint64),

@@ -1,7 +1,7 @@
-// camera_ops.hpp -- primary ray of a sample-batch slot, shared by k_raygen, the level-0 packet
-// traversal and the level-0 shade (which regenerate the ray in registers instead of reading a
-// ray queue, see DESIGN.md "fused primary rays").  Same float operation order everywhere, so a
-// regenerated ray is bit-identical to the one k_raygen stores.
+// camera_ops.hpp -- primary ray of a sample-batch slot, shared by k_raygen and the level-0 packet
+// traversal (which generates the ray in registers and stores it for the level-0 shade, see
+// DESIGN.md "fused primary rays").  Same float operation order in both, so the rays are
+// bit-identical.
 #pragma once
 
 #include "shade_ops.hpp"
@@ -88,8 +88,8 @@ struct PrimaryGen {
     CameraView cam;
     FrameParams fp;
     const int4* tiles;
-    // when set, the packet traversal stores the rays it generated (k_raygen's queue layout) for a
-    // level-0 shade that reads them instead of regenerating
+    // the packet traversal stores the rays it generated (k_raygen's queue layout) for the
+    // level-0 shade
     float4* store_ro;
     float4* store_rd;
     float* store_time;

@@ -23,15 +23,9 @@ using namespace pgrt;
 
 namespace {
 
-constexpr long long kMaxBatchRays = 16ll << 20;  // level-0 rays per sample batch
+constexpr long long kMaxBatchRays = 16ll << 20;  // level-0 rays per sample batch (pgrt_config default)
 constexpr int kTraceGridThreads = 2048 * 256;    // persistent trace grid (global overflow stacks)
 constexpr int kMaxFramesInFlight = 16;
-// sample batches queued on the device across all frames in flight (each batch is ~3 launches per
-// level): a frame is submitted only when the pending frames leave room for its batches (the
-// oldest pending frames complete first).  C4 on one GPU (32 batches per frame) faulted with 6
-// frames = ~3800 launches queued at once and ran clean with 2 (r1d); frames of one or a few
-// batches (C2, C3) are unaffected.
-constexpr int kMaxBatchesInFlight = 64;
 constexpr int kMaxFramesPerCall = 64;
 
 struct StageTimer {
@@ -104,28 +98,16 @@ enum { CAT_RAYGEN, CAT_TRACE, CAT_SHADE, CAT_SHADOW, CAT_COMBINE, CAT_LTRACE, CA
 }  // namespace
 
 namespace pgrt {
-// byte signature of the host-side arguments of a captured launch sequence
-struct Signature {
-    std::vector<unsigned char> v;
-    void add_bytes(const void* p, size_t n) {
-        const unsigned char* b = static_cast<const unsigned char*>(p);
-        v.insert(v.end(), b, b + n);
-    }
-    template <class T>
-    void add(const T& x) {
-        add_bytes(&x, sizeof(T));
-    }
-};
 
 // One pipeline instance: queues, level nodes, shadow queue and counters for a subset of the
 // frame's tiles, enqueued on its own stream.  Two slots run concurrently: each launch of one
 // slot fills the CUs the other slot's latency-bound launches leave idle (the tail of every
-// level, the deep Whitted levels).  r1 A/B on C2 (tools/ab_slots.sh): 1 slot 0.87 ms, 2 slots
-// 0.79-0.80, 3 slots 0.80, 4+ slots slower (more streams than the 4 hardware queues); a stagger
-// (slot k+1 waits for slot k's level 0, PGRT_STAGGER_LEVEL) was slower (0.90).
+// level, the deep Whitted levels).  r1 A/B on C2: 1 slot 0.87 ms, 2 slots 0.79-0.80, 3 slots
+// 0.80, 4+ slots slower (more streams than the 4 hardware queues); a stagger (slot k+1 waits for
+// slot k's level 0) was slower (0.90).
 struct FrameSlot {
     hipStream_t stream = nullptr;
-    hipEvent_t ev_stagger = nullptr, ev_done = nullptr;
+    hipEvent_t ev_done = nullptr;
     DevBuf<int4> tiles;
     DevBuf<float4> q_ro[2], q_rd[2], q_hit[2];
     DevBuf<float> q_time[2];
@@ -161,48 +143,13 @@ struct FrameSlot {
     std::vector<int4> tiles_dev;  // host copy of the device tile list
     int expect_count[kMaxLevels] = {0};  // grid hints from the previous frame (0 = unknown)
     int expect_shadow_total = 0;
-    // captured launch sequence of this slot and the host arguments it was captured with
-    hipGraphExec_t gexec = nullptr;
-    std::vector<unsigned char> gsig;
-    int graph_trace_launches = 0;
-    void add_buffers(Signature& g) const {
-        for (int b = 0; b < 2; ++b) {
-            g.add(q_ro[b].p);
-            g.add(q_rd[b].p);
-            g.add(q_hit[b].p);
-            g.add(q_time[b].p);
-        }
-        g.add(q_cap);
-        for (size_t L = 0; L < n_color.size(); ++L) {
-            g.add(n_color[L]->p);
-            g.add(n_att[L]->p);
-            g.add(n_link[L]->p);
-            g.add(level_cap[L]);
-        }
-        g.add(s_ro.p);
-        g.add(s_rd.p);
-        g.add(s_hit.p);
-        g.add(s_contrib.p);
-        g.add(s_cap);
-        g.add(fc.p);
-        g.add(pinned_fc);
-        g.add(pinned_tiles);
-        g.add(tiles.p);
-        g.add(accum.p);
-        g.add(gstack.p);
-        g.add_bytes(expect_count, sizeof(expect_count));
-        g.add(expect_shadow_total);
-    }
     FrameSlot() {
         PGRT_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-        PGRT_HIP(hipEventCreateWithFlags(&ev_stagger, hipEventDisableTiming));
         PGRT_HIP(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
     }
     ~FrameSlot() {
-        if (gexec) (void)hipGraphExecDestroy(gexec);
         if (pinned_fc) (void)hipHostFree(pinned_fc);
         if (pinned_tiles) (void)hipHostFree(pinned_tiles);
-        if (ev_stagger) (void)hipEventDestroy(ev_stagger);
         if (ev_done) (void)hipEventDestroy(ev_done);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -264,18 +211,12 @@ struct pgrt_ctx {
     DevBuf<DevLight> lights;
     SceneView view{};
     bool has_scene = false;
-    unsigned long long scene_gen = 0;  // bumped by every pgrt_set_scene
-    bool group_max_env = false;        // PGRT_GROUP_MAX given (else the default follows the mode)
-    // levels 0..packet_levels traced as wave packets (PGRT_PACKET_LEVELS): level 0 is coherent by
-    // construction (8x8 pixel blocks), levels 1-2 since k_shade queues each wave's reflections and
-    // refractions as separate pixel-ordered groups (r1g C2: 0 / 1 / 2 / 3 / all levels 0.206 /
-    // 0.197 / 0.194 / 0.196 / 0.202 ms/frame)
-    int packet_levels = 2;
-    // level-0 rays (PGRT_FUSED_RAYGEN): 0 k_raygen writes the ray queue; 1 the packet traversal
-    // and the level-0 shade both regenerate them; 2 (default) the traversal generates and stores
-    // them; 3 the traversal also shades its packets (one level-0 kernel; r1g: 938 us vs 486 + 457,
-    // throughput 0.201 vs 0.197 ms/frame -- the shading is latency-bound, not HBM-bound)
-    int fused_raygen = 2;
+    pgrt_config cfg{};  // pgrt_set_config (zero = defaults)
+    // levels traced as wave packets: level 0 is coherent by construction (8x8 pixel blocks),
+    // levels 1-2 because k_shade queues each wave's reflections and refractions as separate
+    // pixel-ordered groups (r1g C2: packets on levels 0 / 0-1 / 0-2 / 0-3 / all: 0.206 / 0.197 /
+    // 0.194 / 0.196 / 0.202 ms/frame)
+    int packet_levels = 3;
     pgrt_bvh_info info{};
 
     CameraView cam{};
@@ -286,7 +227,6 @@ struct pgrt_ctx {
     std::vector<std::unique_ptr<FrameSet>> sets;
     int frames_in_flight = 1;
     unsigned long long next_ticket = 1;
-    DevBuf<FrameCounters> fc;  // pgrt_intersect_closest
     DevBuf<int> gstack;        // pgrt_intersect_closest
     DevBuf<float> out_tmp;
     StageTimer timer;
@@ -465,17 +405,11 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
     pos.alloc((size_t)n * 9);
     PGRT_HIP(hipMemcpyAsync(pos.p, d->positions, (size_t)n * 9 * sizeof(float), hipMemcpyHostToDevice, st));
     BuildOut bo{};
-    // layout knobs, read per set_scene so one process can compare them (tests, tools/ab_env.sh):
-    // PGRT_BVH=lbvh selects the plain Karras LBVH (default PLOC); PGRT_BVH_WIDTH=8 the
-    // quantized 8-wide traversal layout (default binary, faster on the avenger proxy);
-    // PGRT_SPLIT=beta the early-split-clipping budget of the PLOC build (extra references as a
-    // fraction of the triangle count, 0 = off)
-    const char* eb = getenv("PGRT_BVH");
-    const int builder = (eb && std::string(eb) == "lbvh") || n < 2 ? kBuilderLbvh : kBuilderPloc;
-    const char* ew = getenv("PGRT_BVH_WIDTH");
-    const int width = (ew && std::string(ew) == "8") ? 8 : 2;
-    const char* es = getenv("PGRT_SPLIT");
-    const float beta = es ? std::max(0.0f, std::min(4.0f, (float)atof(es))) : kDefaultSplitBeta;
+    // layout choices (pgrt_config): builder, traversal width, split budget
+    const pgrt_config& cfg = ctx->cfg;
+    const int builder = cfg.bvh_builder == PGRT_BVH_LBVH || n < 2 ? kBuilderLbvh : kBuilderPloc;
+    const int width = cfg.bvh_width == 8 ? 8 : 2;
+    const float beta = std::max(0.0f, std::min(4.0f, cfg.split_beta));
     bo.builder = builder;
     bo.leaf_max = kLeafMaxTris;
     auto tb = std::chrono::steady_clock::now();
@@ -517,13 +451,7 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
     v.nodes8 = ctx->nodes8.p;
     v.tri8 = ctx->tri8.p;
     v.depth8 = wide_depth;
-    const char* epl = getenv("PGRT_PACKET_LEVELS");  // read per set_scene (tests compare settings)
-    ctx->packet_levels = epl ? atoi(epl) : 2;
-    const char* efr = getenv("PGRT_FUSED_RAYGEN");
-    ctx->fused_raygen = efr ? atoi(efr) : 2;
-    const char* eg = getenv("PGRT_GROUP_MAX");  // read per set_scene (tests compare settings)
-    v.group_max = eg ? atoi(eg) : kDefaultGroupMax;
-    ctx->group_max_env = eg != nullptr;
+    v.group_max = kDefaultGroupMax;  // per frame: pgrt_config.group_max / frames in flight
     v.wide = width == 8 ? 1 : 0;
     v.ntri = n;
     v.depth = bo.max_depth;
@@ -657,6 +585,27 @@ FrameSet* frame_set(pgrt_ctx* ctx, int i) {
     return ctx->sets[i].get();
 }
 
+// level-0 rays per sample batch
+long long batch_rays(const pgrt_ctx* ctx) {
+    return ctx->cfg.max_batch_rays > 0 ? ctx->cfg.max_batch_rays : kMaxBatchRays;
+}
+
+// is level L traced as wave packets (pgrt_config.packet_levels)
+bool packet_level(const pgrt_ctx* ctx, int L) {
+    const int k = ctx->cfg.packet_levels;
+    if (k == PGRT_PACKETS_OFF) return false;
+    return L < (k == PGRT_PACKETS_AUTO ? ctx->packet_levels : k);
+}
+
+// 8-lanes-per-ray threshold: with frames in flight the concurrent frames hide the latency floors
+// (r1 scan: 100k rays 0.392 -> 0.366 ms/frame), synchronous frames use the larger default
+int group_max(const pgrt_ctx* ctx) {
+    const int g = ctx->cfg.group_max;
+    if (g < 0) return 0;
+    if (g > 0) return g;
+    return ctx->frames_in_flight > 1 ? kDefaultGroupMaxInFlight : kDefaultGroupMax;
+}
+
 // Enqueue the frame described by fs (params, tiles, output) on fs's slot streams after
 // fs->ev_ready.  Tiles are <= kTile x kTile; out_mode 0 writes a framebuffer (origin ox,oy, pitch
 // in pixels), 1 tile-compact buffers.  No host synchronisation.
@@ -666,28 +615,17 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
     const int ntiles = (int)tiles.size();
     const int spp = p->spp_side * p->spp_side;
     const int levels = p->max_level + 1;
-    // pipeline slots: tiles dealt round-robin (slot j gets tiles j, j+K, ...)
-    // (one slot per frame when frames are in flight: the concurrent frames fill the CUs instead,
-    // r1 scan: 6 frames x 1 slot 0.39 ms/frame, 3 frames x 2 slots 0.53)
-    static const int env_slots = [] {
-        const char* e = getenv("PGRT_SLOTS");
-        return e ? std::max(1, std::min(3, atoi(e))) : 0;
-    }();
-    const int want_slots = env_slots ? env_slots : (ctx->frames_in_flight > 1 ? 1 : kDefaultSlots);
-    static const int stagger_level = [] {  // slot k+1 starts after slot k's level-L shade (-1: no stagger)
-        const char* e = getenv("PGRT_STAGGER_LEVEL");
-        return e ? atoi(e) : -1;
-    }();
-    // pipeline knobs read per set_scene (ctx->packet_levels, ctx->fused_raygen; see there)
-    const int packet_levels = ctx->packet_levels;
-    const int fused_raygen = ctx->fused_raygen;
-    static const bool packet_shadow = [] {  // shadow queue as wave packets (A/B knob)
-        const char* e = getenv("PGRT_PACKET_SHADOW");
-        return e ? atoi(e) != 0 : false;
-    }();
+    // pipeline slots: tiles dealt round-robin (slot j gets tiles j, j+K, ...); one slot per frame
+    // when frames are in flight: the concurrent frames fill the CUs instead (r1 scan: 6 frames x
+    // 1 slot 0.39 ms/frame, 3 frames x 2 slots 0.53)
+    const int want_slots = ctx->frames_in_flight > 1 ? 1 : kDefaultSlots;
     const int K = ntiles == 0 ? 0 : std::max(1, std::min(want_slots, ntiles));
     SceneView view = ctx->view;
-    if (!ctx->group_max_env && ctx->frames_in_flight > 1) view.group_max = kDefaultGroupMaxInFlight;
+    view.group_max = group_max(ctx);
+    const long long max_batch = batch_rays(ctx);
+    // level-0 rays generated inside the packet traversal (no k_raygen launch, no 32-B/ray read in
+    // the traversal); it stores them for the level-0 shade
+    const bool fuse = packet_level(ctx, 0) && trace_packets_available(view);
     fs->K = K;
     fs->batches = 0;
     while ((int)fs->slots.size() < K) fs->slots.emplace_back(new FrameSlot());
@@ -707,23 +645,14 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
     fp0.jitter = p->jitter;
     fp0.seed = p->seed;
     fp0.frame = p->frame;
-    static const bool graphs = [] {  // PGRT_GRAPHS=1: hipGraph replay (off by default, see below)
-        const char* e = getenv("PGRT_GRAPHS");
-        return e ? atoi(e) != 0 : false;
-    }();
-    // hipGraph replay: a slot's whole launch sequence (~25 launches at d=5) is captured once and
-    // replayed while every host-side launch argument is unchanged (the signature below).  It cuts
-    // the host's enqueue cost per frame 0.058 -> 0.012 ms, but r1 A/B with frames in flight
-    // (tools/inflight_scan.py) measured lower device throughput (C2, 4 in flight: 0.37 -> 0.45
-    // ms/frame), so kernels are launched one by one unless PGRT_GRAPHS=1
-    const bool use_graph = graphs && p->profile == 0 && stagger_level < 0;
     for (int j = 0; j < K; ++j) {
         FrameSlot* sl = fs->slots[j].get();
         hipStream_t s = sl->stream;
         const int nt = (ntiles - j + K - 1) / K;
         const long long npix = (long long)nt * kTile * kTile;
-        PGRT_REQUIRE(npix <= kMaxBatchRays * 8, PGRT_ERR_INVALID_ARGUMENT, "frame too large");
-        const int nsb = (int)std::max(1ll, std::min<long long>(spp, kMaxBatchRays / npix));
+        const int nsb = (int)std::max(1ll, std::min<long long>(spp, max_batch / npix));
+        PGRT_REQUIRE(npix * nsb < (1ll << 30), PGRT_ERR_INVALID_ARGUMENT,
+                     "frame too large: " + std::to_string(npix) + " pixels in one pipeline slot");
         const int batches = (spp + nsb - 1) / nsb;
         fs->batches += batches;
         ensure_frame_buffers(sl, (int)(npix * nsb), levels, view.nlight, batches);
@@ -735,45 +664,6 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
         // the pinned tile list may still feed this slot's previous upload
         PGRT_HIP(hipEventSynchronize(sl->ev_done));
         for (int t = j, q = 0; t < ntiles; t += K, ++q) sl->pinned_tiles[q] = tiles[t];
-        if (j > 0 && stagger_level >= 0) PGRT_HIP(hipStreamWaitEvent(s, fs->slots[j - 1]->ev_stagger, 0));
-        bool replay = false;
-        if (use_graph) {
-            Signature g;
-            g.add(*p);
-            g.add(ctx->cam);
-            g.add(view);
-            g.add(ctx->scene_gen);
-            g.add(K);
-            g.add(j);
-            g.add(nt);
-            g.add_bytes(sl->pinned_tiles, sizeof(int4) * nt);
-            g.add(fs->out);
-            g.add(fs->out_mode);
-            g.add(fs->ox);
-            g.add(fs->oy);
-            g.add(fs->pitch);
-            g.add(fs->nframes);
-            g.add(fs->frame_out_tiles);
-            g.add(fs->frame_stride);
-            sl->add_buffers(g);
-            if (sl->gexec && g.v == sl->gsig) {
-                replay = true;
-            } else {
-                if (sl->gexec) (void)hipGraphExecDestroy(sl->gexec);
-                sl->gexec = nullptr;
-                sl->gsig = std::move(g.v);
-                PGRT_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
-            }
-        }
-        if (replay) {
-            PGRT_HIP(hipGraphLaunch(sl->gexec, s));
-            PGRT_HIP(hipEventRecord(sl->ev_stagger, s));
-            sl->host_fc.resize(batches);
-            PGRT_HIP(hipEventRecord(sl->ev_done, s));
-            trace_launches += sl->graph_trace_launches;
-            continue;
-        }
-        const int launches_before = trace_launches;
         // the device tile list is re-uploaded only when it changed
         if (sl->tiles_dev.size() != (size_t)nt || !std::equal(sl->tiles_dev.begin(), sl->tiles_dev.end(),
                                                                sl->pinned_tiles, [](const int4& a, const int4& b) {
@@ -786,7 +676,6 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
         FrameParams fp = fp0;
         fp.ntiles = nt;
         fp.slot = j;
-        bool staggered = false;
         for (int bi = 0; bi < batches; ++bi) {
             const int s0 = bi * nsb;
             fp.s0 = s0;
@@ -797,15 +686,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             for (int b = 0; b < 2; ++b)
                 q[b] = Queue{sl->q_ro[b].p, sl->q_rd[b].p, sl->q_time[b].p, sl->q_hit[b].p, sl->q_cap};
             ShadowQueue sq{sl->s_ro.p, sl->s_rd.p, sl->s_hit.p, sl->s_contrib.p, sl->s_cap};
-            // fused primary rays: the level-0 packet traversal and shade regenerate each ray from
-            // the camera in registers instead of k_raygen writing (and both reading) a 36-B/ray queue
-            // (mode 2: the traversal also stores them and the shade reads the queue; mode 3: the
-            // traversal shades its packets itself -- no level-0 hit / ray queue, no k_shade launch)
-            const bool fuse = fused_raygen > 0 && packet_levels >= 0 && trace_packets_available(view, true);
-            const bool shade0 = fuse && fused_raygen == 3 && view.nmat <= kLdsMats && view.ntex <= kLdsTex;
-            const bool store = fuse && (fused_raygen == 2 || (fused_raygen == 3 && !shade0));
-            const PrimaryGen gen{ctx->cam, fp, sl->tiles.p, store ? q[0].ro : nullptr, store ? q[0].rd : nullptr,
-                                 store ? q[0].time : nullptr, &fcd->count0};
+            const PrimaryGen gen{ctx->cam, fp, sl->tiles.p, q[0].ro, q[0].rd, q[0].time, &fcd->count0};
             int id = ctx->timer.begin(s, CAT_RAYGEN);
             if (!fuse) launch_raygen(ctx->cam, fp, sl->tiles.p, q[0], n0, fcd, s);
             debug_sync(s, "raygen", 0, bi);
@@ -818,34 +699,46 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 LevelNodes ln{sl->n_color[L]->p, sl->n_link[L]->p, sl->n_att[L]->p};
                 // grid hints: last frame's per-level counts (+25 %); level 0 is exact
                 const int ex = L == 0 ? n0 : sl->expect_count[L];
-                const ShadeArgs shade_args{qn, ln, sq, fcd};
+                TraceLaunch tl;
+                tl.ro = qc.ro;
+                tl.rd = qc.rd;
+                tl.hits = qc.hit;
+                tl.count_dev = L == 0 && fuse ? nullptr : fc_count_ptr(fcd, L);
+                tl.count_host = L == 0 && fuse ? n0 : 0;
+                tl.max_count = maxc;
+                tl.expect = ex;
+                tl.gstack = sl->gstack.p;
+                tl.gstack_threads = kTraceGridThreads;
+                tl.counters = fcd->trav[L];
+                tl.count = p->profile >= 2;
+                tl.packets = packet_level(ctx, L);  // coherent 8x8-pixel waves -> packet traversal
+                tl.gen = L == 0 && fuse ? &gen : nullptr;
                 id = ctx->timer.begin_kernel(CAT_TRACE, CAT_LTRACE + L);
-                const bool launched =
-                    launch_trace(view, qc.ro, qc.rd, qc.hit, L == 0 && fuse ? nullptr : fc_count_ptr(fcd, L),
-                                 L == 0 && fuse ? n0 : 0, maxc, &fcd->fetch[L], sl->gstack.p, kTraceGridThreads,
-                                 fcd->trav[L], p->profile >= 2, s, ex, 1, true,
-                                 L <= packet_levels,  // coherent 8x8-pixel waves -> packet traversal
-                                 L == 0 && fuse ? &gen : nullptr, L == 0 && shade0 ? &shade_args : nullptr);
+                const bool launched = launch_trace(view, tl, s);
                 ctx->timer.end_kernel(s, id, launched);
                 debug_sync(s, "trace", L, bi);
                 ++trace_launches;
                 id = ctx->timer.begin(s, CAT_SHADE, CAT_LSHADE + L);
-                if (!(L == 0 && shade0))
-                    launch_shade(view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex,
-                                 L == 0 && fuse && !store ? &gen : nullptr);
+                launch_shade(view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex);
                 debug_sync(s, "shade", L, bi);
                 ctx->timer.end(s, id);
-                if (!staggered && (L == std::min(stagger_level, levels - 1))) {
-                    PGRT_HIP(hipEventRecord(sl->ev_stagger, s));
-                    staggered = true;
-                }
             }
             if (view.nlight > 0 && p->max_level > 0) {  // every level's shadow rays, one launch
+                TraceLaunch tl;
+                tl.ro = sq.ro;
+                tl.rd = sq.rd;
+                tl.hits = sq.hit;
+                tl.count_dev = fc_shadow_counts(fcd);
+                tl.count_terms = levels;
+                tl.max_count = sq.cap;
+                tl.expect = sl->expect_shadow_total;
+                tl.gstack = sl->gstack.p;
+                tl.gstack_threads = kTraceGridThreads;
+                tl.counters = fcd->trav[kMaxLevels];
+                tl.count = p->profile >= 2;
+                tl.allow_group = false;  // shadow rays: one lane per ray (no 8-lane groups, no packets)
                 id = ctx->timer.begin_kernel(CAT_TRACE, CAT_SHADOW);
-                const bool launched = launch_trace(
-                    view, sq.ro, sq.rd, sq.hit, fc_shadow_counts(fcd), 0, sq.cap, &fcd->fetch[kMaxLevels],
-                    sl->gstack.p, kTraceGridThreads, fcd->trav[kMaxLevels], p->profile >= 2, s,
-                    sl->expect_shadow_total, levels, false, packet_shadow);  // shadow rays: no 8-lane groups
+                const bool launched = launch_trace(view, tl, s);
                 ctx->timer.end_kernel(s, id, launched);
                 debug_sync(s, "shadow trace", levels, bi);
                 ++trace_launches;
@@ -869,28 +762,9 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             ctx->timer.end(s, id);
         }
         sl->host_fc.resize(batches);
-        static const bool export_kernel = [] {  // A/B knob: PGRT_EXPORT=0 copies + memsets instead
-            const char* e = getenv("PGRT_EXPORT");
-            return e ? atoi(e) != 0 : true;
-        }();
-        if (export_kernel) {
-            launch_export_counters(sl->fc.p, sl->pinned_fc, batches, s);  // and zero them for the next frame
-            debug_sync(s, "export", 0, 0);
-        } else {
-            PGRT_HIP(hipMemcpyAsync(sl->pinned_fc, sl->fc.p, sizeof(FrameCounters) * batches, hipMemcpyDeviceToHost,
-                                    s));
-            PGRT_HIP(hipMemsetAsync(sl->fc.p, 0, sizeof(FrameCounters) * batches, s));
-        }
-        if (use_graph) {
-            hipGraph_t graph = nullptr;
-            PGRT_HIP(hipStreamEndCapture(s, &graph));
-            const hipError_t e = hipGraphInstantiate(&sl->gexec, graph, nullptr, nullptr, 0);
-            (void)hipGraphDestroy(graph);
-            PGRT_HIP(e);
-            sl->graph_trace_launches = trace_launches - launches_before;
-            PGRT_HIP(hipGraphLaunch(sl->gexec, s));
-        }
-        if (!staggered) PGRT_HIP(hipEventRecord(sl->ev_stagger, s));
+        // the frame's counters to pinned host memory, zeroed on the device for the next frame
+        launch_export_counters(sl->fc.p, sl->pinned_fc, batches, s);
+        debug_sync(s, "export", 0, 0);
         PGRT_HIP(hipEventRecord(sl->ev_done, s));
     }
     PGRT_HIP(hipGetLastError());
@@ -1196,12 +1070,36 @@ void pgrt_destroy(pgrt_ctx* ctx) {
 
 const char* pgrt_last_error(const pgrt_ctx* ctx) { return ctx ? ctx->err.c_str() : "NULL context"; }
 
+int pgrt_get_config(const pgrt_ctx* ctx, pgrt_config* cfg) {
+    if (!ctx || !cfg) return PGRT_ERR_INVALID_ARGUMENT;
+    *cfg = ctx->cfg;
+    return PGRT_OK;
+}
+
+int pgrt_set_config(pgrt_ctx* ctx, const pgrt_config* cfg) {
+    if (!ctx || !cfg) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        PGRT_REQUIRE(cfg->bvh_builder == 0 || cfg->bvh_builder == PGRT_BVH_LBVH || cfg->bvh_builder == PGRT_BVH_PLOC,
+                     PGRT_ERR_INVALID_ARGUMENT, "bvh_builder must be 0, PGRT_BVH_LBVH or PGRT_BVH_PLOC");
+        PGRT_REQUIRE(cfg->bvh_width == 0 || cfg->bvh_width == 2 || cfg->bvh_width == 8, PGRT_ERR_INVALID_ARGUMENT,
+                     "bvh_width must be 0, 2 or 8");
+        PGRT_REQUIRE(cfg->split_beta >= 0.0f && cfg->split_beta <= 4.0f, PGRT_ERR_INVALID_ARGUMENT,
+                     "split_beta must be in [0, 4]");
+        PGRT_REQUIRE(cfg->packet_levels >= PGRT_PACKETS_OFF && cfg->packet_levels <= kMaxLevels,
+                     PGRT_ERR_INVALID_ARGUMENT, "packet_levels must be AUTO, OFF or in [1, 16]");
+        PGRT_REQUIRE(cfg->max_batch_rays >= 0 && cfg->max_batch_rays <= (1ll << 29), PGRT_ERR_INVALID_ARGUMENT,
+                     "max_batch_rays must be in [0, 2^29]");
+        PGRT_REQUIRE(cfg->max_batches_in_flight >= 0, PGRT_ERR_INVALID_ARGUMENT, "max_batches_in_flight must be >= 0");
+        drain_frames(ctx);  // pending frames were enqueued with the old choices
+        ctx->cfg = *cfg;
+    });
+}
+
 int pgrt_set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* scene) {
     if (!ctx) return PGRT_ERR_INVALID_ARGUMENT;
     return guarded(ctx, [&] {
         drain_frames(ctx);  // frames in flight read the old scene
         PGRT_HIP(hipStreamSynchronize(ctx->stream));
-        ++ctx->scene_gen;
         set_scene(ctx, scene);
     });
 }
@@ -1309,10 +1207,17 @@ int pgrt_intersect_closest(pgrt_ctx* ctx, const float* rays, int n, float* hits)
         PGRT_HIP(hipMemcpyAsync(ro.p, a.data(), sizeof(float4) * n, hipMemcpyHostToDevice, ctx->stream));
         PGRT_HIP(hipMemcpyAsync(rd.p, b.data(), sizeof(float4) * n, hipMemcpyHostToDevice, ctx->stream));
         if (ctx->gstack.n == 0) ctx->gstack.alloc((size_t)kTraceGridThreads * kGlobalStack);
-        ctx->fc.alloc(1);
-        PGRT_HIP(hipMemsetAsync(ctx->fc.p, 0, sizeof(FrameCounters), ctx->stream));
-        launch_trace(ctx->view, ro.p, rd.p, h.p, nullptr, n, n, &ctx->fc.p->fetch[0], ctx->gstack.p,
-                     kTraceGridThreads, nullptr, false, ctx->stream);
+        TraceLaunch tl;
+        tl.ro = ro.p;
+        tl.rd = rd.p;
+        tl.hits = h.p;
+        tl.count_host = n;
+        tl.max_count = n;
+        tl.gstack = ctx->gstack.p;
+        tl.gstack_threads = kTraceGridThreads;
+        SceneView view = ctx->view;
+        view.group_max = group_max(ctx);  // batches up to it: 8 / 4 lanes per ray
+        launch_trace(view, tl, ctx->stream);
         PGRT_HIP(hipGetLastError());
         PGRT_HIP(hipMemcpyAsync(hits, h.p, sizeof(float4) * n, hipMemcpyDeviceToHost, ctx->stream));
         PGRT_HIP(hipStreamSynchronize(ctx->stream));
@@ -1509,9 +1414,10 @@ int submit_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device, 
                      "rank 0 needs an output buffer");
         FrameSet* fs = frame_set(ctx, (int)(ctx->next_ticket % (unsigned long long)ctx->frames_in_flight));
         if (fs->pending) finish_through(ctx, fs->ticket);  // the set's previous frame completes first
-        // bound the batches queued across frames in flight (this frame's own count estimated
-        // with one slot per frame, as enqueue_frame deals them when frames are in flight)
-        {
+        // pgrt_config.max_batches_in_flight: bound the sample batches queued across frames in
+        // flight (this frame's own count estimated with one slot per frame, as enqueue_frame deals
+        // them when frames are in flight)
+        if (const int cap = ctx->cfg.max_batches_in_flight; cap > 0) {
             long long nt;
             if (distributed) {
                 nt = (long long)rank_tiles(ctx->cam.width, ctx->cam.height, ctx->rank, ctx->world).size();
@@ -1522,7 +1428,7 @@ int submit_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device, 
             }
             const long long npix = std::max(1ll, nt * nframes) * kTile * kTile;
             const int spp = p->spp_side * p->spp_side;
-            const int nsb = (int)std::max(1ll, std::min<long long>(spp, kMaxBatchRays / npix));
+            const int nsb = (int)std::max(1ll, std::min<long long>(spp, batch_rays(ctx) / npix));
             const int mine = (spp + nsb - 1) / nsb;
             for (;;) {
                 int queued = 0;
@@ -1532,7 +1438,7 @@ int submit_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device, 
                         queued += s->batches;
                         if (!oldest || s->ticket < oldest) oldest = s->ticket;
                     }
-                if (!oldest || queued + mine <= kMaxBatchesInFlight) break;
+                if (!oldest || queued + mine <= cap) break;
                 finish_through(ctx, oldest);
             }
         }

@@ -222,11 +222,9 @@ __global__ __launch_bounds__(kB) void k_ploc_tris(const float* __restrict__ pos,
 void build_ploc(const float* pos, const float4* rlo, const float4* rhi, const int* order, int n, float4* tri,
                 BvhNode* nodes, BuildOut* out, int* iterations, hipStream_t stream) {
     const int total = 2 * n - 1;
-    // build knobs (A/B): PGRT_PLOC_RADIUS (<= 64), PGRT_SAH_TRI (triangle-test cost / node step)
-    const char* er = getenv("PGRT_PLOC_RADIUS");
-    const int radius = er ? std::max(1, std::min(kMaxRadius, atoi(er))) : kDefaultRadius;
-    const char* ec = getenv("PGRT_SAH_TRI");
-    const float cost_tri = ec ? (float)atof(ec) : kDefaultCostTri;
+    // r1g A/B (profiles/r1g/c5_bvh_knobs_ab.txt): radius 8..32 and triangle cost 0.5..2 within 2 %
+    const int radius = kDefaultRadius;
+    const float cost_tri = kDefaultCostTri;
     DevBuf<float4> nlo, nhi, cl_lo[2], cl_hi[2];
     DevBuf<int2> kids;
     DevBuf<int> parent, cl_node[2], nn, count, collapse, flags, offset, misc;

@@ -49,26 +49,14 @@ void launch_raygen(const CameraView& cam, const FrameParams& fp, const int4* til
 
 // ------------------------------------------------------------------ shading (trace body)
 
-// LDS_TABLES: the material and texture-descriptor tables are copied to LDS per block
-// (kLdsMats / kLdsTex, shade_ray.hpp)
-
-// k_shade: the hit triangle's attributes loaded one ray ahead (A/B switch; r1h: 0.1982 vs
-// 0.2000 ms/frame without / with -- off)
-#ifndef PGRT_ATTR_PREFETCH
-#define PGRT_ATTR_PREFETCH 0
-#endif
 // k_shade block size (one allocation atomic per block and iteration, shade_ray.hpp; r1f A/B:
 // 256 beat 512 and 1024)
-#ifndef PGRT_SHADE_BLOCK
-#define PGRT_SHADE_BLOCK 256
-#endif
-constexpr int kShadeBlock = PGRT_SHADE_BLOCK;
+constexpr int kShadeBlock = 256;
 static_assert(kShadeBlock % kBlock == 0, "k_shade blocks are whole multiples of kBlock");
 
-template <bool LDS_TABLES, bool GEN>
+template <bool LDS_TABLES>
 __global__ __launch_bounds__(kShadeBlock) void k_shade(SceneView s, FrameParams fp, int level, Queue q, Queue next,
-                                                  LevelNodes nodes, ShadowQueue sq, FrameCounters* fc, PrimaryGen gen,
-                                                  int n_gen) {
+                                                       LevelNodes nodes, ShadowQueue sq, FrameCounters* fc) {
     __shared__ float lut255[256];
     __shared__ DevMaterial smat[LDS_TABLES ? kLdsMats : 1];
     __shared__ DevTexture stex[LDS_TABLES ? kLdsTex : 1];
@@ -81,11 +69,8 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(SceneView s, FrameParams 
     int it_par = 0;
     const DevMaterial* mats = LDS_TABLES ? smat : s.mats;
     fill_byte_lut(lut255);  // ends with __syncthreads: the tables above are visible too
-    // GEN (level 0, fused primary rays): n_gen rays regenerated from the camera, no ray queue
-    // was written; this launch publishes the level-0 count in raygen's place
-    const int n = GEN ? n_gen : min(fc_count(*fc, level), q.cap);
+    const int n = min(fc_count(*fc, level), q.cap);
     const int tid = threadIdx.x;
-    if (GEN && blockIdx.x == 0 && tid == 0) fc->count0 = n_gen;
     // one shadow queue for the whole batch: level L's rays follow those of levels < L (final by now)
     int sq_base = 0;
     for (int l = 0; l < level; ++l) sq_base += fc_shadow(*fc, l);
@@ -98,66 +83,41 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(SceneView s, FrameParams 
     {
         const int i0 = blockIdx.x * kShadeBlock + tid;
         if (i0 < n) {
-            if constexpr (!GEN) {
-                nx_o = q.ro[i0];
-                nx_d = q.rd[i0];
-                nx_t = q.time[i0];
-            }
+            nx_o = q.ro[i0];
+            nx_d = q.rd[i0];
+            nx_t = q.time[i0];
             nx_h = q.hit[i0];
         }
     }
-#if PGRT_ATTR_PREFETCH
-    HitAttr nx_a = load_attr(s, nx_h);
-#endif
     for (int base_i = blockIdx.x * kShadeBlock; base_i < n; base_i += stride) {
         const int i = base_i + tid;
         const bool active = i < n;
-        float4 cur_o = nx_o, cur_d = nx_d;
-        const float4 cur_h = nx_h;
-        float cur_t = nx_t;
+        const float4 cur_o = nx_o, cur_d = nx_d, cur_h = nx_h;
+        const float cur_t = nx_t;
         if (i + stride < n) {
-            if constexpr (!GEN) {
-                nx_o = q.ro[i + stride];
-                nx_d = q.rd[i + stride];
-                nx_t = q.time[i + stride];
-            }
+            nx_o = q.ro[i + stride];
+            nx_d = q.rd[i + stride];
+            nx_t = q.time[i + stride];
             nx_h = q.hit[i + stride];
         }
-        if constexpr (GEN) {
-            if (active) cur_t = primary_ray(gen.cam, gen.fp, gen.tiles, i, cur_o, cur_d) ? PGRT_IOR_AIR : 0.0f;
-        }
         ShadeOut r;
-#if PGRT_ATTR_PREFETCH
-        // the next ray's attributes are requested before this ray's allocation round trip (its
-        // hit arrived during this ray's shading), so the next hit -> attribute hop overlaps it
-        const HitAttr cur_a = nx_a;
-        shade_eval(s, mats, lut255, level, fp.max_level, active, cur_o, cur_d, cur_t, cur_h, r, &cur_a);
-        if (i + stride < n) nx_a = load_attr(s, nx_h);
-#else
         shade_eval(s, mats, lut255, level, fp.max_level, active, cur_o, cur_d, cur_t, cur_h, r);
-#endif
         const ShadeSlots sl = shade_alloc<kShadeBlock>(alds, it_par, fc, level, sq_base, sbits, r);
         if (active) shade_emit(s, mats, level, i, r, sl, next, nodes, sq, fc);
     }
 }
 
 void launch_shade(const SceneView& s, const FrameParams& fp, int level, Queue q, Queue next, LevelNodes nodes,
-                  ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect,
-                  const PrimaryGen* gen) {
+                  ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect) {
     if (max_count <= 0) return;
     const int per_block = kShadeBlock / kBlock;  // grid_for counts kBlock-thread blocks
     const int grid = std::max(1, grid_for(max_count, expect) / per_block);
-    const PrimaryGen g = gen ? *gen : PrimaryGen{};
-    const bool lds = s.nmat <= kLdsMats && s.ntex <= kLdsTex;
-#define PGRT_LAUNCH_S(L, G)                                                                                    \
-    hipLaunchKernelGGL((k_shade<L, G>), dim3(grid), dim3(kShadeBlock), 0, stream, s, fp, level, q, next, nodes, sq, \
-                       fc, g, max_count)
-    if (lds) {
-        if (gen) PGRT_LAUNCH_S(true, true); else PGRT_LAUNCH_S(true, false);
-    } else {
-        if (gen) PGRT_LAUNCH_S(false, true); else PGRT_LAUNCH_S(false, false);
-    }
-#undef PGRT_LAUNCH_S
+    if (s.nmat <= kLdsMats && s.ntex <= kLdsTex)
+        hipLaunchKernelGGL((k_shade<true>), dim3(grid), dim3(kShadeBlock), 0, stream, s, fp, level, q, next, nodes, sq,
+                           fc);
+    else
+        hipLaunchKernelGGL((k_shade<false>), dim3(grid), dim3(kShadeBlock), 0, stream, s, fp, level, q, next, nodes, sq,
+                           fc);
 }
 
 // ------------------------------------------------------------------ combine + finish

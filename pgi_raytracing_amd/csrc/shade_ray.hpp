@@ -1,6 +1,5 @@
 // shade_ray.hpp -- the per-ray Whitted shading step (APP/raytracer.cpp:237-394, one level of
-// Raytracer::trace), split in three phases so that both k_shade (a level's queue) and the fused
-// level-0 packet kernel (trace + shade without a hit / ray round trip through HBM) run it:
+// Raytracer::trace), in three phases (k_shade, render.hip):
 //   shade_eval   what the ray's hit produces (final colour, dielectric children, shadow rays)
 //   shade_alloc  queue slots for the children / shadow rays: ballot + mbcnt inside the wave, ONE
 //                packed 64-bit atomic (children | shadow rays << 32) per block and iteration
@@ -22,14 +21,6 @@ namespace pgrt {
 // shading tables in LDS when they fit (the hit -> attributes -> material -> texture chain has one
 // global round trip fewer per hop)
 constexpr int kLdsMats = 64, kLdsTex = 32;
-
-// level-0 shading fused into the packet traversal: the level's outputs
-struct ShadeArgs {
-    Queue next;         // level-1 rays
-    LevelNodes nodes;   // level-0 node records
-    ShadowQueue sq;     // the batch's shadow queue (level 0's rays come first)
-    FrameCounters* fc;
-};
 
 // Wave-level slot allocation for small per-lane counts (children <= 2, shadow rays <= lights):
 // the exclusive prefix is sum_b 2^b * (lanes below with bit b set), one ballot + mbcnt per bit.
@@ -78,11 +69,10 @@ __device__ __forceinline__ HitAttr load_attr(const SceneView& s, float4 h) {
     return a;
 }
 
-// Phase 1 for one ray (o4 = org|tnear, d4 = dir|tfar, rtime = medium IOR, h = t|u|v|prim); pa:
-// the hit's attributes when already loaded (k_shade prefetches them one ray ahead), else NULL.
+// Phase 1 for one ray (o4 = org|tnear, d4 = dir|tfar, rtime = medium IOR, h = t|u|v|prim).
 __device__ __forceinline__ void shade_eval(const SceneView& s, const DevMaterial* mats, const float* lut,
                                            int level, int max_level, bool active, float4 o4, float4 d4,
-                                           float rtime, float4 h, ShadeOut& r, const HitAttr* pa = nullptr) {
+                                           float rtime, float4 h, ShadeOut& r) {
     r.kind = 0;
     r.color = make_float4(0, 0, 0, 1);
     r.nshadow = 0;
@@ -106,7 +96,7 @@ __device__ __forceinline__ void shade_eval(const SceneView& s, const DevMaterial
         return;
     }
     const float t = h.x;
-    const HitAttr ha = pa ? *pa : load_attr(s, h);
+    const HitAttr ha = load_attr(s, h);
     const float* a = reinterpret_cast<const float*>(ha.q);
     const float u = h.y, v = h.z;
     V3 nn = v3(interp1(a[0], a[3], a[6], u, v), interp1(a[1], a[4], a[7], u, v), interp1(a[2], a[5], a[8], u, v));

@@ -22,21 +22,11 @@
 
 #include "trace.hpp"
 #include "camera_ops.hpp"
-#include "shade_ray.hpp"
 
 namespace pgrt {
 
 constexpr int kTraceBlock = 256;
 constexpr int kSentinel = 0x7fffffff;  // bottom of every stack: "traversal finished"
-
-// packet traversal A/B switches: packed-pair child box tests (r1f: 507 vs 485 us per L0 launch,
-// off), precomputed triangle normals (r1f: 503 vs 511 us, on)
-#ifndef PGRT_PK_BOX
-#define PGRT_PK_BOX 0
-#endif
-#ifndef PGRT_TRI_NG
-#define PGRT_TRI_NG 1
-#endif
 
 __device__ __forceinline__ bool box_hit(float lox, float hix, float loy, float hiy, float loz,
                                         float hiz, float idx, float idy, float idz, float oix,
@@ -88,29 +78,6 @@ __device__ __forceinline__ void tri_test(float4 q0, float4 q1, float4 q2, float 
                                          float& best_v, int& best_prim) {
     tri_test_ng(q0, q1, q2, tri_normal(q1, q2), ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v,
                 best_prim);
-}
-
-// both child boxes of a binary node at once: the slab fmas as packed pairs (v_pk_fma_f32);
-// conservative like box_hit (the boxes are padded, the exit distance scaled by 1 + 1e-6)
-typedef float pgrt_f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void box_hit2(float4 a, float4 b, float4 c, float idx, float idy, float idz, float oix,
-                                         float oiy, float oiz, float tmax, bool& h0, bool& h1, float& t0,
-                                         float& t1) {
-    const pgrt_f2 vidx = {idx, idx}, vidy = {idy, idy}, vidz = {idz, idz};
-    const pgrt_f2 voix = {-oix, -oix}, voiy = {-oiy, -oiy}, voiz = {-oiz, -oiz};
-    const pgrt_f2 lx = {a.x, b.x}, hx = {a.y, b.y}, ly = {a.z, b.z}, hy = {a.w, b.w}, lz = {c.x, c.z},
-                  hz = {c.y, c.w};
-    const pgrt_f2 tx0 = __builtin_elementwise_fma(lx, vidx, voix), tx1 = __builtin_elementwise_fma(hx, vidx, voix);
-    const pgrt_f2 ty0 = __builtin_elementwise_fma(ly, vidy, voiy), ty1 = __builtin_elementwise_fma(hy, vidy, voiy);
-    const pgrt_f2 tz0 = __builtin_elementwise_fma(lz, vidz, voiz), tz1 = __builtin_elementwise_fma(hz, vidz, voiz);
-    const float e0 = fmaxf(fmaxf(fminf(tx0.x, tx1.x), fminf(ty0.x, ty1.x)), fmaxf(fminf(tz0.x, tz1.x), 0.0f));
-    const float x0 = fminf(fminf(fmaxf(tx0.x, tx1.x), fmaxf(ty0.x, ty1.x)), fminf(fmaxf(tz0.x, tz1.x), tmax));
-    const float e1 = fmaxf(fmaxf(fminf(tx0.y, tx1.y), fminf(ty0.y, ty1.y)), fmaxf(fminf(tz0.y, tz1.y), 0.0f));
-    const float x1 = fminf(fminf(fmaxf(tx0.y, tx1.y), fmaxf(ty0.y, ty1.y)), fminf(fmaxf(tz0.y, tz1.y), tmax));
-    t0 = e0;
-    t1 = e1;
-    h0 = e0 <= x0 * 1.000001f;
-    h1 = e1 <= x1 * 1.000001f;
 }
 
 __device__ __forceinline__ int ray_count(const int* count_dev, int count_terms, int count_host, int cap) {
@@ -664,30 +631,13 @@ typedef const __attribute__((address_space(4))) float* cfloat_ptr;
 __device__ __forceinline__ float4 cload4(cfloat_ptr p) { return make_float4(p[0], p[1], p[2], p[3]); }
 constexpr int kPktStack = 64;  // wave-uniform stack entries (>= BVH depth + 2)
 
-// SHADE (level 0 with GEN): the wave shades its packet right after the traversal (shade_ray.hpp)
-// -- ray and hit stay in registers, no hit record or ray queue goes through HBM, and the level-0
-// k_shade launch disappears.  The loop is then block-uniform (shade_alloc has barriers).
-template <bool COUNT, bool GEN, bool SHADE>
+template <bool COUNT, bool GEN>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const float4* __restrict__ ro,
                                                            const float4* __restrict__ rd, float4* __restrict__ hits,
                                                            const int* __restrict__ count_dev, int count_terms,
                                                            int count_host, int cap,
-                                                           unsigned long long* __restrict__ counters, PrimaryGen gen,
-                                                           ShadeArgs sh) {
+                                                           unsigned long long* __restrict__ counters, PrimaryGen gen) {
     __shared__ int wstack[kTraceBlock / 64][kPktStack];
-    __shared__ float lut255[SHADE ? 256 : 1];
-    __shared__ DevMaterial smat[SHADE ? kLdsMats : 1];
-    __shared__ DevTexture stex[SHADE ? kLdsTex : 1];
-    __shared__ ShadeAllocLds<kTraceBlock> alds;
-    int it_par = 0;
-    SceneView ss = s;  // shading view: descriptors from LDS
-    if constexpr (SHADE) {
-        for (int k = threadIdx.x; k < s.nmat; k += kTraceBlock) smat[k] = s.mats[k];
-        for (int k = threadIdx.x; k < s.ntex; k += kTraceBlock) stex[k] = s.tex[k];
-        ss.tex = stex;
-        fill_byte_lut(lut255);  // ends with __syncthreads
-    }
-    const int sbits = s.nlight > 0 ? 32 - __clz(s.nlight) : 0;
     const int wib = threadIdx.x >> 6;
     const int lane = __lane_id();
     const int n = ray_count(count_dev, count_terms, count_host, cap);
@@ -697,8 +647,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const fl
     const cfloat_ptr nodes = (cfloat_ptr)(const void*)s.nodes;  // 16 floats per node
     const cfloat_ptr tris = (cfloat_ptr)(const void*)s.tri;     // 12 floats per triangle
     unsigned long long nvis = 0, ntest = 0;
-    for (int bbase = blockIdx.x * kTraceBlock; bbase < n; bbase += gridDim.x * kTraceBlock) {
-        const int base = bbase + wib * 64;  // waves past n run no traversal but join the barriers
+    for (int base = (blockIdx.x * kTraceBlock) + wib * 64; base < n; base += gridDim.x * kTraceBlock) {
         const int i = base + lane;
         const bool valid = i < n;
         float4 o4 = make_float4(0, 0, 0, 0), d4 = make_float4(0, 0, 1, -1.0f);
@@ -742,13 +691,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const fl
                                          __float_as_int(nd[15]));
                 if (COUNT) ++rvis;
                 float t0, t1;
-#if PGRT_PK_BOX
-                bool h0, h1;
-                box_hit2(a, b, c, idx, idy, idz, oix, oiy, oiz, best_t, h0, h1, t0, t1);
-#else
                 const bool h0 = box_hit(a.x, a.y, a.z, a.w, c.x, c.y, idx, idy, idz, oix, oiy, oiz, best_t, t0);
                 const bool h1 = box_hit(b.x, b.y, b.z, b.w, c.z, c.w, idx, idy, idz, oix, oiy, oiz, best_t, t1);
-#endif
                 const unsigned long long b0 = __ballot(h0), b1 = __ballot(h1);
                 if (b0 == 0ull && b1 == 0ull) {
                     node = sp > 0 ? wstack[wib][--sp] : kSentinel;
@@ -768,27 +712,15 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const fl
                     const cfloat_ptr q = tris + 12 * k;
                     const float4 q0 = cload4(q), q1 = cload4(q + 4), q2 = cload4(q + 8);
                     if (COUNT) ++rtest;
-#if PGRT_TRI_NG
                     const float4 ng = cload4((cfloat_ptr)(const void*)s.tri_ng + 4 * k);  // precomputed Ng
                     if (live)
                         tri_test_ng(q0, q1, q2, ng, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v,
                                     best_prim);
-#else
-                    if (live) tri_test(q0, q1, q2, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v, best_prim);
-#endif
                 }
                 node = sp > 0 ? wstack[wib][--sp] : kSentinel;
             }
         }
-        const float4 hit = make_float4(live ? best_t : tfar, best_u, best_v, __int_as_float(best_prim));
-        if constexpr (SHADE) {
-            ShadeOut r;
-            shade_eval(ss, smat, lut255, 0, gen.fp.max_level, valid, o4, d4, pv ? PGRT_IOR_AIR : 0.0f, hit, r);
-            const ShadeSlots sl = shade_alloc<kTraceBlock>(alds, it_par, sh.fc, 0, 0, sbits, r);
-            if (valid) shade_emit(ss, smat, 0, i, r, sl, sh.next, sh.nodes, sh.sq, sh.fc);
-        } else {
-            if (valid) hits[i] = hit;
-        }
+        if (valid) hits[i] = make_float4(live ? best_t : tfar, best_u, best_v, __int_as_float(best_prim));
         if (COUNT && lane == 0) {
             nvis += rvis;
             ntest += rtest;
@@ -813,98 +745,73 @@ void set_trace_events(hipEvent_t start, hipEvent_t stop) {
 #define PGRT_TLAUNCH(kernel, grid, block, lds, stream, ...) \
     hipExtLaunchKernelGGL(kernel, grid, block, lds, stream, t_ev_start, t_ev_stop, 0, __VA_ARGS__)
 
-bool trace_packets_available(const SceneView& s, bool coherent) {
-    static const bool packets = [] {  // PGRT_PACKETS=0: level 0 on the one-lane kernel too
-        const char* e = getenv("PGRT_PACKETS");
-        return !(e && atoi(e) == 0);
-    }();
-    return coherent && packets && !s.wide && s.root >= 0 && s.depth + 2 <= kPktStack;
+bool trace_packets_available(const SceneView& s) {
+    return !s.wide && s.root >= 0 && s.depth + 2 <= kPktStack;
 }
 
-bool launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4* hits, const int* count_dev,
-                  int count_host, int max_count, int* fetch, int* gstack, int gstack_threads,
-                  unsigned long long* counters, bool count, hipStream_t stream, int expect, int count_terms,
-                  bool allow_group, bool coherent, const PrimaryGen* gen, const ShadeArgs* shade) {
+// 4 lanes per ray (two child slots each) above this many rays, 8 at or below it (r1 A/B)
+constexpr int kGroup8Max = 150000;
+// queues up to kTailMax rays spread over more waves: kTailRpw rays per wave (r1 A/B: 64, i.e.
+// full waves, was best)
+constexpr int kTailMax = 131072, kTailRpw = 64;
+
+bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) {
+    const int max_count = t.max_count;
     if (max_count <= 0) return false;
-    // gen (fused primary rays) is only passed when trace_packets_available(s, coherent) holds
-    static const bool force_spill = getenv("PGRT_FORCE_SPILL") != nullptr;  // A/B of the stack layout
+    const int ex = t.expect > 0 && t.expect < max_count ? t.expect : max_count;  // grid sizing only
     if (s.wide) {
-        int grid = ceil_div(expect > 0 && expect < max_count ? expect : max_count, kTraceBlock);
-        if (grid > gstack_threads / kTraceBlock) grid = gstack_threads / kTraceBlock;
-        if (count)
-            PGRT_TLAUNCH((k_trace8<true>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
-                               count_dev, count_terms, count_host, max_count, gstack, counters);
+        int grid = ceil_div(ex, kTraceBlock);
+        if (grid > t.gstack_threads / kTraceBlock) grid = t.gstack_threads / kTraceBlock;
+        if (t.count)
+            PGRT_TLAUNCH((k_trace8<true>), dim3(grid), dim3(kTraceBlock), 0, stream, s, t.ro, t.rd, t.hits,
+                         t.count_dev, t.count_terms, t.count_host, max_count, t.gstack, t.counters);
         else
-            PGRT_TLAUNCH((k_trace8<false>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits,
-                               count_dev, count_terms, count_host, max_count, gstack, counters);
+            PGRT_TLAUNCH((k_trace8<false>), dim3(grid), dim3(kTraceBlock), 0, stream, s, t.ro, t.rd, t.hits,
+                         t.count_dev, t.count_terms, t.count_host, max_count, t.gstack, t.counters);
         return true;
     }
-    // coherent level-0 waves: packet traversal
-    if (trace_packets_available(s, coherent)) {
-        const int exg = expect > 0 && expect < max_count ? expect : max_count;
-        int grid = ceil_div(exg, kTraceBlock);
+    // coherent waves (level 0's 8x8-pixel blocks, the coherent bounce levels): packet traversal
+    if ((t.packets || t.gen) && trace_packets_available(s)) {
+        int grid = ceil_div(ex, kTraceBlock);
         if (grid > 16384) grid = 16384;
-        const PrimaryGen g = gen ? *gen : PrimaryGen{};
-        const ShadeArgs sa = shade ? *shade : ShadeArgs{};
-#define PGRT_LAUNCH_P(C, G, SH)                                                                                  \
-    PGRT_TLAUNCH((k_trace_pkt<C, G, SH>), dim3(grid), dim3(kTraceBlock), 0, stream, s, ro, rd, hits, count_dev, \
-                 count_terms, count_host, max_count, counters, g, sa)
-        if (count) {
-            if (gen && shade) PGRT_LAUNCH_P(true, true, true);
-            else if (gen) PGRT_LAUNCH_P(true, true, false);
-            else PGRT_LAUNCH_P(true, false, false);
+        const PrimaryGen g = t.gen ? *t.gen : PrimaryGen{};
+#define PGRT_LAUNCH_P(C, G)                                                                                   \
+    PGRT_TLAUNCH((k_trace_pkt<C, G>), dim3(grid), dim3(kTraceBlock), 0, stream, s, t.ro, t.rd, t.hits,        \
+                 t.count_dev, t.count_terms, t.count_host, max_count, t.counters, g)
+        if (t.count) {
+            if (t.gen) PGRT_LAUNCH_P(true, true); else PGRT_LAUNCH_P(true, false);
         } else {
-            if (gen && shade) PGRT_LAUNCH_P(false, true, true);
-            else if (gen) PGRT_LAUNCH_P(false, true, false);
-            else PGRT_LAUNCH_P(false, false, false);
+            if (t.gen) PGRT_LAUNCH_P(false, true); else PGRT_LAUNCH_P(false, false);
         }
 #undef PGRT_LAUNCH_P
         return true;
     }
-    const int group_max = s.group_max;
-    static const int group8_max = [] {
-        const char* e = getenv("PGRT_GROUP8_MAX");  // r1 A/B: 4 lanes on level 1, 8 below
-        return e ? atoi(e) : 150000;
-    }();
-    {
-        const int exg = expect > 0 && expect < max_count ? expect : max_count;
-        if (allow_group && exg <= group_max && s.depth8 + 1 <= kGroupStack) {
-            // 8 lanes per ray for the smallest queues (the latency floor of the slowest ray),
-            // 4 lanes (two child slots each) when there are enough rays to fill the machine
-            const bool g4 = exg > group8_max;
-#define PGRT_LAUNCH_G(C, G)                                                                                        \
-    PGRT_TLAUNCH((k_trace8g<C, G>), dim3(ceil_div(exg, kTraceBlock / G) > 16384 ? 16384 : ceil_div(exg, kTraceBlock / G)), \
-                       dim3(kTraceBlock), 0, stream, s, ro, rd, hits, count_dev, count_terms, count_host, max_count, counters)
-            if (count) {
-                if (g4) PGRT_LAUNCH_G(true, 4); else PGRT_LAUNCH_G(true, 8);
-            } else {
-                if (g4) PGRT_LAUNCH_G(false, 4); else PGRT_LAUNCH_G(false, 8);
-            }
-#undef PGRT_LAUNCH_G
-            return true;
+    if (t.allow_group && ex <= s.group_max && s.depth8 + 1 <= kGroupStack) {
+        // 8 lanes per ray for the smallest queues (the latency floor of the slowest ray),
+        // 4 lanes (two child slots each) when there are enough rays to fill the machine
+        const bool g4 = ex > kGroup8Max;
+#define PGRT_LAUNCH_G(C, G)                                                                                       \
+    PGRT_TLAUNCH((k_trace8g<C, G>), dim3(std::min(16384, ceil_div(ex, kTraceBlock / G))), dim3(kTraceBlock), 0, \
+                 stream, s, t.ro, t.rd, t.hits, t.count_dev, t.count_terms, t.count_host, max_count, t.counters)
+        if (t.count) {
+            if (g4) PGRT_LAUNCH_G(true, 4); else PGRT_LAUNCH_G(true, 8);
+        } else {
+            if (g4) PGRT_LAUNCH_G(false, 4); else PGRT_LAUNCH_G(false, 8);
         }
+#undef PGRT_LAUNCH_G
+        return true;
     }
-    // rays per wave: full waves for big queues; small (tail) queues may spread thinner
-    static const int tail_rpw = [] {
-        const char* e = getenv("PGRT_TAIL_RPW");
-        return e ? atoi(e) : 64;
-    }();
-    static const int tail_max = [] {
-        const char* e = getenv("PGRT_TAIL_MAX");
-        return e ? atoi(e) : 131072;
-    }();
-    const int ex = expect > 0 && expect < max_count ? expect : max_count;
-    const int rpw = ex <= tail_max ? tail_rpw : 64;
+    const int rpw = ex <= kTailMax ? kTailRpw : 64;
     int grid = ceil_div(ex, (kTraceBlock / 64) * rpw);
-    if (grid > gstack_threads / kTraceBlock) grid = gstack_threads / kTraceBlock;
+    if (grid > t.gstack_threads / kTraceBlock) grid = t.gstack_threads / kTraceBlock;
     // all-LDS stack when the BVH depth fits (depth + 2 entries per lane, <= 64 KB per block)
     const int entries = s.depth + 2;
-    const bool spill = force_spill || entries * kTraceBlock * 4 > 65536;
+    const bool spill = entries * kTraceBlock * 4 > 65536;
     const size_t lds = (size_t)(spill ? kLdsStack : entries) * kTraceBlock * sizeof(int);
-#define PGRT_LAUNCH(C, S)                                                                                   \
-    PGRT_TLAUNCH((k_trace<C, S>), dim3(grid), dim3(kTraceBlock), lds, stream, s, ro, rd, hits, count_dev, \
-                       count_terms, count_host, max_count, gstack, counters, rpw)
-    if (count) {
+#define PGRT_LAUNCH(C, S)                                                                                       \
+    PGRT_TLAUNCH((k_trace<C, S>), dim3(grid), dim3(kTraceBlock), lds, stream, s, t.ro, t.rd, t.hits, t.count_dev, \
+                 t.count_terms, t.count_host, max_count, t.gstack, t.counters, rpw)
+    if (t.count) {
         if (spill) PGRT_LAUNCH(true, true); else PGRT_LAUNCH(true, false);
     } else {
         if (spill) PGRT_LAUNCH(false, true); else PGRT_LAUNCH(false, false);

@@ -26,7 +26,6 @@ struct FrameCounters {
     // statistics only (fire-and-forget atomics), on cache lines of their own so they never
     // serialise with the allocation atomics
     alignas(128) int refract[kMaxLevels];  // refraction rays among the rays of level L
-    alignas(128) int fetch[2 * kMaxLevels];  // work counters of the closest-hit launches (level, shadow)
     // profile == 2: per closest-hit launch {sum node visits, sum triangle tests, max visits of
     // one ray, max tests of one ray}; [0, kMaxLevels) level queues, [kMaxLevels, 2k) shadows
     alignas(128) unsigned long long trav[2 * kMaxLevels][16];  // visits, tests, max visits, max tests, max wave iterations
@@ -87,18 +86,35 @@ struct ShadowQueue {  // one per batch: the shadow rays of every level, level-ma
     int cap;
 };
 
-// fetch: a zeroed device int per launch (persistent waves pull 64 rays per atomic).
-// Ray count: sum of count_dev[0 .. count_terms) when count_dev is set, else count_host.
-// returns false when nothing was launched (max_count <= 0)
+// One closest-hit launch over a ray queue (ro/rd in, hits out).  Ray count: the sum of
+// count_dev[0], count_dev[2], ... (count_terms words, stride 2: FrameCounters::alloc) clamped to
+// max_count when count_dev is set, else count_host.  expect sizes the grid only (counts live on
+// the device; last frame's count avoids dispatching empty workgroups).  Kernel choice: gen
+// (level 0: rays generated in registers) or packets -> wave packets over the binary BVH; queues
+// of <= group_max rays (allow_group) -> 8 / 4 lanes per ray over the 8-wide BVH; else one lane
+// per ray.  count: profile == 2 traversal counters into counters[16].
 struct PrimaryGen;  // camera_ops.hpp
-struct ShadeArgs;   // shade_ray.hpp
-// the level-0 packet traversal is used for coherent queues (and can regenerate primary rays)
-bool trace_packets_available(const SceneView& s, bool coherent);
-bool launch_trace(const SceneView& s, const float4* ro, const float4* rd, float4* hits, const int* count_dev,
-                  int count_host, int max_count, int* fetch, int* gstack, int gstack_threads,
-                  unsigned long long* counters, bool count, hipStream_t stream, int expect = 0,
-                  int count_terms = 1, bool allow_group = true, bool coherent = false,
-                  const PrimaryGen* gen = nullptr, const ShadeArgs* shade = nullptr);
+struct TraceLaunch {
+    const float4* ro = nullptr;
+    const float4* rd = nullptr;
+    float4* hits = nullptr;
+    const int* count_dev = nullptr;
+    int count_terms = 1;
+    int count_host = 0;
+    int max_count = 0;
+    int expect = 0;
+    int* gstack = nullptr;  // per-thread global stack region (one-lane kernels)
+    int gstack_threads = 0;
+    unsigned long long* counters = nullptr;
+    bool count = false;
+    bool allow_group = true;
+    bool packets = false;
+    const PrimaryGen* gen = nullptr;
+};
+// the packet traversal needs the binary layout and a tree that fits its wave-uniform stack
+bool trace_packets_available(const SceneView& s);
+// returns false when nothing was launched (max_count <= 0)
+bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream);
 // events the next launch_trace records at its kernel's start / end (nullptr: none)
 void set_trace_events(hipEvent_t start, hipEvent_t stop);
 int trace_block_size();
@@ -111,8 +127,7 @@ void launch_occluded(const SceneView& s, const float4* ro, const float4* rd, int
 void launch_raygen(const CameraView& cam, const FrameParams& fp, const int4* tiles, Queue q, int n0,
                    FrameCounters* fc, hipStream_t stream);
 void launch_shade(const SceneView& s, const FrameParams& fp, int level, Queue q, Queue next, LevelNodes nodes,
-                  ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect = 0,
-                  const PrimaryGen* gen = nullptr);  // gen: level 0 regenerates its rays (max_count of them)
+                  ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect = 0);
 // level L's final colours from its shadow hits and level L+1's colours (child)
 void launch_combine(const SceneView& s, int level, LevelNodes nodes, const float4* child, ShadowQueue sq,
                     const FrameCounters* fc, int max_count, hipStream_t stream, int expect = 0);
@@ -135,11 +150,10 @@ void launch_unpack_tiles(const float* gathered, float* rgba, int width, int heig
                          int channels, hipStream_t stream, int frames = 1, int frame0 = 0, int nframes = 1);
 
 // scene / BVH build
-constexpr int kBuilderLbvh = 0;  // Karras 2012 over 63-bit Morton codes
-constexpr int kBuilderPloc = 1;  // PLOC clustering over the same Morton order + SAH collapse
-constexpr float kDefaultSplitBeta = 0.0f;  // PGRT_SPLIT default (extra references / triangles)
-constexpr int kDefaultSlots = 2;           // PGRT_SLOTS default: staggered pipeline slots per frame
-constexpr int kDefaultGroupMax = 400000;   // PGRT_GROUP_MAX default: queues up to this many rays use
+constexpr int kBuilderLbvh = PGRT_BVH_LBVH;  // Karras 2012 over 63-bit Morton codes
+constexpr int kBuilderPloc = PGRT_BVH_PLOC;  // PLOC clustering over the same Morton order + SAH collapse
+constexpr int kDefaultSlots = 2;           // pipeline slots of a synchronous frame (r1 A/B: 2 > 1, 3)
+constexpr int kDefaultGroupMax = 400000;   // pgrt_config.group_max default: queues up to this many rays use
                                            // the 8-lanes-per-ray kernel (r1 A/B: tail levels -45 %)
 constexpr int kDefaultGroupMaxInFlight = 100000;  // with frames in flight the concurrent frames hide
                                                   // the latency floors: level 2 (~150k rays) runs

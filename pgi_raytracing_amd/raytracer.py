@@ -43,6 +43,8 @@ def lib():
         "pgrt_create": (ip, [ip, C.POINTER(vp)]),
         "pgrt_destroy": (None, [vp]),
         "pgrt_last_error": (C.c_char_p, [vp]),
+        "pgrt_get_config": (ip, [vp, C.POINTER(abi.Config)]),
+        "pgrt_set_config": (ip, [vp, C.POINTER(abi.Config)]),
         "pgrt_set_scene": (ip, [vp, C.POINTER(abi.SceneDesc)]),
         "pgrt_bvh_get_info": (ip, [vp, C.POINTER(abi.BvhInfo)]),
         "pgrt_set_camera": (ip, [vp, C.POINTER(abi.Camera)]),
@@ -129,6 +131,26 @@ class Context:
 
     def __del__(self):
         self.close()
+
+    def get_config(self) -> abi.Config:
+        cfg = abi.Config()
+        _check(self.h, self.L.pgrt_get_config(self.h, C.byref(cfg)))
+        return cfg
+
+    def configure(self, **kw) -> abi.Config:
+        """pgrt_set_config with the given fields changed (others kept); returns the previous config.
+        BVH fields take effect at the next set_scene."""
+        old = self.get_config()
+        cfg = abi.Config.from_buffer_copy(old)
+        for k, v in kw.items():
+            if not hasattr(cfg, k):
+                raise AttributeError(f"pgrt_config has no field {k}")
+            setattr(cfg, k, v)
+        _check(self.h, self.L.pgrt_set_config(self.h, C.byref(cfg)))
+        return old
+
+    def set_config(self, cfg: abi.Config):
+        _check(self.h, self.L.pgrt_set_config(self.h, C.byref(cfg)))
 
     def set_scene(self, scene: Scene):
         d = scene.desc()

@@ -197,22 +197,20 @@ def test_distributed_world1_equals_render(gpu_ctx, avenger_scene):
 
 
 @pytest.mark.parametrize("builder,width,split,group", [
-    ("lbvh", "2", "0", "0"), ("ploc", "8", "0", "0"), ("lbvh", "8", "0", "0"), ("ploc", "2", "0", "0"),
-    ("ploc", "2", "1.0", "0"), ("ploc", "8", "0.5", "0"),
-    ("ploc", "2", "0", "1000000000"), ("lbvh", "2", "0.5", "1000000000"), ("ploc", "2", "0.5", "1000000000")])
-def test_bvh_layouts_bit_exact(gpu_ctx, avenger_scene, monkeypatch, builder, width, split, group):
-    """Every BVH builder / traversal layout / split budget gives the same closest hits and
-    frames: the hit is order-independent (ties to the smaller triangle index, conservative box
-    tests), and split references cover their triangle."""
-    monkeypatch.setenv("PGRT_BVH", builder)
-    monkeypatch.setenv("PGRT_BVH_WIDTH", width)
-    monkeypatch.setenv("PGRT_SPLIT", split)
-    monkeypatch.setenv("PGRT_GROUP_MAX", group)  # 8 lanes per ray over the 8-wide BVH for queues <= group
+    (abi.PGRT_BVH_LBVH, 2, 0.0, -1), (abi.PGRT_BVH_PLOC, 8, 0.0, -1), (abi.PGRT_BVH_LBVH, 8, 0.0, -1),
+    (abi.PGRT_BVH_PLOC, 2, 0.0, -1), (abi.PGRT_BVH_PLOC, 2, 1.0, -1), (abi.PGRT_BVH_PLOC, 8, 0.5, -1),
+    (abi.PGRT_BVH_PLOC, 2, 0.0, 1 << 30), (abi.PGRT_BVH_LBVH, 2, 0.5, 1 << 30), (abi.PGRT_BVH_PLOC, 2, 0.5, 1 << 30)])
+def test_bvh_layouts_bit_exact(gpu_ctx, avenger_scene, builder, width, split, group):
+    """Every BVH builder / traversal layout / split budget (pgrt_config) gives the same closest
+    hits and frames: the hit is order-independent (ties to the smaller triangle index,
+    conservative box tests), and split references cover their triangle.  group: queues up to it
+    take 8 (4) lanes per ray over the 8-wide BVH (-1 never)."""
+    old = gpu_ctx.configure(bvh_builder=builder, bvh_width=width, split_beta=split, group_max=group)
     try:
         gpu_ctx.set_scene(avenger_scene)
         info = gpu_ctx.bvh_info()
-        assert info.width == int(width) and info.builder == (0 if builder == "lbvh" else 1)
-        if builder == "ploc" and float(split) > 0:
+        assert info.width == width and info.builder == builder
+        if builder == abi.PGRT_BVH_PLOC and split > 0:
             assert info.num_references > info.num_triangles
         else:
             assert info.num_references == info.num_triangles
@@ -229,23 +227,18 @@ def test_bvh_layouts_bit_exact(gpu_ctx, avenger_scene, monkeypatch, builder, wid
         _, exact = assert_frames_match(img, ref)
         assert exact == 1.0
     finally:
-        monkeypatch.delenv("PGRT_BVH")
-        monkeypatch.delenv("PGRT_BVH_WIDTH")
-        monkeypatch.delenv("PGRT_SPLIT")
-        monkeypatch.delenv("PGRT_GROUP_MAX")
+        gpu_ctx.set_config(old)
         gpu_ctx.set_scene(avenger_scene)
 
 
-@pytest.mark.parametrize("fused,packets", [("0", "0"), ("1", "0"), ("2", "0"), ("2", "2"), ("3", "2"), ("3", "9"),
-                                            ("2", "-1")])
-def test_pipeline_modes_bit_exact(gpu_ctx, avenger_scene, monkeypatch, fused, packets):
-    """Every level-0 ray mode (k_raygen queue / regenerated in trace + shade / stored by the
-    packet traversal / traversal + shade fused) and every packet-traversal depth renders the
-    oracle's frame bit for bit, frames in flight and batched frames included."""
-    monkeypatch.setenv("PGRT_FUSED_RAYGEN", fused)
-    monkeypatch.setenv("PGRT_PACKET_LEVELS", packets)
+@pytest.mark.parametrize("packets", [abi.PGRT_PACKETS_OFF, 1, abi.PGRT_PACKETS_AUTO, 16])
+def test_packet_levels_bit_exact(gpu_ctx, avenger_scene, packets):
+    """Every packet-traversal depth (none: k_raygen + one lane per ray; level 0 only, which
+    generates its rays in the traversal; the default; every level) renders the oracle's frame
+    bit for bit, frames in flight and batched frames included."""
+    gpu_ctx.set_scene(avenger_scene)
+    old = gpu_ctx.configure(packet_levels=packets)
     try:
-        gpu_ctx.set_scene(avenger_scene)
         W, H = 96, 64
         cam = abi.default_camera(W, H)
         gpu_ctx.set_camera(cam)
@@ -270,9 +263,7 @@ def test_pipeline_modes_bit_exact(gpu_ctx, avenger_scene, monkeypatch, fused, pa
             gpu_ctx.set_frames_in_flight(1)
             gpu_ctx.free(buf)
     finally:
-        monkeypatch.delenv("PGRT_FUSED_RAYGEN")
-        monkeypatch.delenv("PGRT_PACKET_LEVELS")
-        gpu_ctx.set_scene(avenger_scene)
+        gpu_ctx.set_config(old)
 
 
 def test_occluded_matches_closest_hit(gpu_ctx, avenger_scene):
