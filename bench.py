@@ -4,33 +4,38 @@
 
 One step = one frame of BASELINE config C2 (avenger-proxy, 1920x1080, 1 spp pinhole, Whitted
 depth 5, spherical env map) rendered into an HBM-resident framebuffer (--config C3/C4/C5 select
-the other BASELINE configs for the records in DESIGN.md).  N > 1: one process
-per GPU (torch.distributed launcher env), 64x64 image tiles dealt round-robin to ranks, one
-ncclGather (RCCL over xGMI) to rank 0 and an unpack kernel there -- the total frame is fixed
-(strong scaling).  Rays = every closest-hit query (primary + shadow + reflect + refract).
-Frames are submitted in batches of --frames-per-call consecutive frames (one launch sequence
-covers all of them, pgrt_render_frames_device_async; every frame is fully traced into its own
-framebuffer) with up to --in-flight calls overlapping on the device (throughput = ms_per_step);
-the latency of one synchronous frame is reported beside it (frame_latency_ms).
+the other BASELINE configs).  Rays = every closest-hit query (primary + shadow + reflect +
+refract).  Frames are submitted in batches of --frames-per-call consecutive frames (one launch
+sequence covers all of them, pgrt_render_frames_device_async; every frame is fully traced into
+its own framebuffer) with up to --in-flight calls overlapping on the device (throughput =
+ms_per_step); the latency of one synchronous frame is reported beside it (frame_latency_ms).
+
+N > 1 GPUs: one process per GPU.  `python bench.py --gpus N` without a launcher environment starts
+the N rank processes itself (subprocess, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set; this
+parent never touches a GPU); under torch.distributed.run the ranks come from the environment.
+64x64 image tiles are dealt to ranks (csrc/tiles.hpp), every rank renders its tiles of the
+call's frames, ONE ncclGather (RCCL over xGMI, libpgrt's own communicator) moves them to rank
+0, where one kernel unpacks every frame into its framebuffer.  The frame is fixed as N grows
+(strong scaling); value = all ranks' rays / the max over ranks of the timed region.
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from collections import deque
-
-import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 # one hardware queue per frame in flight (+ the context stream): HIP's default of 4 would make
 # frames share queues; read by the HIP runtime at its initialisation, i.e. before libpgrt loads
 # (r1i C2, 8 frames per call: 8 queues / 6 in flight 0.197 ms; 12 / 6 0.191; 12 / 8 0.186;
-# 16 / 8-14 0.185-0.187)
-# (the GPU boxes export GPU_MAX_HW_QUEUES=4, HIP's default: raise it, a setdefault would not)
+# 16 / 8-14 0.185-0.187).  The GPU boxes export GPU_MAX_HW_QUEUES=4 (HIP's default): raise it.
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
     os.environ["GPU_MAX_HW_QUEUES"] = "16"
 sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -42,25 +47,27 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # triangle record: v0|id, e1, e2)
 RAY_BYTES, NODE_BYTES, WIDE_NODE_BYTES, TRI_BYTES = 48, 64, 80, 48
 
-
-# BASELINE.json configs (SURVEY.md §8d "Concrete inputs"); C2 is the headline bench line, the
-# others are measured with --config and recorded in DESIGN.md / profiles/
+# BASELINE.json configs (SURVEY.md §8d "Concrete inputs"); C2 is the headline bench line
 CONFIGS = {
     "C2": dict(width=1920, height=1080, max_level=5, spp_side=1, dof=0, scene="avenger", in_flight=8),
-    # (r1h after the counter-zeroing fix: C3 14.4 / 15.0 / 12.6 ms at 2 / 4 / 6 in flight)
+    # r1h: C3 14.4 / 15.0 / 12.6 ms at 2 / 4 / 6 in flight
     "C3": dict(width=1920, height=1080, max_level=5, spp_side=8, dof=1, scene="avenger"),
+    # r2a: 47.4 ms/frame at 6 in flight (32 sample batches per frame, no batch bound)
     "C4": dict(width=3840, height=2160, max_level=5, spp_side=8, dof=1, scene="avenger"),
     # r1h: 23.4 / 23.8 / 22.3 ms at 2 / 4 / 6 in flight
     "C5": dict(width=4096, height=4096, max_level=8, spp_side=1, dof=0, scene="random1m"),
 }
+# PMC-measured HBM traffic per closest-hit launch of the bench's profiled configuration
+# (tools/profile.sh + tools/traffic.py, committed under profiles/)
+TRAFFIC = {"C2": "profiles/r2/traffic_C2.json", "C5": "profiles/r2/traffic_C5.json"}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # frames timed; default 600 x world (N GPUs batch 8 x N frames per call: 75 calls either way,
-    # ~10x the 8 calls in flight, so pipeline fill and drain stay a small part of the timed region
-    # at every N; r1i C2: 200 frames 0.207 ms/frame, 960 frames 0.186)
+    # frames timed; default for C2 600 x world (N GPUs batch 8 x N frames per call: 75 calls
+    # either way, ~10x the 8 calls in flight, so pipeline fill and drain stay a small part of the
+    # timed region at every N; r1i C2: 200 frames 0.207 ms/frame, 960 frames 0.186)
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
@@ -74,11 +81,13 @@ def parse():
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the profiled roofline frames (the run profiles/ rocprofv3 summaries are taken of)")
     ap.add_argument("--in-flight", type=int, default=None,
-                    help="frames in flight (pgrt_set_frames_in_flight); default 6 (r1 scan, tools/inflight_scan.py)")
+                    help="calls in flight (pgrt_set_frames_in_flight); default 8 for C2, 6 otherwise")
     ap.add_argument("--frames-per-call", type=int, default=None,
-                    help="frames per submission (pgrt_render_frames_*_async, 1..64); default 8 x world for C2, 1 otherwise (r1e scans)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+                    help="frames per submission (pgrt_render_frames_*_async, 1..64); default 8 x world for C2, "
+                         "1 otherwise (r1e scans)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (multi-thread leg)")
+    ap.add_argument("--packet-levels", type=int, default=None,
+                    help="A/B only: pgrt_config.packet_levels (default AUTO: chosen per level by libpgrt)")
     a = ap.parse_args()
     for k, v in CONFIGS[a.config].items():
         if getattr(a, k, None) is None:
@@ -86,12 +95,136 @@ def parse():
     return a
 
 
+# ------------------------------------------------------------------ rank launcher (N > 1)
+
+def visible_gpus() -> int:
+    """GPUs this process may use, without initialising HIP: the *_VISIBLE_DEVICES lists, else the
+    KFD topology nodes that have SIMDs (the GPU agents)."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip() != ""])
+    n = 0
+    for f in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+        try:
+            with open(f) as fh:
+                props = dict(line.split() for line in fh if len(line.split()) == 2)
+            n += int(props.get("simd_count", "0")) > 0
+        except (OSError, ValueError):
+            pass
+    return n
+
+
+def launch_ranks(n: int) -> int:
+    """Start N rank processes of this script (fresh processes: this one never touched a GPU) and
+    forward rank 0's stdout; the first failing rank stops the others."""
+    have = visible_gpus()
+    if have < n:
+        print(f"bench.py: --gpus {n} needs {n} GPUs, {have} visible on this node", file=sys.stderr)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else sys.stderr))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:  # the others would wait for the failed rank forever
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+# ------------------------------------------------------------------ CPU baseline
+
+def cpu_share() -> dict:
+    """Host cores: the machine's (nproc), this process's affinity mask and the cgroup CPU quota;
+    the baseline runs on all cores this process may use."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        info["affinity"] = os.cpu_count()
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, period = fh.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    info["cgroup_quota"] = quota
+    info["omp_num_threads"] = os.environ.get("OMP_NUM_THREADS")
+    info["threads"] = max(1, min(info["affinity"] or 1, int(quota) if quota else 1 << 30))
+    return info
+
+
+def cpu_baseline(args, scene, cam, params):
+    """The CPU restatement (oracle/, test infrastructure: timed only here) on the host cores.
+    C2: whole frames until the budget is spent; C3-C5: every 16th row."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle  # cpu_baseline leg only: the checker, timed as the baseline
+
+    share = cpu_share()
+    threads = share["threads"]
+    t0 = time.perf_counter()
+    osc = pyoracle.OracleScene(scene)
+    build_s = time.perf_counter() - t0
+    row_step = 1 if args.config == "C2" else 16
+
+    def timed(nthreads, budget_s):
+        frames = rays_c = 0
+        t1 = time.perf_counter()
+        while True:
+            _, sc = osc.render(cam, params, row_step=row_step, threads=nthreads)
+            rays_c += sc.rays()
+            frames += 1
+            dt_c = time.perf_counter() - t1
+            if dt_c >= budget_s:
+                return rays_c / dt_c / 1e6, frames, rays_c, dt_c
+
+    what = "whole C2 frames" if row_step == 1 else f"{args.config} frames, every 16th row"
+    v_mt, f_mt, r_mt, t_mt = timed(threads, args.cpu_seconds)
+    v_st, f_st, r_st, t_st = timed(1, args.cpu_seconds / 2)
+    return {"value": round(v_mt, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{f_mt} x {what} ({r_mt} rays, {t_mt:.1f} s) on {threads} host threads (OpenMP over rows); "
+                      f"oracle/ CPU restatement with its own SAH BVH (built in {build_s:.1f} s, not timed)",
+            "host": share,
+            "single_thread_value": round(v_st, 3),
+            "single_thread_sample": f"{f_st} x {what} ({r_st} rays, {t_st:.1f} s), 1 thread (the reference's "
+                                    f"single Producer thread)"}
+
+
+def workload(args) -> str:
+    return (f"{args.config} {'avenger-proxy' if args.scene == 'avenger' else '1M random triangles'} "
+            f"{args.width}x{args.height} Whitted d={args.max_level} + env map, "
+            f"{args.spp_side ** 2} spp {'DoF' if args.dof else 'pinhole'}")
+
+
+# ------------------------------------------------------------------ main
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     if args.steps is None:
-        args.steps = 600 * world
+        args.steps = 600 * world if args.config == "C2" else 20
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
@@ -117,96 +250,99 @@ def main():
     params = abi.make_params(spp_side=args.spp_side, max_level=args.max_level, dof=args.dof,
                              jitter=abi.PGRT_JITTER_HASH if (args.spp_side > 1 or args.dof) else abi.PGRT_JITTER_NONE)
     ctx = Context(local_rank)
+    if args.packet_levels is not None:
+        ctx.configure(packet_levels=args.packet_levels)
     ctx.set_scene(scene)
     ctx.set_camera(cam)
     bvh = ctx.bvh_info()
     # frames per call: ~22 M rays per call per rank (8 C2 frames on 1 GPU, 8 x world frames of a
     # rank's 1/world share at N GPUs); r1e scans: N=1 F=8 0.255 ms/frame (F=16 with 6 in flight
     # 0.39), emulated N=8 rank F=64 0.040 ms/frame (F=16 0.045)
-    # (C3/C4/C5 frames are 15-80x heavier than C2's and fill the GPU on their own: 1 per call)
+    # (C3/C4/C5 frames are 15-250x heavier than C2's and fill the GPU on their own: 1 per call)
     F = max(1, min(64, args.frames_per_call or (8 * world if args.config == "C2" else 1)))
     fb = ctx.alloc(F * args.width * args.height * 16) if rank == 0 or world == 1 else None
+    comm_ranks = 1
     if world > 1:
         uid = [Context.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(world, rank, uid[0])
+        comm_ranks, _ = ctx.comm_info()
 
     def frame(p):  # synchronous frame (latency, profiled frames)
         if world > 1:
             return ctx.render_distributed_device(p, fb)
         return ctx.render_device(p, fb)
 
-    # frames in flight: a step is one whole frame (every rank's tiles rendered, gathered and
-    # unpacked on rank 0); up to `in_flight` consecutive frames overlap on the device, so one
-    # frame's latency-bound deep levels share the CUs with the next frame's wide levels
-    # (r1g measured C5 at 175 ms/frame with 6 in flight: a new frame set's counters were zeroed
-    # by a NULL-stream hipMemset racing the slot streams, fixed in r1h)
+    # calls in flight: a step is one whole frame (every rank's tiles rendered, gathered and
+    # unpacked on rank 0); up to `in_flight` calls overlap on the device, so one call's
+    # latency-bound deep levels share the CUs with the next call's wide levels
     in_flight = args.in_flight or CONFIGS[args.config].get("in_flight", 6)
     ctx.set_frames_in_flight(in_flight)
+    gather_ms = []
 
-    def run_frames(n):
+    def run_frames(n, record=False):
         pending, rays_n = deque(), 0
+
+        def wait_one():
+            st = ctx.render_wait(pending.popleft())
+            if record and world > 1:
+                gather_ms.append(st.ms_gather)
+            return st.rays()
+
         for f0 in range(0, n, F):
             nf = min(F, n - f0)
             pending.append(ctx.render_frames_distributed_device_async(params, nf, fb) if world > 1
                            else ctx.render_frames_device_async(params, nf, fb))
             if len(pending) >= in_flight:
-                rays_n += ctx.render_wait(pending.popleft()).rays()
+                rays_n += wait_one()
         while pending:
-            rays_n += ctx.render_wait(pending.popleft()).rays()
+            rays_n += wait_one()
         return rays_n
 
+    warmup_requested = args.warmup
     if args.roofline_only:
         args.warmup = args.steps = 0
-    if not args.roofline_only:  # every frame set is allocated and warm before the timed region
+    else:  # every frame set is allocated and warm before the timed region
         args.warmup = max(args.warmup, in_flight * F)
     run_frames(args.warmup)
     ctx.synchronize()
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
-    rays = run_frames(args.steps)
+    rays = run_frames(args.steps, record=True)
     ctx.synchronize()
+    elapsed = time.perf_counter() - t0
     if dist:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
     # frame latency (one synchronous frame at a time), reported beside the throughput
-    lat = [0.0]
+    lat = []
     for _ in range(min(args.steps, 30)):
         t1 = time.perf_counter()
         frame(params)
         lat.append(time.perf_counter() - t1)
-    lat = lat[1:] or lat
-    latency_ms = sorted(lat)[len(lat) // 2] * 1e3
-    if dist:
-        import torch
-
-        lt = torch.tensor([latency_ms], dtype=torch.float64)
-        dist.all_reduce(lt, op=dist.ReduceOp.MAX)
-        latency_ms = float(lt.item())
+    latency_ms = sorted(lat)[len(lat) // 2] * 1e3 if lat else None
     total_rays = rays
+    per_rank_ms = [elapsed / max(1, args.steps) * 1e3]
     if dist:
-        import torch
-
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        r = torch.tensor([rays], dtype=torch.float64)
-        dist.all_reduce(r, op=dist.ReduceOp.SUM)
-        total_rays = int(r.item())
+        g = [None] * world
+        dist.all_gather_object(g, {"elapsed": elapsed, "rays": rays, "latency_ms": latency_ms})
+        per_rank_ms = [x["elapsed"] / max(1, args.steps) * 1e3 for x in g]
+        elapsed = max(x["elapsed"] for x in g)  # max over ranks
+        total_rays = sum(x["rays"] for x in g)
+        latency_ms = max(x["latency_ms"] or 0.0 for x in g)
 
     roof = None
     if not args.no_roofline:
         # live per-kernel timing: HIP events on libpgrt's own stream around every closest-hit
-        # launch (profile=1), and the instrumented traversal counts (profile=2, separate frame)
-        # (1 GPU: the timed configuration, F frames per launch sequence)
+        # launch (profile=1), and the instrumented traversal counts (profile=2, separate call)
+        # (1 GPU: the timed configuration, F frames per launch sequence; N GPUs: one frame)
         def prof_call(p):
             return ctx.render_frames_device(p, F, fb) if world == 1 else frame(p)
 
         frames_per_prof = F if world == 1 else 1
         p1 = abi.RenderParams.from_buffer_copy(params)
         p1.profile = 1
-        reps = 5
+        reps = 5 if args.config == "C2" else 2
         ms_trace = 0.0
         launches = 0
         for _ in range(reps):
@@ -228,8 +364,8 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None,
-            "kernel": "closest hit: k_trace_pkt (wave packets, levels 0-2; level 0 generates its rays) + k_trace "
-                      "(one lane per ray, levels 3-5 and the shadow queue)",
+            "kernel": "closest hit: k_trace_pkt (wave packets; level 0 generates its rays) + k_trace / k_trace8g "
+                      "(one / 8 lanes per ray: deeper levels, the shadow queue)",
             "avg_launch_ms": round(avg_launch_ms, 4),
             "frames_per_launch": frames_per_prof,
             "launches_per_call": launches // reps,
@@ -239,16 +375,21 @@ def main():
             "tri_tests_per_ray": round(s2.tri_tests / max(1, frame_rays), 2),
             "bytes_per_ray": round(alg_bytes / max(1, frame_rays), 1),
         }
-        tf = os.path.join(ROOT, "profiles", "traffic_c2.json")
-        if args.config == "C2" and os.path.exists(tf):
-            try:
-                roof["traffic"] = json.load(open(tf)).get("bytes_per_launch")
-            except Exception:  # noqa: BLE001
-                pass
+        tf = os.path.join(ROOT, TRAFFIC.get(args.config, "-"))
+        if world == 1 and os.path.exists(tf):
+            with open(tf) as fh:
+                t = json.load(fh)
+            roof["traffic"] = t.get("bytes_per_launch")
+            roof["traffic_source"] = f"{TRAFFIC[args.config]} ({t.get('round')}; FETCH_SIZE x2 + WRITE_SIZE per launch)"
+            roof["traffic_frac"] = round(roof["traffic"] / (avg_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            if t.get("valu_issue"):
+                roof["valu_issue"] = t["valu_issue"]
+                roof["valu_issue_note"] = t.get("valu_issue_note")
 
     if args.roofline_only:
         if rank == 0:
-            print(json.dumps({"metric": METRIC, "config": args.config, "roofline": roof}), flush=True)
+            print(json.dumps({"metric": METRIC, "config": args.config, "workload": workload(args), "roofline": roof}),
+                  flush=True)
         if dist:
             dist.barrier()
             dist.destroy_process_group()
@@ -261,38 +402,14 @@ def main():
         for _ in range(2):
             ctx.render(params)
         t1 = time.perf_counter()
-        nh = max(3, args.steps // 2)
+        nh = max(3, min(args.steps // 2, 100))
         for _ in range(nh):
             ctx.render(params)
         host_fb = round((time.perf_counter() - t1) / nh * 1e3, 4)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.scene == "avenger":
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import pyoracle  # cpu_baseline leg only: the CPU restatement timed on the host cores
-
-        osc = pyoracle.OracleScene(scene)
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-
-        def timed(nthreads, budget_s):  # whole C2 frames, repeated until the budget is spent
-            frames = rays_c = 0
-            t1 = time.perf_counter()
-            while True:
-                _, sc = osc.render(cam, params, row_step=1, threads=nthreads)
-                rays_c += sc.rays()
-                frames += 1
-                dt_c = time.perf_counter() - t1
-                if dt_c >= budget_s:
-                    return rays_c / dt_c / 1e6, frames, rays_c, dt_c
-
-        v_mt, f_mt, r_mt, t_mt = timed(threads, args.cpu_seconds)
-        v_st, f_st, r_st, t_st = timed(1, args.cpu_seconds / 2)
-        cpu = {"value": round(v_mt, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-               "sample": f"{f_mt} whole C2 frames ({r_mt} rays, {t_mt:.1f} s) on {threads} host threads "
-                         f"(OpenMP over rows); oracle/ CPU restatement with its own SAH BVH",
-               "single_thread_value": round(v_st, 3),
-               "single_thread_sample": f"{f_st} frames ({r_st} rays, {t_st:.1f} s), 1 thread (the reference's "
-                                       f"single Producer thread)"}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, scene, cam, params)
 
     if rank == 0:
         out = {
@@ -302,10 +419,13 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_requested": warmup_requested,
+            "warmup_note": "raised to in_flight x frames_per_call so every frame set is allocated and warm "
+                           "before the timed region",
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "frames_in_flight": in_flight,
             "frames_per_call": F,
-            "frame_latency_ms": round(latency_ms, 4),
+            "frame_latency_ms": round(latency_ms, 4) if latency_ms else None,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -313,14 +433,16 @@ def main():
             "data": ("synthetic: avenger-proxy OBJ (reference OBJ absent) + spherical_map_windows.jpg"
                      if args.scene == "avenger" else "synthetic: 10^6 random triangles (seed 42) + env map"),
             "config": {
-                "workload": f"{args.config} {'avenger-proxy' if args.scene == 'avenger' else '1M random triangles'} "
-                            f"{args.width}x{args.height} Whitted d={args.max_level} + env map, "
-                            f"{args.spp_side ** 2} spp {'DoF' if args.dof else 'pinhole'}",
+                "workload": workload(args),
                 "triangles": bvh.num_triangles,
                 "rays_per_frame": int(total_rays / args.steps),
                 "parallelism": f"image tiles 64x64 over {world} GPU(s), ncclGather to rank 0" if world > 1
                 else "1 GPU",
             },
+            "world": world,
+            "rccl_ranks": comm_ranks,
+            "per_rank_ms_per_step": [round(x, 4) for x in per_rank_ms],
+            "gather_ms_per_call": round(sum(gather_ms) / len(gather_ms), 4) if gather_ms else None,
             "roofline": roof,
             "host_framebuffer_ms_per_step": host_fb,
             "cpu_baseline": cpu,

@@ -132,9 +132,11 @@ typedef struct pgrt_stats {
     double ms_total;                 /* host wall time of the call */
     /* profile >= 1: ms_trace = every closest-hit launch (level queues + the shadow queue);
      * ms_shadow = the shadow-queue launch alone (a part of ms_trace); ms_combine = the finish
-     * kernel (shadow resolve + bottom-up combine + sample accumulation + gamma); ms_resolve =
-     * 0 (the resolve is part of the finish kernel); ms_gather = host wall time of the RCCL
-     * gather + tile unpack (distributed calls) */
+     * kernel (shadow resolve + bottom-up combine + sample accumulation + gamma).
+     * Distributed frames: ms_gather = device time of the ncclGather (including the wait for the
+     * slowest rank) + rank 0's tile unpack, ms_resolve = the unpack alone (asynchronous frames,
+     * reported by pgrt_render_wait); the synchronous pgrt_render_distributed* report the host
+     * wall time of gather + unpack as ms_gather. */
     double ms_raygen, ms_trace, ms_shade, ms_shadow, ms_combine, ms_resolve, ms_gather;
     int trace_launches;              /* launches of the closest-hit kernel in ms_trace */
     int levels;                      /* trace levels executed */
@@ -269,6 +271,9 @@ int pgrt_unpack_tiles_host(int width, int height, int tile_size, int world,
                            const float* gathered, float* rgba);
 int pgrt_comm_unique_id(char id[128]);
 int pgrt_comm_init(pgrt_ctx* ctx, int world, int rank, const char id[128]);
+/* The communicator's rank count and this context's rank as RCCL reports them (ncclCommCount /
+ * ncclCommUserRank); without a communicator the context's world / rank (1 / 0 by default). */
+int pgrt_comm_info(const pgrt_ctx* ctx, int* nranks, int* rank);
 /* Rank-local half of the distributed render, for callers that gather with their own
  * communicator: render the tiles of `rank` (of `world`) of the camera image into a tile-compact
  * device buffer of pgrt_tile_count(W, H, 64, rank, world) * 64 * 64 * 4 floats (local tile j is
@@ -326,6 +331,9 @@ typedef struct pgrt_level_diag {
     uint64_t wide_visits;         /* the part of visits that were 8-wide nodes */
     double ms_trace, ms_shade;    /* this level's launches (profile >= 1 on the call; summed
                                      over sample batches) */
+    uint64_t packet_steps_hit;    /* levels traced as wave packets (sampled blocks): lane-steps
+                                     at which the lane's ray hit a child box of the wave's node */
+    uint64_t packet_steps_live;   /* ... and live lane-steps; hit / live = packet utilisation */
 } pgrt_level_diag;
 int pgrt_frame_diag(const pgrt_ctx* ctx, pgrt_level_diag* out, int max_levels);
 

@@ -160,7 +160,9 @@ class LevelDiag(C.Structure):
                                           "shadow_visits", "shadow_tests", "shadow_max_visits", "shadow_max_tests",
                                           "max_wave_iterations", "max_ray_ticks", "stack_spills", "max_stack",
                                           "lr_visits", "lr_tests", "lr_leaves", "lr_node_cyc64", "lr_leaf_cyc64",
-                                          "lr_load_cyc64", "wide_visits")] + [("ms_trace", C.c_double), ("ms_shade", C.c_double)]
+                                          "lr_load_cyc64", "wide_visits")] + [("ms_trace", C.c_double), ("ms_shade", C.c_double),
+                                                                  ("packet_steps_hit", C.c_uint64),
+                                                                  ("packet_steps_live", C.c_uint64)]
 
 
 class BvhInfo(C.Structure):

@@ -183,11 +183,21 @@ struct FrameSet {
     int cam_w = 0, cam_h = 0;  // image size at submission (the gather's layout)
     pgrt_stats stats{};
     std::chrono::steady_clock::time_point t0;
-    FrameSet() { PGRT_HIP(hipEventCreateWithFlags(&ev_ready, hipEventDisableTiming)); }
+    // distributed frames: device time of the gather (ncclGather, including the wait for the
+    // slowest peer) and of rank 0's unpack, read when the frame is waited for
+    hipEvent_t ev_g0 = nullptr, ev_g1 = nullptr, ev_g2 = nullptr;
+    bool gather_timed = false;
+    FrameSet() {
+        PGRT_HIP(hipEventCreateWithFlags(&ev_ready, hipEventDisableTiming));
+        PGRT_HIP(hipEventCreate(&ev_g0));
+        PGRT_HIP(hipEventCreate(&ev_g1));
+        PGRT_HIP(hipEventCreate(&ev_g2));
+    }
     ~FrameSet() {
         for (auto& s : slots)
             if (s->stream) (void)hipStreamSynchronize(s->stream);
-        if (ev_ready) (void)hipEventDestroy(ev_ready);
+        for (hipEvent_t e : {ev_ready, ev_g0, ev_g1, ev_g2})
+            if (e) (void)hipEventDestroy(e);
     }
 };
 }  // namespace pgrt
@@ -212,11 +222,17 @@ struct pgrt_ctx {
     SceneView view{};
     bool has_scene = false;
     pgrt_config cfg{};  // pgrt_set_config (zero = defaults)
-    // levels traced as wave packets: level 0 is coherent by construction (8x8 pixel blocks),
-    // levels 1-2 because k_shade queues each wave's reflections and refractions as separate
-    // pixel-ordered groups (r1g C2: packets on levels 0 / 0-1 / 0-2 / 0-3 / all: 0.206 / 0.197 /
+    // PGRT_PACKETS_AUTO: bit L = level L traced as wave packets.  Level 0 always (8x8 pixel
+    // blocks are coherent by construction); deeper levels by their measured packet utilisation
+    // (the fraction of the wave's node stream a lane's ray needed, FrameCounters::pkt): on while
+    // it stays >= kPacketMinUtil, re-probed every kPacketProbeFrames frames while off.  Start:
+    // levels 0-2 (k_shade queues each wave's reflections and refractions as separate
+    // pixel-ordered groups; r1g C2: packets on levels 0 / 0-1 / 0-2 / 0-3 / all: 0.206 / 0.197 /
     // 0.194 / 0.196 / 0.202 ms/frame)
-    int packet_levels = 3;
+    unsigned auto_packets = 0x7u;
+    double packet_util[kMaxLevels] = {};  // last measured utilisation per level (0 = never measured)
+    unsigned long long frames_collected = 0;
+    int probe_level = -1;  // level traced as packets in the next frame to refresh its utilisation
     pgrt_bvh_info info{};
 
     CameraView cam{};
@@ -594,7 +610,36 @@ long long batch_rays(const pgrt_ctx* ctx) {
 bool packet_level(const pgrt_ctx* ctx, int L) {
     const int k = ctx->cfg.packet_levels;
     if (k == PGRT_PACKETS_OFF) return false;
-    return L < (k == PGRT_PACKETS_AUTO ? ctx->packet_levels : k);
+    if (k == PGRT_PACKETS_AUTO) return L == 0 || ((ctx->auto_packets >> L) & 1u) != 0 || L == ctx->probe_level;
+    return L < k;
+}
+
+// PGRT_PACKETS_AUTO: a level stays on wave packets while its rays use at least this fraction of
+// the wave's node stream (calibrated on C2 / C5), re-probed while off
+constexpr double kPacketMinUtil = 0.4;
+constexpr unsigned long long kPacketProbeFrames = 32;
+
+void update_packet_choice(pgrt_ctx* ctx, const std::vector<FrameCounters>& fcs, int levels) {
+    if (ctx->cfg.packet_levels != PGRT_PACKETS_AUTO) return;
+    ctx->probe_level = -1;
+    for (int L = 1; L < levels && L < kMaxLevels; ++L) {
+        unsigned long long u = 0, l = 0;
+        for (const FrameCounters& h : fcs) {
+            u += h.pkt[L][0];
+            l += h.pkt[L][1];
+        }
+        if (l < 4096) continue;  // not traced as packets (or too few rays to judge)
+        ctx->packet_util[L] = (double)u / (double)l;
+        if (ctx->packet_util[L] >= kPacketMinUtil) ctx->auto_packets |= 1u << L;
+        else ctx->auto_packets &= ~(1u << L);
+    }
+    // re-probe the shallowest level that is off (its rays may have become coherent)
+    if (++ctx->frames_collected % kPacketProbeFrames == 0)
+        for (int L = 1; L < levels && L < kMaxLevels; ++L)
+            if (!((ctx->auto_packets >> L) & 1u)) {
+                ctx->probe_level = L;
+                break;
+            }
 }
 
 // 8-lanes-per-ray threshold: with frames in flight the concurrent frames hide the latency floors
@@ -713,6 +758,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 tl.count = p->profile >= 2;
                 tl.packets = packet_level(ctx, L);  // coherent 8x8-pixel waves -> packet traversal
                 tl.gen = L == 0 && fuse ? &gen : nullptr;
+                tl.pkt_util = fcd->pkt[L];
                 id = ctx->timer.begin_kernel(CAT_TRACE, CAT_LTRACE + L);
                 const bool launched = launch_trace(view, tl, s);
                 ctx->timer.end_kernel(s, id, launched);
@@ -823,6 +869,7 @@ void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
             enqueue_frame(ctx, fs);
             continue;
         }
+        update_packet_choice(ctx, ctx->last_fc, levels);
         for (auto& h : ctx->last_fc) {
             for (int L = 0; L < levels; ++L) {
                 rays_shadow += (uint64_t)fc_shadow(h, L);
@@ -877,6 +924,7 @@ void gather_frame(pgrt_ctx* ctx, FrameSet* fs) {
     const size_t tile_floats = (size_t)kTile * kTile * 3;  // RGB tiles (out_mode 2)
     const size_t block = (size_t)F * per_rank * tile_floats;  // one rank's frames, frame-major
     const float* src = nullptr;
+    PGRT_HIP(hipEventRecord(fs->ev_g0, ctx->stream));
     if (ctx->emulated) {
         ctx->gathered.alloc(block * ctx->world);
         PGRT_HIP(hipMemcpyAsync(ctx->gathered.p + (size_t)ctx->rank * block, fs->tilebuf.p, sizeof(float) * block,
@@ -893,14 +941,28 @@ void gather_frame(pgrt_ctx* ctx, FrameSet* fs) {
         if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string("ncclGather: ") + ncclGetErrorString(r));
         src = ctx->rank == 0 ? ctx->gathered.p : nullptr;
     }
+    PGRT_HIP(hipEventRecord(fs->ev_g1, ctx->stream));
     if (src)  // every frame of the call in one launch (grid.y = frame)
         launch_unpack_tiles(src, fs->dist_fb, W, H, ctx->world, per_rank, 3, ctx->stream, F, 0, F);
+    PGRT_HIP(hipEventRecord(fs->ev_g2, ctx->stream));
+    fs->gather_timed = true;
     PGRT_HIP(hipGetLastError());
+}
+
+// device ms of a completed frame's gather (ncclGather incl. the wait for peers) + unpack
+void gather_times(FrameSet* fs, pgrt_stats* st) {
+    if (!fs->gather_timed) return;
+    float g = 0, u = 0;
+    PGRT_HIP(hipEventElapsedTime(&g, fs->ev_g0, fs->ev_g1));
+    PGRT_HIP(hipEventElapsedTime(&u, fs->ev_g1, fs->ev_g2));
+    st->ms_gather = g + u;
+    st->ms_resolve = u;
 }
 
 // complete a pending frame: collect, gather (distributed), release the set's buffers
 void finish_frame(pgrt_ctx* ctx, FrameSet* fs) {
     fs->pending = false;
+    fs->gather_timed = false;
     collect_frame(ctx, fs);
     if (fs->distributed) gather_frame(ctx, fs);
     PGRT_HIP(hipEventRecord(fs->ev_ready, ctx->stream));
@@ -1368,6 +1430,18 @@ int pgrt_comm_init(pgrt_ctx* ctx, int world, int rank, const char id[128]) {
     });
 }
 
+int pgrt_comm_info(const pgrt_ctx* ctx, int* nranks, int* rank) {
+    if (!ctx || !nranks || !rank) return PGRT_ERR_INVALID_ARGUMENT;
+    if (!ctx->comm) {
+        *nranks = ctx->world;
+        *rank = ctx->rank;
+        return PGRT_OK;
+    }
+    if (ncclCommCount(ctx->comm, nranks) != ncclSuccess || ncclCommUserRank(ctx->comm, rank) != ncclSuccess)
+        return PGRT_ERR_RCCL;
+    return PGRT_OK;
+}
+
 int pgrt_render_distributed_device(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device, pgrt_stats* st) {
     if (!ctx || !p) return PGRT_ERR_INVALID_ARGUMENT;
     return guarded(ctx, [&] {
@@ -1485,6 +1559,7 @@ int pgrt_render_wait(pgrt_ctx* ctx, unsigned long long ticket, pgrt_stats* st) {
         PGRT_REQUIRE(fs, PGRT_ERR_INVALID_ARGUMENT, "unknown ticket (or its frame set was reused)");
         finish_through(ctx, ticket);
         PGRT_HIP(hipEventSynchronize(fs->ev_ready));
+        gather_times(fs, &fs->stats);
         if (st) *st = fs->stats;
     });
 }
@@ -1536,6 +1611,8 @@ int pgrt_frame_diag(const pgrt_ctx* ctx, pgrt_level_diag* out, int max_levels) {
             for (int k = 0; k < 6; ++k)
                 d.longest_ray[k] = std::max<uint64_t>(d.longest_ray[k], h.trav[L][8 + k] & 0xffffffull);
             d.ms_trace = ctx->level_ms[L][0];
+            d.packet_steps_hit += h.pkt[L][0];
+            d.packet_steps_live += h.pkt[L][1];
             d.ms_shade = ctx->level_ms[L][1];
             d.shadow_visits += h.trav[kMaxLevels + L][0];
             d.shadow_tests += h.trav[kMaxLevels + L][1];

@@ -50,12 +50,14 @@ void launch_raygen(const CameraView& cam, const FrameParams& fp, const int4* til
 // ------------------------------------------------------------------ shading (trace body)
 
 // k_shade block size (one allocation atomic per block and iteration, shade_ray.hpp; r1f A/B:
-// 256 beat 512 and 1024)
+// 256 beat 512 and 1024).  The kernel is latency-bound (dependent hit -> attribute -> texel
+// chain): it is compiled for 6 waves per SIMD (80 VGPRs, 2 spilled) instead of the 4 the
+// unconstrained 98 VGPRs allow -- r2c C2 A/B: 0.1938 -> 0.1901 ms/frame (5 waves 0.1907)
 constexpr int kShadeBlock = 256;
 static_assert(kShadeBlock % kBlock == 0, "k_shade blocks are whole multiples of kBlock");
 
 template <bool LDS_TABLES>
-__global__ __launch_bounds__(kShadeBlock) void k_shade(SceneView s, FrameParams fp, int level, Queue q, Queue next,
+__global__ __launch_bounds__(kShadeBlock, 6) void k_shade(SceneView s, FrameParams fp, int level, Queue q, Queue next,
                                                        LevelNodes nodes, ShadowQueue sq, FrameCounters* fc) {
     __shared__ float lut255[256];
     __shared__ DevMaterial smat[LDS_TABLES ? kLdsMats : 1];

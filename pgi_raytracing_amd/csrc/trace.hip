@@ -636,7 +636,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const fl
                                                            const float4* __restrict__ rd, float4* __restrict__ hits,
                                                            const int* __restrict__ count_dev, int count_terms,
                                                            int count_host, int cap,
-                                                           unsigned long long* __restrict__ counters, PrimaryGen gen) {
+                                                           unsigned long long* __restrict__ counters, PrimaryGen gen,
+                                                           unsigned long long* __restrict__ util) {
     __shared__ int wstack[kTraceBlock / 64][kPktStack];
     const int wib = threadIdx.x >> 6;
     const int lane = __lane_id();
@@ -647,6 +648,11 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const fl
     const cfloat_ptr nodes = (cfloat_ptr)(const void*)s.nodes;  // 16 floats per node
     const cfloat_ptr tris = (cfloat_ptr)(const void*)s.tri;     // 12 floats per triangle
     unsigned long long nvis = 0, ntest = 0;
+    // packet utilisation (sampled: every 8th block): internal-node steps at which this lane's ray
+    // hit a child box, and steps it spent live -- their ratio is the fraction of the wave's node
+    // stream the ray needed (pgrt_config.packet_levels AUTO decides per level from it)
+    const bool sample = util != nullptr && (blockIdx.x & 7) == 0;
+    unsigned useful = 0, live_steps = 0;
     for (int base = (blockIdx.x * kTraceBlock) + wib * 64; base < n; base += gridDim.x * kTraceBlock) {
         const int i = base + lane;
         const bool valid = i < n;
@@ -693,6 +699,10 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const fl
                 float t0, t1;
                 const bool h0 = box_hit(a.x, a.y, a.z, a.w, c.x, c.y, idx, idy, idz, oix, oiy, oiz, best_t, t0);
                 const bool h1 = box_hit(b.x, b.y, b.z, b.w, c.z, c.w, idx, idy, idz, oix, oiy, oiz, best_t, t1);
+                if (sample && live) {
+                    ++live_steps;
+                    useful += (h0 || h1) ? 1u : 0u;
+                }
                 const unsigned long long b0 = __ballot(h0), b1 = __ballot(h1);
                 if (b0 == 0ull && b1 == 0ull) {
                     node = sp > 0 ? wstack[wib][--sp] : kSentinel;
@@ -724,6 +734,17 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const fl
         if (COUNT && lane == 0) {
             nvis += rvis;
             ntest += rtest;
+        }
+    }
+    if (sample) {  // wave sums, one atomic pair per wave of the sampled blocks
+        unsigned long long u = useful, l = live_steps;
+        for (int off = 32; off >= 1; off >>= 1) {
+            u += __shfl_xor(u, off, 64);
+            l += __shfl_xor(l, off, 64);
+        }
+        if (lane == 0 && l > 0) {
+            atomicAdd(&util[0], u);
+            atomicAdd(&util[1], l);
         }
     }
     if (COUNT && lane == 0) {  // per-wave counts (one packet step = one node visit)
@@ -777,7 +798,7 @@ bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) 
         const PrimaryGen g = t.gen ? *t.gen : PrimaryGen{};
 #define PGRT_LAUNCH_P(C, G)                                                                                   \
     PGRT_TLAUNCH((k_trace_pkt<C, G>), dim3(grid), dim3(kTraceBlock), 0, stream, s, t.ro, t.rd, t.hits,        \
-                 t.count_dev, t.count_terms, t.count_host, max_count, t.counters, g)
+                 t.count_dev, t.count_terms, t.count_host, max_count, t.counters, g, t.pkt_util)
         if (t.count) {
             if (t.gen) PGRT_LAUNCH_P(true, true); else PGRT_LAUNCH_P(true, false);
         } else {

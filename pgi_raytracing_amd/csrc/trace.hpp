@@ -29,6 +29,9 @@ struct FrameCounters {
     // profile == 2: per closest-hit launch {sum node visits, sum triangle tests, max visits of
     // one ray, max tests of one ray}; [0, kMaxLevels) level queues, [kMaxLevels, 2k) shadows
     alignas(128) unsigned long long trav[2 * kMaxLevels][16];  // visits, tests, max visits, max tests, max wave iterations
+    // packet traversal utilisation per level (sampled blocks): {lane-steps whose ray hit a child
+    // box, live lane-steps}; filled only by levels traced as packets
+    alignas(128) unsigned long long pkt[kMaxLevels][2];
 };
 
 __host__ __device__ inline int fc_count(const FrameCounters& f, int L) {
@@ -110,6 +113,7 @@ struct TraceLaunch {
     bool allow_group = true;
     bool packets = false;
     const PrimaryGen* gen = nullptr;
+    unsigned long long* pkt_util = nullptr;  // packet launches: sampled utilisation sums (FrameCounters::pkt)
 };
 // the packet traversal needs the binary layout and a tree that fits its wave-uniform stack
 bool trace_packets_available(const SceneView& s);

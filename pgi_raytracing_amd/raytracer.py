@@ -76,6 +76,7 @@ def lib():
         "pgrt_unpack_tiles_host": (ip, [ip, ip, ip, ip, fp, fp]),
         "pgrt_comm_unique_id": (ip, [C.c_char_p]),
         "pgrt_comm_init": (ip, [vp, ip, ip, C.c_char_p]),
+        "pgrt_comm_info": (ip, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "pgrt_render_tiles_device": (ip, [vp, C.POINTER(abi.RenderParams), ip, ip, vp, C.POINTER(abi.Stats)]),
         "pgrt_render_distributed": (ip, [vp, C.POINTER(abi.RenderParams), fp, C.POINTER(abi.Stats)]),
         "pgrt_render_distributed_device": (ip, [vp, C.POINTER(abi.RenderParams), vp, C.POINTER(abi.Stats)]),
@@ -293,6 +294,12 @@ class Context:
 
     def comm_init(self, world: int, rank: int, uid: bytes):
         _check(self.h, self.L.pgrt_comm_init(self.h, world, rank, C.c_char_p(uid)))
+
+    def comm_info(self) -> tuple[int, int]:
+        """(ranks, rank) of the context's RCCL communicator (ncclCommCount / ncclCommUserRank)."""
+        n, r = C.c_int(), C.c_int()
+        _check(self.h, self.L.pgrt_comm_info(self.h, C.byref(n), C.byref(r)))
+        return n.value, r.value
 
     def render_tiles_device(self, params, rank: int, world: int, dev_ptr: int):
         """This rank's tiles into a tile-compact device buffer (pgrt_render_tiles_device)."""

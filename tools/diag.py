@@ -30,7 +30,7 @@ def main():
     t = time.time()
     ctx.set_scene(sc)
     info = ctx.bvh_info()
-    print(json.dumps({"bvh": {"builder": ["lbvh", "ploc"][info.builder], "iters": info.build_iterations,
+    print(json.dumps({"bvh": {"builder": {1: "lbvh", 2: "ploc"}.get(info.builder, info.builder), "iters": info.build_iterations,
                               "tris": info.num_triangles, "nodes": info.num_nodes, "depth": info.max_depth,
                               "width": info.width, "refs": info.num_references, "split": round(info.split_beta, 3), "build_ms": round(info.build_ms, 3), "set_scene_s": round(time.time() - t, 3)}}))
     if c5:

@@ -1,14 +1,16 @@
 #!/bin/bash
-# rocprofv3 passes for the bench workload (run on the GPU box via gpurun):
+# rocprofv3 passes for one bench workload (run on the GPU box via gpurun):
 #   1. kernel trace + stats (per-kernel average durations)
-#   2./3. PMC passes, one counter group each (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass)
-# Usage: tools/profile.sh <tag> [bench args...]
+#   2.-5. PMC passes, one counter group each (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass):
+#         FETCH_SIZE | WRITE_SIZE | TCC hit/miss | VALU instructions + GRBM cycles
+# Usage: tools/profile.sh <tag> <config> [bench args...]   (config: C2 | C3 | C4 | C5)
 set -u
 cd "$(dirname "$0")/.."
-TAG=${1:-r1}
-shift || true
-ARGS=${*:-"--roofline-only"}
-OUT=gpurun_out/prof_$TAG
+TAG=${1:-r2}
+CFG=${2:-C2}
+shift 2 || shift $#
+ARGS="--config $CFG ${*:---roofline-only}"
+OUT=gpurun_out/prof_${TAG}_${CFG}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 run() {  # name limit rocprof-args...
@@ -22,9 +24,9 @@ run() {  # name limit rocprof-args...
     tail -3 "$OUT/$name.log"
     if [ $rc -ne 0 ]; then exit $rc; fi
 }
-run trace 400 --kernel-trace --stats
-run pmc_fetch 400 --kernel-trace --pmc FETCH_SIZE
-run pmc_write 400 --kernel-trace --pmc WRITE_SIZE
-run pmc_l2 400 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum
-python3 tools/traffic.py "$OUT" "$OUT/traffic_c2.json" "$TAG"
-find "$OUT" -name "*.csv" | head -20
+run trace 300 --kernel-trace --stats
+run pmc_fetch 300 --kernel-trace --pmc FETCH_SIZE
+run pmc_write 300 --kernel-trace --pmc WRITE_SIZE
+run pmc_l2 300 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum
+run pmc_valu 300 --kernel-trace --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE
+python3 tools/traffic.py "$OUT" "$OUT/traffic_${CFG}.json" "$TAG" "$CFG $(grep -o '"workload": "[^"]*"' "$OUT/trace.log" | head -1)"

@@ -5,7 +5,11 @@ coalesced reads -> x2; WRITE_SIZE exact; both in KB (1024 B).  Reports the mean 
 closest-hit launch (k_trace / k_trace8g / k_trace8, every level and the shadow queue), the same
 unit as bench.py's roofline `achieved`.
 
-usage: python tools/traffic.py gpurun_out/prof_<tag> profiles/traffic_c2.json <round>"""
+Also (optional passes) the VALU issue rate of the closest-hit launches: SQ_INSTS_VALU
+(wave-instructions) x 2 cycles (a wave64 VALU instruction occupies a SIMD-32 for 2 cycles) over
+the SIMD-cycles of the launch (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs), per kernel.
+
+usage: python tools/traffic.py gpurun_out/prof_<tag> profiles/<r>/traffic_<cfg>.json <round> [workload]"""
 import collections
 import csv
 import glob
@@ -29,6 +33,7 @@ def per_dispatch(path, counter):
 
 def main():
     root, out, rnd = sys.argv[1], sys.argv[2], sys.argv[3]
+    workload = sys.argv[4] if len(sys.argv) > 4 else "C2 avenger-proxy 1920x1080 Whitted d=5 (bench.py default)"
     fetch, fn = per_dispatch(os.path.join(root, "pmc_fetch"), "FETCH_SIZE")
     write, wn = per_dispatch(os.path.join(root, "pmc_write"), "WRITE_SIZE")
 
@@ -39,7 +44,7 @@ def main():
     f_kb = sum(fetch[d] for d in fids) / max(1, len(fids))
     w_kb = sum(write[d] for d in wids) / max(1, len(wids))
     res = {
-        "workload": "C2 avenger-proxy 1920x1080 Whitted d=5 (bench.py default)",
+        "workload": workload,
         "kernel": "closest-hit launches (k_trace, k_trace8g), every level + shadow queue",
         "source": f"{root}: rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE, separate passes",
         "correction": "gfx950: FETCH_SIZE x2 (MI355X_MICROARCH.md HBM section); WRITE_SIZE as reported; KB=1024 B",
@@ -50,6 +55,21 @@ def main():
         "bytes_per_launch": int(round((2 * f_kb + w_kb) * 1024)),
         "round": rnd,
     }
+    valu, vn = per_dispatch(os.path.join(root, "pmc_valu"), "SQ_INSTS_VALU")
+    gui, _ = per_dispatch(os.path.join(root, "pmc_valu"), "GRBM_GUI_ACTIVE")
+    if valu:
+        by = collections.defaultdict(lambda: [0.0, 0.0, 0])
+        for d in trace_ids(vn):
+            k = vn[d].split("(")[0].split("<")[0].strip()
+            by[k][0] += valu[d]
+            by[k][1] += gui.get(d, 0.0)
+            by[k][2] += 1
+        res["valu_issue"] = {
+            k: {"launches": n, "valu_insts_per_launch": round(v / n), "frac": round(2 * v / (1024 * g / 8), 4) if g else None}
+            for k, (v, g, n) in by.items()}
+        res["valu_issue_note"] = ("frac = SQ_INSTS_VALU x 2 cyc / (1024 SIMDs x GRBM_GUI_ACTIVE / 8): the fraction of "
+                                  "the chip's VALU issue slots the launch used (1.0 = every SIMD issuing a wave64 "
+                                  "VALU instruction every 2 cycles)")
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))
