@@ -305,6 +305,11 @@ def main():
     else:  # every frame set is allocated and warm before the timed region
         args.warmup = max(args.warmup, in_flight * F)
     run_frames(args.warmup)
+    share = None
+    if world > 1 and not args.roofline_only:
+        # rank 0's tile share from measured calls (libpgrt collective): its rendering against the
+        # xGMI gather it receives and the unpack it runs
+        share = ctx.tune_distribution(params, F, fb, calls=4)
     ctx.synchronize()
     if dist:
         dist.barrier()
@@ -443,6 +448,7 @@ def main():
             "rccl_ranks": comm_ranks,
             "per_rank_ms_per_step": [round(x, 4) for x in per_rank_ms],
             "gather_ms_per_call": round(sum(gather_ms) / len(gather_ms), 4) if gather_ms else None,
+            "rank0_share": f"{share[0]}/{share[1]}" if share else None,
             "roofline": roof,
             "host_framebuffer_ms_per_step": host_fb,
             "cpu_baseline": cpu,

@@ -176,7 +176,10 @@ typedef struct pgrt_config {
     long long max_batch_rays;  /* level-0 rays per sample batch (0 = 16M); smaller values split a
                                   frame's samples into more batches (queue memory vs launches) */
     int max_batches_in_flight; /* sample batches queued across frames in flight (0 = no bound) */
-    int reserved[5];
+    int rank0_share_a, rank0_share_b; /* distributed frames: rank 0 renders a tiles for every b of
+                                         another rank (1..64 each; 0 = the default deal of
+                                         pgrt_tile_share; pgrt_tune_distribution sets them) */
+    int reserved[3];
 } pgrt_config;
 
 /* ---- context ---- */
@@ -255,32 +258,55 @@ int pgrt_occluded(pgrt_ctx* ctx, const float* rays, int n, int* occluded);
 
 /* ---- multi-GPU image tiles (one process per GPU, RCCL over xGMI) ----
  * Tiles are tile_size x tile_size, numbered row-major and dealt to ranks in rounds of
- * a + b*(world-1) tiles: b sub-rounds of one tile per rank, rank 0 in only the first a of them
- * (rank 0 also unpacks every gathered frame, so it renders a/b of another rank's share).
- * pgrt_tile_share reports (a, b) for a world size (PGRT_RANK0_SHARE="a/b" overrides; a == b is
- * the round-robin deal t -> rank t % world).  pgrt_tile_index maps local tile j of rank to its
+ * a + b*(world-1) tiles: rank 0 gets a, every other rank b (min(a,b) sub-rounds of one tile per
+ * rank, then the remaining b-a tiles of ranks 1.. or a-b tiles of rank 0), so rank 0 renders a/b
+ * of another rank's share -- less when its unpack of every gathered frame costs more, more when
+ * the gather into it over xGMI is the bound (pgrt_tune_distribution).  pgrt_tile_share reports the
+ * default (a, b) for a world size (PGRT_RANK0_SHARE="a/b" overrides; a == b is the round-robin
+ * deal t -> rank t % world).  pgrt_tile_index maps local tile j of rank to its
  * tile index (error past the rank's last tile); pgrt_tile_count is the rank's tile count. */
 int pgrt_tile_count(int width, int height, int tile_size, int rank, int world);
 int pgrt_tile_index(int width, int height, int tile_size, int rank, int world, int j);
 int pgrt_tile_share(int world, int* a, int* b);
 int pgrt_tile_rect(int width, int height, int tile_size, int tile_index, int rect[4]);
 /* Unpack a rank-major gathered tile buffer (every rank's tiles in its local order, each tile
- * tile_size^2 * 4 floats, each rank's block padded to the longest rank list) into a W x H RGBA
- * framebuffer.  Host reference of the device unpack. */
+ * tile_size^2 * 4 floats, ranks back to back with exactly pgrt_tile_count tiles each) into a
+ * W x H RGBA framebuffer.  Host reference of the device unpack. */
 int pgrt_unpack_tiles_host(int width, int height, int tile_size, int world,
                            const float* gathered, float* rgba);
+/* The same three with an explicit share (rank 0 renders a tiles for every b of another rank,
+ * 1..64 each; a = b = 0: the default share) -- the deal of a context whose pgrt_config sets
+ * rank0_share_a / rank0_share_b. */
+int pgrt_tile_count_ex(int width, int height, int tile_size, int rank, int world, int a, int b);
+int pgrt_tile_index_ex(int width, int height, int tile_size, int rank, int world, int a, int b, int j);
+int pgrt_unpack_tiles_host_ex(int width, int height, int tile_size, int world, int a, int b,
+                              const float* gathered, float* rgba);
 int pgrt_comm_unique_id(char id[128]);
-int pgrt_comm_init(pgrt_ctx* ctx, int world, int rank, const char id[128]);
+int pgrt_comm_init(pgrt_ctx* ctx, int world, int rank, const char id[128]); /* world <= 16 */
 /* The communicator's rank count and this context's rank as RCCL reports them (ncclCommCount /
  * ncclCommUserRank); without a communicator the context's world / rank (1 / 0 by default). */
 int pgrt_comm_info(const pgrt_ctx* ctx, int* nranks, int* rank);
 /* Rank-local half of the distributed render, for callers that gather with their own
  * communicator: render the tiles of `rank` (of `world`) of the camera image into a tile-compact
  * device buffer of pgrt_tile_count(W, H, 64, rank, world) * 64 * 64 * 4 floats (local tile j is
- * tile pgrt_tile_index(W, H, 64, rank, world, j); edge tiles are padded). */
+ * tile pgrt_tile_index(W, H, 64, rank, world, j); edge tiles are padded).  The deal is the
+ * context's (pgrt_config.rank0_share_*), which is pgrt_tile_share's unless those are set. */
 int pgrt_render_tiles_device(pgrt_ctx* ctx, const pgrt_render_params* p, int rank, int world,
                              void* tiles_device, pgrt_stats* st);
-/* Render this rank's tiles, gather them on rank 0 with one ncclGather, unpack on device.
+/* Device form of pgrt_unpack_tiles_host_ex for callers that gather pgrt_render_tiles_device
+ * buffers themselves: tiles_device is rank-major (exactly pgrt_tile_count_ex tiles per rank,
+ * RGBA tiles), rgba_device W*H*4 floats.  Synchronous. */
+int pgrt_unpack_tiles_device(pgrt_ctx* ctx, int width, int height, int world, int a, int b,
+                             const void* tiles_device, void* rgba_device);
+/* Collective (every rank calls it with the same arguments): measure the distributed batched
+ * frames (p, nframes per call into rgba_device as pgrt_render_frames_distributed_device_async)
+ * for rank-0 shares a/8 = 4/8 .. 32/8 -- `calls` timed calls each, the slowest rank's wall time
+ * (ncclAllReduce max) decides -- and keep the fastest in the context's pgrt_config
+ * (rank0_share_a/b, returned in *a, *b).  With one rank it returns 1/1 and does nothing. */
+int pgrt_tune_distribution(pgrt_ctx* ctx, const pgrt_render_params* p, int nframes,
+                           void* rgba_device, int calls, int* a, int* b);
+/* Render this rank's tiles, gather them on rank 0 (grouped ncclSend / ncclRecv of each rank's
+ * exact tile list), unpack on device.
  * rgba_host (rank 0 only, may be NULL elsewhere): W*H*4 floats. */
 int pgrt_render_distributed(pgrt_ctx* ctx, const pgrt_render_params* p, float* rgba_host,
                             pgrt_stats* st);

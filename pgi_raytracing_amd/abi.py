@@ -122,7 +122,9 @@ class Config(C.Structure):
         ("group_max", C.c_int),
         ("max_batch_rays", C.c_longlong),
         ("max_batches_in_flight", C.c_int),
-        ("reserved", C.c_int * 5),
+        ("rank0_share_a", C.c_int),
+        ("rank0_share_b", C.c_int),
+        ("reserved", C.c_int * 3),
     ]
 
 

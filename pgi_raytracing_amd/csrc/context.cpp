@@ -178,6 +178,7 @@ struct FrameSet {
     int frame_out_tiles = 0;  // tiles per frame in the tile-compact output (>= frame_tiles)
     long long frame_stride = 0;  // floats between frames of a framebuffer output
     bool distributed = false;
+    TileDeal deal{1, 1, 1};  // distributed: the tile deal this frame was rendered with
     float* dist_fb = nullptr;
     DevBuf<float> tilebuf;  // distributed: this rank's tiles, tile-compact
     int cam_w = 0, cam_h = 0;  // image size at submission (the gather's layout)
@@ -914,36 +915,66 @@ void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
     st->overflow_retries = retries;
 }
 
-// distributed frame: ncclGather of every rank's tile-compact buffer to rank 0 and the unpack
-// kernel there, on the context stream (after the frame's slots)
+// this rank's tile count and every rank's list layout for a distributed frame of W x H
+UnpackSrc unpack_layout(const TileDeal& d, int W, int H) {
+    const int total = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
+    UnpackSrc u{};
+    u.prefix[0] = 0;
+    for (int r = 0; r < d.world; ++r) {
+        u.count[r] = deal_count(d, total, r);
+        u.prefix[r + 1] = u.prefix[r] + u.count[r];
+    }
+    return u;
+}
+
+// distributed frame: every rank's tile-compact RGB buffer to rank 0 (grouped ncclSend / ncclRecv
+// with each rank's exact tile count -- no padding crosses xGMI; rank 0's own tiles stay in
+// place) and the unpack kernel there, on the context stream (after the frame's slots)
 void gather_frame(pgrt_ctx* ctx, FrameSet* fs) {
     const int W = fs->cam_w, H = fs->cam_h;
-    const int total = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
-    const int per_rank = deal_max_count(tile_deal(ctx->world), total);
+    const TileDeal& d = fs->deal;
     const int F = fs->nframes;
     const size_t tile_floats = (size_t)kTile * kTile * 3;  // RGB tiles (out_mode 2)
-    const size_t block = (size_t)F * per_rank * tile_floats;  // one rank's frames, frame-major
-    const float* src = nullptr;
+    UnpackSrc u = unpack_layout(d, W, H);
+    const int me = ctx->rank;
+    bool unpack = me == 0;
     PGRT_HIP(hipEventRecord(fs->ev_g0, ctx->stream));
     if (ctx->emulated) {
-        ctx->gathered.alloc(block * ctx->world);
-        PGRT_HIP(hipMemcpyAsync(ctx->gathered.p + (size_t)ctx->rank * block, fs->tilebuf.p, sizeof(float) * block,
-                                hipMemcpyDeviceToDevice, ctx->stream));
-        src = ctx->rank == 0 ? ctx->gathered.p : nullptr;
-    } else if (ctx->world == 1 && !ctx->comm) {
-        src = fs->tilebuf.p;
+        // one GPU measures rank `me`: its tiles are copied to their place in a full-size buffer
+        // (the other ranks' blocks stay unwritten), rank 0 also unpacks the whole frame
+        ctx->gathered.alloc((size_t)F * u.prefix[d.world] * tile_floats);
+        PGRT_HIP(hipMemcpyAsync(ctx->gathered.p + (size_t)F * u.prefix[me] * tile_floats, fs->tilebuf.p,
+                                sizeof(float) * F * u.count[me] * tile_floats, hipMemcpyDeviceToDevice, ctx->stream));
+        for (int r = 0; r < d.world; ++r) u.src[r] = ctx->gathered.p + (size_t)F * u.prefix[r] * tile_floats;
+    } else if (d.world == 1) {
+        u.src[0] = fs->tilebuf.p;
     } else {
         PGRT_REQUIRE(ctx->comm, PGRT_ERR_RCCL, "pgrt_comm_init has not been called");
-        if (ctx->rank == 0) ctx->gathered.alloc(block * ctx->world);
-        // one collective for all of the call's frames
-        ncclResult_t r = ncclGather(fs->tilebuf.p, ctx->rank == 0 ? ctx->gathered.p : nullptr, block, ncclFloat, 0,
-                                    ctx->comm, ctx->stream);
-        if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string("ncclGather: ") + ncclGetErrorString(r));
-        src = ctx->rank == 0 ? ctx->gathered.p : nullptr;
+        const size_t others = (size_t)F * (u.prefix[d.world] - u.count[0]) * tile_floats;
+        if (me == 0) ctx->gathered.alloc(std::max<size_t>(1, others));
+        // one group for all of the call's frames
+        auto ok = [](ncclResult_t r, const char* what) {
+            if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(r));
+        };
+        ok(ncclGroupStart(), "ncclGroupStart");
+        if (me == 0) {
+            for (int r = 1; r < d.world; ++r) {
+                float* dst = ctx->gathered.p + (size_t)F * (u.prefix[r] - u.count[0]) * tile_floats;
+                u.src[r] = dst;
+                if (u.count[r] > 0)
+                    ok(ncclRecv(dst, (size_t)F * u.count[r] * tile_floats, ncclFloat, r, ctx->comm, ctx->stream),
+                       "ncclRecv");
+            }
+            u.src[0] = fs->tilebuf.p;
+        } else if (u.count[me] > 0) {
+            ok(ncclSend(fs->tilebuf.p, (size_t)F * u.count[me] * tile_floats, ncclFloat, 0, ctx->comm, ctx->stream),
+               "ncclSend");
+        }
+        ok(ncclGroupEnd(), "ncclGroupEnd");
     }
     PGRT_HIP(hipEventRecord(fs->ev_g1, ctx->stream));
-    if (src)  // every frame of the call in one launch (grid.y = frame)
-        launch_unpack_tiles(src, fs->dist_fb, W, H, ctx->world, per_rank, 3, ctx->stream, F, 0, F);
+    if (unpack)  // every frame of the call in one launch (grid.y = frame)
+        launch_unpack_tiles(u, fs->dist_fb, W, H, d, 3, ctx->stream, 0, F);
     PGRT_HIP(hipEventRecord(fs->ev_g2, ctx->stream));
     fs->gather_timed = true;
     PGRT_HIP(hipGetLastError());
@@ -996,7 +1027,7 @@ void check_frame(const pgrt_ctx* ctx, const pgrt_render_params* p) {
 // the tiles land in fs->tilebuf and finish_frame gathers them into fb (rank 0).
 void start_frame(pgrt_ctx* ctx, FrameSet* fs, const pgrt_render_params* p, std::vector<int4> tiles, float* out,
                  int out_mode, int ox, int oy, int pitch, bool distributed, float* fb, int nframes = 1,
-                 long long frame_stride = 0) {
+                 long long frame_stride = 0, TileDeal deal = TileDeal{1, 1, 1}) {
     check_frame(ctx, p);
     PGRT_REQUIRE(nframes >= 1 && nframes <= kMaxFramesPerCall, PGRT_ERR_INVALID_ARGUMENT,
                  "frames per call must be in [1, 64]");
@@ -1013,12 +1044,10 @@ void start_frame(pgrt_ctx* ctx, FrameSet* fs, const pgrt_render_params* p, std::
     fs->cam_w = ctx->cam.width;
     fs->cam_h = ctx->cam.height;
     if (distributed) {
-        const int W = fs->cam_w, H = fs->cam_h;
-        const int total = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
-        const int per_rank = deal_max_count(tile_deal(ctx->world), total);
-        // padded slots of the tile-compact buffer are never unpacked (t >= total); frame-major
-        fs->tilebuf.alloc((size_t)nframes * per_rank * kTile * kTile * 3);
-        fs->frame_out_tiles = per_rank;
+        // this rank's tiles of every frame, frame-major (the gather's layout, unpack_layout)
+        fs->deal = deal;
+        fs->tilebuf.alloc(std::max<size_t>(1, (size_t)nframes * tiles.size() * kTile * kTile * 3));
+        fs->frame_out_tiles = (int)tiles.size();
         out = fs->tilebuf.p;
         out_mode = 2;
         ox = oy = pitch = 0;
@@ -1069,10 +1098,14 @@ void frame_rect(const pgrt_ctx* ctx, const pgrt_render_params* p, int& x, int& y
                  "render rect outside the camera image");
 }
 
+// the deal of this context's distributed frames (pgrt_config.rank0_share_*, else the default)
+TileDeal ctx_deal(const pgrt_ctx* ctx, int world) {
+    return tile_deal(world, ctx->cfg.rank0_share_a, ctx->cfg.rank0_share_b);
+}
+
 // rank's tiles in its local order (tiles.hpp deal)
-std::vector<int4> rank_tiles(int W, int H, int rank, int world) {
+std::vector<int4> rank_tiles(int W, int H, int rank, const TileDeal& d) {
     std::vector<int4> all = rect_tiles(0, 0, W, H), mine;
-    const TileDeal d = tile_deal(world);
     for (int j = 0;; ++j) {
         const int t = deal_tile(d, rank, j);
         if (t >= (int)all.size()) break;
@@ -1350,19 +1383,29 @@ int pgrt_render_accumulate(pgrt_ctx* ctx, const pgrt_render_params* p, float* me
 
 // ---- tiles / multi-GPU -------------------------------------------------------------------
 
-int pgrt_tile_count(int width, int height, int tile_size, int rank, int world) {
-    if (width <= 0 || height <= 0 || tile_size <= 0 || world <= 0 || rank < 0 || rank >= world)
+int pgrt_tile_count_ex(int width, int height, int tile_size, int rank, int world, int a, int b) {
+    if (width <= 0 || height <= 0 || tile_size <= 0 || world <= 0 || rank < 0 || rank >= world || a < 0 || b < 0 ||
+        a > 64 || b > 64)
         return PGRT_ERR_INVALID_ARGUMENT;
     const long long total = (long long)((width + tile_size - 1) / tile_size) * ((height + tile_size - 1) / tile_size);
-    return deal_count(tile_deal(world), (int)total, rank);
+    return deal_count(tile_deal(world, a, b), (int)total, rank);
+}
+
+int pgrt_tile_index_ex(int width, int height, int tile_size, int rank, int world, int a, int b, int j) {
+    if (width <= 0 || height <= 0 || tile_size <= 0 || world <= 0 || rank < 0 || rank >= world || j < 0 || a < 0 ||
+        b < 0 || a > 64 || b > 64)
+        return PGRT_ERR_INVALID_ARGUMENT;
+    const int total = ((width + tile_size - 1) / tile_size) * ((height + tile_size - 1) / tile_size);
+    const int t = deal_tile(tile_deal(world, a, b), rank, j);
+    return t < total ? t : PGRT_ERR_INVALID_ARGUMENT;
+}
+
+int pgrt_tile_count(int width, int height, int tile_size, int rank, int world) {
+    return pgrt_tile_count_ex(width, height, tile_size, rank, world, 0, 0);
 }
 
 int pgrt_tile_index(int width, int height, int tile_size, int rank, int world, int j) {
-    if (width <= 0 || height <= 0 || tile_size <= 0 || world <= 0 || rank < 0 || rank >= world || j < 0)
-        return PGRT_ERR_INVALID_ARGUMENT;
-    const int total = ((width + tile_size - 1) / tile_size) * ((height + tile_size - 1) / tile_size);
-    const int t = deal_tile(tile_deal(world), rank, j);
-    return t < total ? t : PGRT_ERR_INVALID_ARGUMENT;
+    return pgrt_tile_index_ex(width, height, tile_size, rank, world, 0, 0, j);
 }
 
 int pgrt_tile_share(int world, int* a, int* b) {
@@ -1385,17 +1428,22 @@ int pgrt_tile_rect(int width, int height, int tile_size, int t, int rect[4]) {
 }
 
 int pgrt_unpack_tiles_host(int width, int height, int tile_size, int world, const float* g, float* rgba) {
-    if (width <= 0 || height <= 0 || tile_size <= 0 || world <= 0 || !g || !rgba) return PGRT_ERR_INVALID_ARGUMENT;
+    return pgrt_unpack_tiles_host_ex(width, height, tile_size, world, 0, 0, g, rgba);
+}
+
+int pgrt_unpack_tiles_host_ex(int width, int height, int tile_size, int world, int a, int b, const float* g,
+                              float* rgba) {
+    if (width <= 0 || height <= 0 || tile_size <= 0 || world <= 0 || !g || !rgba || a < 0 || b < 0 || a > 64 || b > 64)
+        return PGRT_ERR_INVALID_ARGUMENT;
     const int tx = (width + tile_size - 1) / tile_size, ty = (height + tile_size - 1) / tile_size;
     const int total = tx * ty;
-    const TileDeal d = tile_deal(world);
-    const int per_rank = deal_max_count(d, total);
+    const TileDeal d = tile_deal(world, a, b);
     const size_t tile_floats = (size_t)tile_size * tile_size * 4;
+    size_t slot = 0;  // rank-major, each rank's tiles in its local order, no padding
     for (int r = 0; r < world; ++r)
-        for (int j = 0; j < per_rank; ++j) {
+        for (int j = 0; j < deal_count(d, total, r); ++j, ++slot) {
             const int t = deal_tile(d, r, j);
-            if (t >= total) continue;
-            const float* src = g + ((size_t)r * per_rank + j) * tile_floats;
+            const float* src = g + slot * tile_floats;
             const int x0 = (t % tx) * tile_size, y0 = (t / tx) * tile_size;
             for (int y = 0; y < tile_size && y0 + y < height; ++y)
                 for (int x = 0; x < tile_size && x0 + x < width; ++x)
@@ -1414,7 +1462,7 @@ int pgrt_comm_unique_id(char id[128]) {
 }
 
 int pgrt_comm_init(pgrt_ctx* ctx, int world, int rank, const char id[128]) {
-    if (!ctx || !id || world <= 0 || rank < 0 || rank >= world) return PGRT_ERR_INVALID_ARGUMENT;
+    if (!ctx || !id || world <= 0 || world > kMaxRanks || rank < 0 || rank >= world) return PGRT_ERR_INVALID_ARGUMENT;
     return guarded(ctx, [&] {
         if (ctx->comm) {
             (void)ncclCommDestroy(ctx->comm);
@@ -1450,8 +1498,9 @@ int pgrt_render_distributed_device(pgrt_ctx* ctx, const pgrt_render_params* p, v
         drain_frames(ctx);
         FrameSet* fs = frame_set(ctx, 0);
         PGRT_HIP(hipEventRecord(fs->ev_ready, ctx->stream));
-        start_frame(ctx, fs, p, rank_tiles(ctx->cam.width, ctx->cam.height, ctx->rank, ctx->world), nullptr, 1, 0,
-                    0, 0, true, static_cast<float*>(rgba_device));
+        const TileDeal deal = ctx_deal(ctx, ctx->world);
+        start_frame(ctx, fs, p, rank_tiles(ctx->cam.width, ctx->cam.height, ctx->rank, deal), nullptr, 1, 0, 0, 0,
+                    true, static_cast<float*>(rgba_device), 1, 0, deal);
         fs->pending = false;
         collect_frame(ctx, fs);
         auto tg = std::chrono::steady_clock::now();
@@ -1494,7 +1543,7 @@ int submit_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device, 
         if (const int cap = ctx->cfg.max_batches_in_flight; cap > 0) {
             long long nt;
             if (distributed) {
-                nt = (long long)rank_tiles(ctx->cam.width, ctx->cam.height, ctx->rank, ctx->world).size();
+                nt = (long long)rank_tiles(ctx->cam.width, ctx->cam.height, ctx->rank, ctx_deal(ctx, ctx->world)).size();
             } else {
                 int x, y, w, h;
                 frame_rect(ctx, p, x, y, w, h);
@@ -1517,8 +1566,9 @@ int submit_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device, 
             }
         }
         if (distributed) {
-            start_frame(ctx, fs, p, rank_tiles(ctx->cam.width, ctx->cam.height, ctx->rank, ctx->world), nullptr, 1,
-                        0, 0, 0, true, static_cast<float*>(rgba_device), nframes);
+            const TileDeal deal = ctx_deal(ctx, ctx->world);
+            start_frame(ctx, fs, p, rank_tiles(ctx->cam.width, ctx->cam.height, ctx->rank, deal), nullptr, 1, 0, 0,
+                        0, true, static_cast<float*>(rgba_device), nframes, 0, deal);
         } else {
             int x, y, w, h;
             frame_rect(ctx, p, x, y, w, h);
@@ -1564,13 +1614,90 @@ int pgrt_render_wait(pgrt_ctx* ctx, unsigned long long ticket, pgrt_stats* st) {
     });
 }
 
+int pgrt_tune_distribution(pgrt_ctx* ctx, const pgrt_render_params* p, int nframes, void* rgba_device, int calls,
+                           int* a_out, int* b_out) {
+    if (!ctx || !p || nframes < 1 || nframes > kMaxFramesPerCall || calls < 1 || calls > 64)
+        return PGRT_ERR_INVALID_ARGUMENT;
+    if (ctx->world <= 1 || (!ctx->comm && !ctx->emulated)) {  // one rank: nothing to balance
+        if (a_out) *a_out = 1;
+        if (b_out) *b_out = 1;
+        return PGRT_OK;
+    }
+    // rank 0's share a/8 of another rank's, from half to four times it: below 1 its unpack is the
+    // larger cost, above 1 the xGMI ingress of the gather into rank 0 is
+    static const int kCand[] = {4, 5, 6, 7, 8, 10, 12, 14, 16, 20, 24, 32};
+    const pgrt_config saved = ctx->cfg;
+    double best = 1e300;
+    int best_a = 0;
+    for (int a : kCand) {
+        pgrt_config c = saved;
+        c.rank0_share_a = a;
+        c.rank0_share_b = 8;
+        int rc = pgrt_set_config(ctx, &c);
+        if (rc != PGRT_OK) return rc;
+        std::vector<unsigned long long> tickets;
+        unsigned long long t = 0;
+        rc = pgrt_render_frames_distributed_device_async(ctx, p, nframes, rgba_device, &t);  // warm: allocations
+        if (rc == PGRT_OK) rc = pgrt_render_wait(ctx, t, nullptr);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int k = 0; k < calls && rc == PGRT_OK; ++k) {
+            rc = pgrt_render_frames_distributed_device_async(ctx, p, nframes, rgba_device, &t);
+            tickets.push_back(t);
+        }
+        for (size_t k = 0; k < tickets.size() && rc == PGRT_OK; ++k)
+            if (tickets.size() - k <= (size_t)ctx->frames_in_flight) rc = pgrt_render_wait(ctx, tickets[k], nullptr);
+        if (rc != PGRT_OK) return rc;
+        double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        // the slowest rank decides; every rank sees the same maxima, so all pick the same share
+        rc = guarded(ctx, [&] {
+            if (!ctx->comm) return;  // emulation: this rank's time alone
+            DevBuf<double> v;
+            v.alloc(1);
+            PGRT_HIP(hipMemcpyAsync(v.p, &ms, sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+            const ncclResult_t r = ncclAllReduce(v.p, v.p, 1, ncclFloat64, ncclMax, ctx->comm, ctx->stream);
+            if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+            PGRT_HIP(hipMemcpyAsync(&ms, v.p, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+            PGRT_HIP(hipStreamSynchronize(ctx->stream));
+        });
+        if (rc != PGRT_OK) return rc;
+        if (ms < best) {
+            best = ms;
+            best_a = a;
+        }
+    }
+    pgrt_config c = saved;
+    c.rank0_share_a = best_a;
+    c.rank0_share_b = 8;
+    const int rc = pgrt_set_config(ctx, &c);
+    if (rc != PGRT_OK) return rc;
+    if (a_out) *a_out = best_a;
+    if (b_out) *b_out = 8;
+    return PGRT_OK;
+}
+
+int pgrt_unpack_tiles_device(pgrt_ctx* ctx, int width, int height, int world, int a, int b, const void* tiles_device,
+                             void* rgba_device) {
+    if (!ctx || width <= 0 || height <= 0 || world <= 0 || world > kMaxRanks || a < 0 || b < 0 || a > 64 || b > 64 ||
+        !tiles_device || !rgba_device)
+        return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        const TileDeal d = tile_deal(world, a, b);
+        UnpackSrc u = unpack_layout(d, width, height);
+        const float* g = static_cast<const float*>(tiles_device);
+        for (int r = 0; r < world; ++r) u.src[r] = g + (size_t)u.prefix[r] * kTile * kTile * 4;
+        launch_unpack_tiles(u, static_cast<float*>(rgba_device), width, height, d, 4, ctx->stream, 0, 1);
+        PGRT_HIP(hipGetLastError());
+        PGRT_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
 int pgrt_render_tiles_device(pgrt_ctx* ctx, const pgrt_render_params* p, int rank, int world, void* tiles_device,
                              pgrt_stats* st) {
     if (!ctx || !p || !tiles_device || world <= 0 || rank < 0 || rank >= world) return PGRT_ERR_INVALID_ARGUMENT;
     return guarded(ctx, [&] {
         PGRT_REQUIRE(ctx->has_cam, PGRT_ERR_NO_CAMERA, "pgrt_set_camera has not been called");
         auto t0 = std::chrono::steady_clock::now();
-        render_tiles(ctx, p, rank_tiles(ctx->cam.width, ctx->cam.height, rank, world),
+        render_tiles(ctx, p, rank_tiles(ctx->cam.width, ctx->cam.height, rank, ctx_deal(ctx, world)),
                      static_cast<float*>(tiles_device), 1, 0, 0, 0, st);
         PGRT_HIP(hipStreamSynchronize(ctx->stream));
         if (st) st->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -244,41 +244,38 @@ void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles,
 
 // ------------------------------------------------------------------ multi-GPU unpack
 
-// g holds, per rank, `frames` frames of tiles_per_rank tiles each (frame-major, tiles in the rank's
-// local order of the tiles.hpp deal); blockIdx.y = frame - frame0, every rank's tiles of that
-// frame are unpacked into rgba + frame * W*H*4
-__global__ __launch_bounds__(kBlock) void k_unpack(const float* __restrict__ g, float4* __restrict__ rgba, int width,
-                                                   int height, TileDeal deal, int tiles_per_rank, int channels,
-                                                   int frames, int frame0) {
+// u.src[r] holds rank r's tiles of `frames` frames (frame-major, u.count[r] tiles per frame in
+// the rank's local order of the tiles.hpp deal, `channels` floats per pixel); blockIdx.y = frame
+// - frame0; every rank's tiles of that frame are unpacked into rgba + frame * W*H*4
+__global__ __launch_bounds__(kBlock) void k_unpack(UnpackSrc u, float4* __restrict__ rgba, int width, int height,
+                                                   TileDeal deal, int channels, int frame0) {
     const int world = deal.world;
     const int frame = frame0 + (int)blockIdx.y;
     const long long idx = (long long)blockIdx.x * kBlock + threadIdx.x;
-    const long long per_rank = (long long)tiles_per_rank * kTile * kTile;
-    if (idx >= per_rank * world) return;
-    const int rank = (int)(idx / per_rank);
-    const long long r = idx - rank * per_rank;
-    const int j = (int)(r / (kTile * kTile));
-    const int p = (int)(r - (long long)j * kTile * kTile);
+    const int tile_slot = (int)(idx / (kTile * kTile));
+    if (tile_slot >= u.prefix[world]) return;
+    int rank = 0;
+    while (rank + 1 < world && u.prefix[rank + 1] <= tile_slot) ++rank;
+    const int j = tile_slot - u.prefix[rank];
+    const int p = (int)(idx - (long long)tile_slot * kTile * kTile);
     const int tiles_x = (width + kTile - 1) / kTile;
-    const int tiles_y = (height + kTile - 1) / kTile;
     const int t = deal_tile(deal, rank, j);
-    if (t >= tiles_x * tiles_y) return;  // padding of the rank's list
     const int x = (t % tiles_x) * kTile + (p % kTile);
     const int y = (t / tiles_x) * kTile + (p / kTile);
-    if (x >= width || y >= height) return;
-    const long long src = ((long long)rank * frames + frame) * per_rank + r;
+    if (x >= width || y >= height) return;  // padding of an edge tile
+    const long long src = ((long long)frame * u.count[rank] + j) * kTile * kTile + p;
+    const float* g = u.src[rank];
     rgba[(size_t)frame * width * height + (size_t)y * width + x] =
         channels == 4 ? reinterpret_cast<const float4*>(g)[src]
                       : make_float4(g[src * 3], g[src * 3 + 1], g[src * 3 + 2], 1.0f);
 }
 
-void launch_unpack_tiles(const float* gathered, float* rgba, int width, int height, int world, int tiles_per_rank,
-                         int channels, hipStream_t stream, int frames, int frame0, int nframes) {
-    const long long total = (long long)world * tiles_per_rank * kTile * kTile;
+void launch_unpack_tiles(const UnpackSrc& u, float* rgba, int width, int height, const TileDeal& deal, int channels,
+                         hipStream_t stream, int frame0, int nframes) {
+    const long long total = (long long)u.prefix[deal.world] * kTile * kTile;
     if (total <= 0 || nframes <= 0) return;
     hipLaunchKernelGGL(k_unpack, dim3((unsigned)((total + kBlock - 1) / kBlock), (unsigned)nframes), dim3(kBlock), 0,
-                       stream, gathered, reinterpret_cast<float4*>(rgba), width, height, tile_deal(world),
-                       tiles_per_rank, channels, frames, frame0);
+                       stream, u, reinterpret_cast<float4*>(rgba), width, height, deal, channels, frame0);
 }
 
 // ------------------------------------------------------------------ progressive accumulation

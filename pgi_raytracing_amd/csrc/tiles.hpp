@@ -1,12 +1,15 @@
 // tiles.hpp -- how the image tiles of a distributed frame are dealt to ranks (host + device).
 //
-// Tiles are numbered row-major.  They are dealt in rounds of R = a + b * (world - 1) consecutive
-// tiles: b sub-rounds of one tile per rank, rank 0 taking part in only the first a of them, so
-// rank 0 renders a / b of another rank's share.  Rank 0 also unpacks every gathered frame into
-// the framebuffer (≈ 10 µs per 1080p frame, ≈ 5 % of a C2 frame's render): with a < b the ranks
-// finish together.  a == b is the plain round-robin deal (tile t -> rank t % world).
-// The share is process-wide: PGRT_RANK0_SHARE="a/b" (1 <= a <= b <= 64), else a default by world
-// size from the C2 measurements: 8/8 at 1-2 GPUs, 7/8 at 3-4, 6/8 at 5-7, 5/8 at 8+.
+// Tiles are numbered row-major and dealt in rounds of R = a + b * (world - 1) consecutive tiles:
+// rank 0 gets a tiles per round, every other rank b.  Inside a round, min(a, b) sub-rounds deal
+// one tile to every rank in turn (tile -> rank tile % world), then either (b - a) sub-rounds deal
+// one tile to each of ranks 1..world-1 (a < b) or the last (a - b) tiles go to rank 0 (a > b).
+// a == b is the plain round-robin deal.  The interleaving spreads the glass-canopy hotspot over
+// every rank.  Rank 0's share a/b trades its own rendering against the gather it receives and
+// the unpack it runs: a < b when the unpack is the larger cost (C2 compute emulation, r1j), a > b
+// when the xGMI ingress into rank 0 is (pgrt_tune_distribution measures it).
+// Default by world size from the C2 emulation: 8/8 at 1-2 GPUs, 7/8 at 3-4,
+// 6/8 at 5-7, 5/8 at 8+; PGRT_RANK0_SHARE="a/b" (1 <= a, b <= 64) overrides it process-wide.
 #pragma once
 
 #include <cstdlib>
@@ -22,7 +25,7 @@ inline TileDeal tile_deal(int world) {
     static const int env_a = [] {
         const char* e = std::getenv("PGRT_RANK0_SHARE");
         int a = 0, b = 0;
-        if (e && std::sscanf(e, "%d/%d", &a, &b) == 2 && a >= 1 && b >= a && b <= 64) return a * 100 + b;
+        if (e && std::sscanf(e, "%d/%d", &a, &b) == 2 && a >= 1 && a <= 64 && b >= 1 && b <= 64) return a * 100 + b;
         return 0;
     }();
     TileDeal d{world, 8, 8};
@@ -44,6 +47,13 @@ inline TileDeal tile_deal(int world) {
     return d;
 }
 
+// an explicit share (a, b >= 1); world 1 deals every tile to rank 0
+inline TileDeal tile_deal(int world, int a, int b) {
+    if (a <= 0 || b <= 0) return tile_deal(world);
+    if (world <= 1) return TileDeal{world, 1, 1};
+    return TileDeal{world, a, b};
+}
+
 __host__ __device__ inline int deal_round(const TileDeal& d) { return d.a + d.b * (d.world - 1); }
 
 // tile t -> (rank, local index j on that rank)
@@ -54,14 +64,18 @@ __host__ __device__ inline void deal_owner(const TileDeal& d, int t, int& rank, 
         return;
     }
     const int R = deal_round(d), round = t / R, pos = t - round * R;
-    if (pos < d.a * d.world) {
+    const int m = d.a < d.b ? d.a : d.b;
+    if (pos < m * d.world) {
         const int sub = pos / d.world;
         rank = pos - sub * d.world;
         j = round * (rank == 0 ? d.a : d.b) + sub;
-    } else {
-        const int p2 = pos - d.a * d.world, sub = d.a + p2 / (d.world - 1);
+    } else if (d.a < d.b) {
+        const int p2 = pos - m * d.world, sub = m + p2 / (d.world - 1);
         rank = 1 + p2 % (d.world - 1);
         j = round * d.b + sub;
+    } else {
+        rank = 0;
+        j = round * d.a + m + (pos - m * d.world);
     }
 }
 
@@ -69,10 +83,14 @@ __host__ __device__ inline void deal_owner(const TileDeal& d, int t, int& rank, 
 __host__ __device__ inline int deal_tile(const TileDeal& d, int rank, int j) {
     if (d.world <= 1) return j;
     const int R = deal_round(d);
-    if (rank == 0) return (j / d.a) * R + (j % d.a) * d.world;
-    const int round = j / d.b, sub = j % d.b;
-    if (sub < d.a) return round * R + sub * d.world + rank;
-    return round * R + d.a * d.world + (sub - d.a) * (d.world - 1) + (rank - 1);
+    const int m = d.a < d.b ? d.a : d.b;
+    if (rank == 0) {
+        const int round = j / d.a, k = j % d.a;
+        return k < m ? round * R + k * d.world : round * R + m * d.world + (k - m);
+    }
+    const int round = j / d.b, k = j % d.b;
+    if (k < m) return round * R + k * d.world + rank;
+    return round * R + m * d.world + (k - m) * (d.world - 1) + (rank - 1);
 }
 
 // tiles of `rank` among `total`
@@ -86,11 +104,18 @@ inline int deal_count(const TileDeal& d, int total, int rank) {
     return lo;
 }
 
-// the longest rank list (the gather's per-rank block)
+// the longest rank list
 inline int deal_max_count(const TileDeal& d, int total) {
     int m = 0;
     for (int r = 0; r < d.world && r < 2; ++r) m = deal_count(d, total, r) > m ? deal_count(d, total, r) : m;
     return m;  // ranks >= 1 hold the same count or one less than rank 1
+}
+
+// exclusive prefix of the rank lists: the rank-major position of rank r's first tile
+inline long long deal_offset(const TileDeal& d, int total, int rank) {
+    long long o = 0;
+    for (int r = 0; r < rank; ++r) o += deal_count(d, total, r);
+    return o;
 }
 
 }  // namespace pgrt

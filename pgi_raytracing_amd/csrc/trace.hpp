@@ -149,9 +149,19 @@ void launch_accumulate_frame(const float* frame, float* sum, float* mean, long l
                              hipStream_t stream);
 // copy `n` FrameCounters to pinned host memory and zero them on the device
 void launch_export_counters(FrameCounters* dev, FrameCounters* host, int n, hipStream_t stream);
-// gathered: rank-major tile-compact buffers, `channels` floats per pixel (4: RGBA, 3: RGB + alpha 1)
-void launch_unpack_tiles(const float* gathered, float* rgba, int width, int height, int world, int tiles_per_rank,
-                         int channels, hipStream_t stream, int frames = 1, int frame0 = 0, int nframes = 1);
+// Distributed frames: rank r's tile-compact buffer (frame-major, count[r] tiles per frame in its
+// local deal order); prefix = exclusive prefix of the counts (prefix[world] = all tiles)
+constexpr int kMaxRanks = 16;
+struct UnpackSrc {
+    const float* src[kMaxRanks];
+    int count[kMaxRanks];
+    int prefix[kMaxRanks + 1];
+};
+struct TileDeal;  // tiles.hpp
+// unpack frames frame0 .. frame0 + nframes - 1 of every rank's tiles into rgba (W*H*4 floats per
+// frame); channels 4 (RGBA tiles) or 3 (RGB tiles, alpha 1: the gather format)
+void launch_unpack_tiles(const UnpackSrc& u, float* rgba, int width, int height, const TileDeal& deal, int channels,
+                         hipStream_t stream, int frame0, int nframes);
 
 // scene / BVH build
 constexpr int kBuilderLbvh = PGRT_BVH_LBVH;  // Karras 2012 over 63-bit Morton codes

@@ -74,9 +74,15 @@ def lib():
         "pgrt_tile_share": (ip, [ip, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "pgrt_tile_rect": (ip, [ip, ip, ip, ip, C.POINTER(C.c_int)]),
         "pgrt_unpack_tiles_host": (ip, [ip, ip, ip, ip, fp, fp]),
+        "pgrt_tile_count_ex": (ip, [ip, ip, ip, ip, ip, ip, ip]),
+        "pgrt_tile_index_ex": (ip, [ip, ip, ip, ip, ip, ip, ip, ip]),
+        "pgrt_unpack_tiles_host_ex": (ip, [ip, ip, ip, ip, ip, ip, fp, fp]),
         "pgrt_comm_unique_id": (ip, [C.c_char_p]),
         "pgrt_comm_init": (ip, [vp, ip, ip, C.c_char_p]),
         "pgrt_comm_info": (ip, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+        "pgrt_tune_distribution": (ip, [vp, C.POINTER(abi.RenderParams), ip, vp, ip, C.POINTER(C.c_int),
+                                        C.POINTER(C.c_int)]),
+        "pgrt_unpack_tiles_device": (ip, [vp, ip, ip, ip, ip, ip, vp, vp]),
         "pgrt_render_tiles_device": (ip, [vp, C.POINTER(abi.RenderParams), ip, ip, vp, C.POINTER(abi.Stats)]),
         "pgrt_render_distributed": (ip, [vp, C.POINTER(abi.RenderParams), fp, C.POINTER(abi.Stats)]),
         "pgrt_render_distributed_device": (ip, [vp, C.POINTER(abi.RenderParams), vp, C.POINTER(abi.Stats)]),
@@ -300,6 +306,17 @@ class Context:
         n, r = C.c_int(), C.c_int()
         _check(self.h, self.L.pgrt_comm_info(self.h, C.byref(n), C.byref(r)))
         return n.value, r.value
+
+    def tune_distribution(self, params, nframes: int, dev_ptr: int | None, calls: int = 4) -> tuple[int, int]:
+        """Collective: pick rank 0's tile share a/b from measured distributed calls (kept in the config)."""
+        a, b = C.c_int(), C.c_int()
+        _check(self.h, self.L.pgrt_tune_distribution(self.h, C.byref(params), nframes, C.c_void_p(dev_ptr or 0), calls,
+                                                      C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def unpack_tiles_device(self, width: int, height: int, world: int, share, tiles_dev: int, rgba_dev: int):
+        _check(self.h, self.L.pgrt_unpack_tiles_device(self.h, width, height, world, share[0], share[1],
+                                                       C.c_void_p(tiles_dev), C.c_void_p(rgba_dev)))
 
     def render_tiles_device(self, params, rank: int, world: int, dev_ptr: int):
         """This rank's tiles into a tile-compact device buffer (pgrt_render_tiles_device)."""

@@ -54,12 +54,15 @@ def _deal_owner(world, a, b, t):
     if world <= 1:
         return 0, t
     R = a + b * (world - 1)
+    m = min(a, b)
     rnd, pos = divmod(t, R)
-    if pos < a * world:
+    if pos < m * world:
         sub, r = divmod(pos, world)
         return r, rnd * (a if r == 0 else b) + sub
-    p2 = pos - a * world
-    return 1 + p2 % (world - 1), rnd * b + a + p2 // (world - 1)
+    p2 = pos - m * world
+    if a < b:
+        return 1 + p2 % (world - 1), rnd * b + m + p2 // (world - 1)
+    return 0, rnd * a + m + p2
 
 
 def _share(L, world):
@@ -101,25 +104,51 @@ def test_tile_plan_partitions_the_frame(W, H, world):
     assert (cover == 1).all()
 
 
-@pytest.mark.parametrize("W,H,world", [(200, 130, 3), (64, 64, 1), (130, 70, 4), (700, 500, 8)])
-def test_unpack_tiles_host(W, H, world):
-    """Rank-major gathered tiles (the deal's local order, blocks padded to the longest rank list)
-    reassemble into the frame."""
+@pytest.mark.parametrize("W,H,world,share", [(1920, 1080, 2, (20, 8)), (1920, 1080, 8, (19, 8)), (640, 480, 4, (3, 1)),
+                                             (700, 500, 3, (8, 8)), (1920, 1080, 8, (5, 8)), (100, 70, 2, (64, 1))])
+def test_tile_plan_explicit_share(W, H, world, share):
+    """Explicit shares (rank 0 renders a tiles per b of another rank, a > b included: the gather
+    into rank 0 is the bound) partition the frame; counts follow a/b."""
+    L = lib()
+    a, b = share
+    total = (-(-W // 64)) * (-(-H // 64))
+    counts = [L.pgrt_tile_count_ex(W, H, 64, r, world, a, b) for r in range(world)]
+    assert sum(counts) == total
+    owner = set()
+    for r in range(world):
+        for j in range(counts[r]):
+            t = L.pgrt_tile_index_ex(W, H, 64, r, world, a, b, j)
+            assert 0 <= t < total and t not in owner
+            owner.add(t)
+            assert _deal_owner(world, a, b, t) == (r, j)
+    assert len(owner) == total
+    R = a + b * (world - 1)
+    if world > 1 and total >= 4 * R:
+        assert abs(counts[0] / counts[1] - a / b) < 0.25 * a / b
+
+
+@pytest.mark.parametrize("W,H,world,share", [(200, 130, 3, (0, 0)), (64, 64, 1, (0, 0)), (130, 70, 4, (0, 0)),
+                                             (700, 500, 8, (0, 0)), (700, 500, 3, (17, 8)), (300, 200, 2, (4, 1))])
+def test_unpack_tiles_host(W, H, world, share):
+    """Rank-major gathered tiles (the deal's local order, exactly pgrt_tile_count tiles per rank,
+    no padding) reassemble into the frame."""
     L = lib()
     T = 64
     tx, ty = -(-W // T), -(-H // T)
     total = tx * ty
-    a, b = _share(L, world)
-    per_rank = max(L.pgrt_tile_count(W, H, T, r, world) for r in range(world))
+    a, b = share if share[0] else _share(L, world)
+    counts = [L.pgrt_tile_count_ex(W, H, T, r, world, *share) for r in range(world)]
+    offset = np.concatenate([[0], np.cumsum(counts)])
     frame = np.random.default_rng(0).random((H, W, 4), dtype=np.float32)
-    g = np.zeros((world, per_rank, T, T, 4), np.float32)
+    g = np.zeros((total, T, T, 4), np.float32)
     for t in range(total):
         r, j = _deal_owner(world, a, b, t)
         x0, y0 = (t % tx) * T, (t // tx) * T
         blk = frame[y0:y0 + T, x0:x0 + T]
-        g[r, j, :blk.shape[0], :blk.shape[1]] = blk
+        g[offset[r] + j, :blk.shape[0], :blk.shape[1]] = blk
     out = np.zeros_like(frame)
-    assert L.pgrt_unpack_tiles_host(W, H, T, world, abi.fptr(g.reshape(-1)), abi.fptr(out.reshape(-1))) == 0
+    assert L.pgrt_unpack_tiles_host_ex(W, H, T, world, share[0], share[1], abi.fptr(g.reshape(-1)),
+                                       abi.fptr(out.reshape(-1))) == 0
     assert (out == frame).all()
 
 

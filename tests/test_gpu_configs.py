@@ -171,3 +171,38 @@ def test_c5_random_1m_4096_d8(gpu_ctx, c5_scene):
         _, s = gpu_ctx.render(abi.make_params(max_level=8, rect=(0, int(y), W, 1)))
         got += (s.rays_primary, s.rays_shadow, s.rays_reflect, s.rays_refract)
     assert tuple(got) == (sto.rays_primary, sto.rays_shadow, sto.rays_reflect, sto.rays_refract)
+
+
+@pytest.mark.parametrize("share", [(0, 0), (20, 8), (3, 8)])
+def test_device_unpack_eight_ranks(gpu_ctx, avenger_scene, share):
+    """The multi-GPU assembly with world 8 on one GPU: every rank's tiles rendered through
+    pgrt_render_tiles_device into its slot of a rank-major buffer (exactly pgrt_tile_count_ex
+    tiles per rank), unpacked by the device kernel (pgrt_unpack_tiles_device), equal the full
+    frame bit for bit -- for the default deal and explicit rank-0 shares above and below 1."""
+    from pgi_raytracing_amd.raytracer import lib
+
+    gpu_ctx.set_scene(avenger_scene)
+    W, H, world = 700, 450, 8
+    gpu_ctx.set_camera(abi.default_camera(W, H))
+    p = abi.make_params(max_level=5, spp_side=2, jitter=abi.PGRT_JITTER_HASH, frame=6)
+    L = lib()
+    old = gpu_ctx.configure(rank0_share_a=share[0], rank0_share_b=share[1])
+    counts = [L.pgrt_tile_count_ex(W, H, 64, r, world, *share) for r in range(world)]
+    assert sum(counts) == (-(-W // 64)) * (-(-H // 64))
+    tile_bytes = 64 * 64 * 16
+    g = gpu_ctx.alloc(sum(counts) * tile_bytes)
+    fb = gpu_ctx.alloc(W * H * 16)
+    try:
+        off = 0
+        for r in range(world):
+            gpu_ctx.render_tiles_device(p, r, world, g + off * tile_bytes)
+            off += counts[r]
+        gpu_ctx.unpack_tiles_device(W, H, world, share, g, fb)
+        out = gpu_ctx.to_host(fb, (H, W, 4))
+        ref, _ = gpu_ctx.render(p)
+        assert _frames_equal(out, ref)
+        assert gpu_ctx.tune_distribution(p, 1, fb) == (1, 1)  # one rank: nothing to tune
+    finally:
+        gpu_ctx.set_config(old)
+        gpu_ctx.free(g)
+        gpu_ctx.free(fb)

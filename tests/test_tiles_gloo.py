@@ -44,7 +44,8 @@ def _worker(rank, world, port, obj, env, q):
     sc.set_environment(env)
     osc = pyoracle.OracleScene(sc)
     cam = abi.default_camera(W, H)
-    per_rank = max(L.pgrt_tile_count(W, H, T, r, world) for r in range(world))
+    counts = [L.pgrt_tile_count(W, H, T, r, world) for r in range(world)]
+    per_rank = max(counts)
     mine = [L.pgrt_tile_index(W, H, T, rank, world, j) for j in range(L.pgrt_tile_count(W, H, T, rank, world))]
     buf = np.zeros((per_rank, T, T, 4), np.float32)
     rect = (C.c_int * 4)()
@@ -58,7 +59,9 @@ def _worker(rank, world, port, obj, env, q):
     gathered = [torch.zeros_like(t_buf) for _ in range(world)] if rank == 0 else None
     dist.gather(t_buf, gathered, dst=0)
     if rank == 0:
-        g = np.ascontiguousarray(torch.cat(gathered).numpy())
+        # rank-major, exactly pgrt_tile_count tiles per rank (the gather pads to equal sizes)
+        g = np.ascontiguousarray(np.concatenate([x.numpy().reshape(per_rank, -1)[:counts[r]]
+                                                 for r, x in enumerate(gathered)]).reshape(-1))
         out = np.zeros((H, W, 4), np.float32)
         assert L.pgrt_unpack_tiles_host(W, H, T, world, abi.fptr(g), abi.fptr(out.reshape(-1))) == 0
         full, _ = osc.render(cam, abi.make_params(max_level=5, spp_side=2, jitter=abi.PGRT_JITTER_HASH), threads=2)
