@@ -89,7 +89,8 @@ struct PrimaryGen {
     FrameParams fp;
     const int4* tiles;
     // the packet traversal stores the rays it generated (k_raygen's queue layout) for the
-    // level-0 shade
+    // level-0 shade; pinhole frames store only the directions (store_ro = store_time = NULL:
+    // every valid ray starts at the camera with tnear 0.001 in air, PinHoleCamera.cpp:31-63)
     float4* store_ro;
     float4* store_rd;
     float* store_time;

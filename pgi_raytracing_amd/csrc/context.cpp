@@ -116,6 +116,7 @@ struct FrameSlot {
     std::vector<std::unique_ptr<DevBuf<int4>>> n_link;
     std::vector<int> level_cap;
     DevBuf<float4> s_ro, s_rd, s_hit, s_contrib;
+    DevBuf<unsigned char> s_lit;
     int s_cap = 0;
     DevBuf<FrameCounters> fc;  // one per sample batch
     std::vector<FrameCounters> host_fc;
@@ -221,6 +222,7 @@ struct pgrt_ctx {
     DevBuf<unsigned char> texels;
     DevBuf<DevLight> lights;
     SceneView view{};
+    float light0[3] = {0, 0, 0};  // the first light's position (compact shadow queues)
     bool has_scene = false;
     pgrt_config cfg{};  // pgrt_set_config (zero = defaults)
     // PGRT_PACKETS_AUTO: bit L = level L traced as wave packets.  Level 0 always (8x8 pixel
@@ -366,6 +368,8 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
         texs[i] = DevTexture{t.width, t.height, t.pitch, t.bpp, pool, (long long)t.pitch * t.height};
         pool += ((long long)t.pitch * t.height + 255) / 256 * 256;
     }
+    if (d->num_lights > 0)
+        for (int k = 0; k < 3; ++k) ctx->light0[k] = d->lights[0].position[k];
     std::vector<DevLight> lights(std::max(1, d->num_lights));
     for (int i = 0; i < d->num_lights; ++i)
         for (int k = 0; k < 3; ++k) {
@@ -534,6 +538,7 @@ void ensure_frame_buffers(FrameSlot* sl, int n0, int levels, int nlight, int bat
         sl->s_rd.alloc(sc);
         sl->s_hit.alloc(sc);
         sl->s_contrib.alloc(sc);
+        sl->s_lit.alloc(sc);
         sl->s_cap = sc;
     }
     if (sl->fc.n < (size_t)batches) {  // zeroed once; every frame's export kernel re-zeroes them
@@ -578,6 +583,7 @@ void grow_after_overflow(FrameSlot* sl, int levels) {
         sl->s_rd.alloc(sh);
         sl->s_hit.alloc(sh);
         sl->s_contrib.alloc(sh);
+        sl->s_lit.alloc(sh);
         sl->s_cap = sh;
     }
 }
@@ -731,8 +737,16 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             Queue q[2];
             for (int b = 0; b < 2; ++b)
                 q[b] = Queue{sl->q_ro[b].p, sl->q_rd[b].p, sl->q_time[b].p, sl->q_hit[b].p, sl->q_cap};
-            ShadowQueue sq{sl->s_ro.p, sl->s_rd.p, sl->s_hit.p, sl->s_contrib.p, sl->s_cap};
-            const PrimaryGen gen{ctx->cam, fp, sl->tiles.p, q[0].ro, q[0].rd, q[0].time, &fcd->count0};
+            // one light over the binary BVH: the compact shadow queue (no origins, one "lit" byte
+            // per ray instead of a hit record: 47 B per shadow ray written and read fewer)
+            const bool compact_shadow = view.nlight == 1 && !view.wide;
+            ShadowQueue sq{compact_shadow ? nullptr : sl->s_ro.p, sl->s_rd.p, compact_shadow ? nullptr : sl->s_hit.p,
+                           sl->s_contrib.p, sl->s_cap, compact_shadow ? sl->s_lit.p : nullptr};
+            // pinhole level 0: the traversal stores directions only (the shade takes the origin,
+            // tnear and medium from the camera: 20 B per primary ray written and read fewer)
+            const bool dir_only = fuse && !p->dof;
+            const PrimaryGen gen{ctx->cam, fp, sl->tiles.p, dir_only ? nullptr : q[0].ro, q[0].rd,
+                                 dir_only ? nullptr : q[0].time, &fcd->count0};
             int id = ctx->timer.begin(s, CAT_RAYGEN);
             if (!fuse) launch_raygen(ctx->cam, fp, sl->tiles.p, q[0], n0, fcd, s);
             debug_sync(s, "raygen", 0, bi);
@@ -766,7 +780,8 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 debug_sync(s, "trace", L, bi);
                 ++trace_launches;
                 id = ctx->timer.begin(s, CAT_SHADE, CAT_LSHADE + L);
-                launch_shade(view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex);
+                const PinholeOrigin l0{ctx->cam.from[0], ctx->cam.from[1], ctx->cam.from[2], L == 0 && dir_only ? 1 : 0};
+                launch_shade(view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex, l0);
                 debug_sync(s, "shade", L, bi);
                 ctx->timer.end(s, id);
             }
@@ -784,6 +799,10 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 tl.counters = fcd->trav[kMaxLevels];
                 tl.count = p->profile >= 2;
                 tl.allow_group = false;  // shadow rays: one lane per ray (no 8-lane groups, no packets)
+                if (compact_shadow) {
+                    tl.const_org = make_float4(ctx->light0[0], ctx->light0[1], ctx->light0[2], 0.01f);
+                    tl.lit = sq.lit;
+                }
                 id = ctx->timer.begin_kernel(CAT_TRACE, CAT_SHADOW);
                 const bool launched = launch_trace(view, tl, s);
                 ctx->timer.end_kernel(s, id, launched);

@@ -58,7 +58,8 @@ static_assert(kShadeBlock % kBlock == 0, "k_shade blocks are whole multiples of 
 
 template <bool LDS_TABLES>
 __global__ __launch_bounds__(kShadeBlock, 6) void k_shade(SceneView s, FrameParams fp, int level, Queue q, Queue next,
-                                                       LevelNodes nodes, ShadowQueue sq, FrameCounters* fc) {
+                                                       LevelNodes nodes, ShadowQueue sq, FrameCounters* fc,
+                                                       PinholeOrigin l0) {
     __shared__ float lut255[256];
     __shared__ DevMaterial smat[LDS_TABLES ? kLdsMats : 1];
     __shared__ DevTexture stex[LDS_TABLES ? kLdsTex : 1];
@@ -82,25 +83,33 @@ __global__ __launch_bounds__(kShadeBlock, 6) void k_shade(SceneView s, FramePara
     const int stride = gridDim.x * kShadeBlock;
     float4 nx_o = make_float4(0, 0, 0, 0), nx_d = make_float4(0, 0, 0, 0), nx_h = make_float4(0, 0, 0, 0);
     float nx_t = 0.0f;
+    // level 0 of a pinhole frame: only the directions were stored (camera_ops.hpp PrimaryGen)
+    const bool from_cam = l0.on != 0;
+    const float4 cam_o = make_float4(l0.x, l0.y, l0.z, 0.001f);
     {
         const int i0 = blockIdx.x * kShadeBlock + tid;
         if (i0 < n) {
-            nx_o = q.ro[i0];
             nx_d = q.rd[i0];
-            nx_t = q.time[i0];
             nx_h = q.hit[i0];
+            if (!from_cam) {
+                nx_o = q.ro[i0];
+                nx_t = q.time[i0];
+            }
         }
     }
     for (int base_i = blockIdx.x * kShadeBlock; base_i < n; base_i += stride) {
         const int i = base_i + tid;
         const bool active = i < n;
-        const float4 cur_o = nx_o, cur_d = nx_d, cur_h = nx_h;
-        const float cur_t = nx_t;
+        const float4 cur_d = nx_d, cur_h = nx_h;
+        const float4 cur_o = from_cam ? cam_o : nx_o;
+        const float cur_t = from_cam ? (cur_d.w >= 0.0f ? PGRT_IOR_AIR : 0.0f) : nx_t;
         if (i + stride < n) {
-            nx_o = q.ro[i + stride];
             nx_d = q.rd[i + stride];
-            nx_t = q.time[i + stride];
             nx_h = q.hit[i + stride];
+            if (!from_cam) {
+                nx_o = q.ro[i + stride];
+                nx_t = q.time[i + stride];
+            }
         }
         ShadeOut r;
         shade_eval(s, mats, lut255, level, fp.max_level, active, cur_o, cur_d, cur_t, cur_h, r);
@@ -110,16 +119,17 @@ __global__ __launch_bounds__(kShadeBlock, 6) void k_shade(SceneView s, FramePara
 }
 
 void launch_shade(const SceneView& s, const FrameParams& fp, int level, Queue q, Queue next, LevelNodes nodes,
-                  ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect) {
+                  ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect,
+                  const PinholeOrigin& l0) {
     if (max_count <= 0) return;
     const int per_block = kShadeBlock / kBlock;  // grid_for counts kBlock-thread blocks
     const int grid = std::max(1, grid_for(max_count, expect) / per_block);
     if (s.nmat <= kLdsMats && s.ntex <= kLdsTex)
         hipLaunchKernelGGL((k_shade<true>), dim3(grid), dim3(kShadeBlock), 0, stream, s, fp, level, q, next, nodes, sq,
-                           fc);
+                           fc, l0);
     else
         hipLaunchKernelGGL((k_shade<false>), dim3(grid), dim3(kShadeBlock), 0, stream, s, fp, level, q, next, nodes, sq,
-                           fc);
+                           fc, l0);
 }
 
 // ------------------------------------------------------------------ combine + finish
@@ -136,9 +146,13 @@ __device__ __forceinline__ float4 opaque_color(const SceneView& s, const ShadowQ
     float blue = 0, green = 0, red = 0;
     for (int j = 0; j < cnt; ++j) {
         const int k = base + j;
-        const int prim = __float_as_int(sq.hit[k].w);
-        bool lit = true;  // is_illuminated (raytracer.cpp:163-173): closest hit decides
-        if (prim >= 0) lit = s.prim_glass[prim] != 0;  // the occluder's material is dielectric
+        bool lit;  // is_illuminated (raytracer.cpp:163-173): closest hit decides
+        if (sq.lit) {
+            lit = sq.lit[k] != 0;  // decided by the shadow trace (compact queue)
+        } else {
+            const int prim = __float_as_int(sq.hit[k].w);
+            lit = prim < 0 || s.prim_glass[prim] != 0;  // no occluder, or a dielectric one
+        }
         if (lit) {
             const float4 c = sq.contrib[k];
             blue += c.x;

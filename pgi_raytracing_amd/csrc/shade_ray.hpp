@@ -248,7 +248,7 @@ __device__ __forceinline__ void shade_emit(const SceneView& s, const DevMaterial
                 const V3 lp = v3(L.pos[0], L.pos[1], L.pos[2]);
                 if (dot(nrm, lp) < 0) continue;  // is_illuminated's N.L test (raytracer.cpp:155)
                 // LightSource::GenerateRay(hit): org = light, dir = hit position vector
-                sq.ro[k] = make_float4(lp.x, lp.y, lp.z, 0.01f);
+                if (sq.ro) sq.ro[k] = make_float4(lp.x, lp.y, lp.z, 0.01f);
                 sq.rd[k] = make_float4(hitp.x, hitp.y, hitp.z, length(v3(lp.x - hitp.x, lp.y - hitp.y, lp.z - hitp.z)));
                 // Phong term for this light (raytracer.cpp:355-382)
                 const V3 lv = normalize(v3(lp.x - hitp.x, lp.y - hitp.y, lp.z - hitp.z));

@@ -104,7 +104,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
                                                        float4* __restrict__ hits,
                                                        const int* __restrict__ count_dev, int count_terms,
                                                        int count_host, int cap, int* __restrict__ gstack,
-                                                       unsigned long long* __restrict__ counters, int rpw) {
+                                                       unsigned long long* __restrict__ counters, int rpw,
+                                                       float4 const_org, unsigned char* __restrict__ lit) {
     extern __shared__ int lstack[];  // [entries][kTraceBlock]
     const int tid = threadIdx.x;
     const int lane = __lane_id();
@@ -139,7 +140,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
         stride_i += wstride;
         const int i = stride_i;
         if (i >= n) break;
-    const float4 o4 = ro[i];
+        const float4 o4 = ro ? ro[i] : const_org;
         const float4 d4 = rd[i];
         const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
         const float dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
@@ -244,7 +245,10 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
             }
             if (COUNT) rcyc_leaf += (unsigned long long)(clock64() - tl0);
         }
-        hits[i] = make_float4(best_t, best_u, best_v, __int_as_float(best_prim));
+        if (lit)  // is_illuminated (raytracer.cpp:163-173): no hit, or the occluder is dielectric
+            lit[i] = (best_prim < 0 || s.prim_glass[best_prim] != 0) ? 1 : 0;
+        else
+            hits[i] = make_float4(best_t, best_u, best_v, __int_as_float(best_prim));
         if (COUNT) {
             const unsigned long long dt = (unsigned long long)(wall_clock64() - t_start);
             if (dt > mclk) {  // the longest ray's profile
@@ -305,7 +309,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8(SceneView s, const float
     uint2* gst = reinterpret_cast<uint2*>(gstack + (size_t)(blockIdx.x * kTraceBlock + tid) * kGlobalStack);
     unsigned long long nvis = 0, ntest = 0, mvis = 0, mtest = 0;
     for (int i = blockIdx.x * kTraceBlock + tid; i < n; i += gridDim.x * kTraceBlock) {
-        const float4 o4 = ro[i];
+            const float4 o4 = ro[i];
         const float4 d4 = rd[i];
         const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
         const float dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
@@ -523,7 +527,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8g(SceneView s, const floa
     const int n = ray_count(count_dev, count_terms, count_host, cap);
     unsigned long long nvis = 0, ntest = 0, mvis = 0, mtest = 0;
     for (int i = blockIdx.x * kGroups + gib; i < n; i += gridDim.x * kGroups) {
-        const float4 o4 = ro[i];
+            const float4 o4 = ro[i];
         const float4 d4 = rd[i];
         const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
         const float dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
@@ -661,9 +665,11 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const fl
         if (valid) {
             if constexpr (GEN) {
                 pv = primary_ray(gen.cam, gen.fp, gen.tiles, i, o4, d4);  // level 0: no ray queue read
+                // the level-0 shade reads the rays back; pinhole rays share origin, tnear and
+                // medium (store_ro / store_time NULL: the shade takes them from the camera)
+                gen.store_rd[i] = d4;
                 if (gen.store_ro) {
                     gen.store_ro[i] = o4;
-                    gen.store_rd[i] = d4;
                     gen.store_time[i] = pv ? PGRT_IOR_AIR : 0.0f;
                 }
             } else {
@@ -779,6 +785,8 @@ constexpr int kTailMax = 131072, kTailRpw = 64;
 bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) {
     const int max_count = t.max_count;
     if (max_count <= 0) return false;
+    PGRT_REQUIRE((t.ro && !t.lit) || (!s.wide && !t.packets && !t.gen && !t.allow_group), PGRT_ERR_INVALID_ARGUMENT,
+                 "compact shadow queues are traced by the one-lane binary kernel only");
     const int ex = t.expect > 0 && t.expect < max_count ? t.expect : max_count;  // grid sizing only
     if (s.wide) {
         int grid = ceil_div(ex, kTraceBlock);
@@ -831,7 +839,7 @@ bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) 
     const size_t lds = (size_t)(spill ? kLdsStack : entries) * kTraceBlock * sizeof(int);
 #define PGRT_LAUNCH(C, S)                                                                                       \
     PGRT_TLAUNCH((k_trace<C, S>), dim3(grid), dim3(kTraceBlock), lds, stream, s, t.ro, t.rd, t.hits, t.count_dev, \
-                 t.count_terms, t.count_host, max_count, t.gstack, t.counters, rpw)
+                 t.count_terms, t.count_host, max_count, t.gstack, t.counters, rpw, t.const_org, t.lit)
     if (t.count) {
         if (spill) PGRT_LAUNCH(true, true); else PGRT_LAUNCH(true, false);
     } else {
@@ -854,7 +862,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_occluded(SceneView s, const flo
     extern __shared__ int lstack[];  // [depth + 2][kTraceBlock]
     const int tid = threadIdx.x;
     for (int i = blockIdx.x * kTraceBlock + tid; i < n; i += gridDim.x * kTraceBlock) {
-        const float4 o4 = ro[i];
+            const float4 o4 = ro[i];
         const float4 d4 = rd[i];
         const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
         const float dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;

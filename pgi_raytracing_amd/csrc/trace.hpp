@@ -82,11 +82,15 @@ struct LevelNodes {  // per-level node records kept until the combine pass
 };
 
 struct ShadowQueue {  // one per batch: the shadow rays of every level, level-major
-    float4* ro;
+    float4* ro;       // NULL in the compact form (one light: every shadow ray starts at it)
     float4* rd;
-    float4* hit;
+    float4* hit;      // closest hits (full form); NULL in the compact form
     float4* contrib;  // (blue, green, red, -) Phong term of the owning node for this light
     int cap;
+    // compact form (one light, binary BVH): the shadow trace writes is_illuminated's verdict
+    // (raytracer.cpp:163-173: no hit, or a hit on a dielectric) as one byte per ray instead of a
+    // 16-B hit record, and reads no origin (LightSource::GenerateRay: org = the light)
+    unsigned char* lit;
 };
 
 // One closest-hit launch over a ray queue (ro/rd in, hits out).  Ray count: the sum of
@@ -114,6 +118,10 @@ struct TraceLaunch {
     bool packets = false;
     const PrimaryGen* gen = nullptr;
     unsigned long long* pkt_util = nullptr;  // packet launches: sampled utilisation sums (FrameCounters::pkt)
+    // shadow queues in the compact form (one-lane kernel): ro == NULL -> every ray starts at
+    // const_org (xyz, tnear in w); lit != NULL -> write is_illuminated's byte, not the hit
+    float4 const_org = make_float4(0, 0, 0, 0);
+    unsigned char* lit = nullptr;
 };
 // the packet traversal needs the binary layout and a tree that fits its wave-uniform stack
 bool trace_packets_available(const SceneView& s);
@@ -130,8 +138,15 @@ void launch_occluded(const SceneView& s, const float4* ro, const float4* rd, int
 // correct, a good guess -- last frame's count -- avoids dispatching empty workgroups)
 void launch_raygen(const CameraView& cam, const FrameParams& fp, const int4* tiles, Queue q, int n0,
                    FrameCounters* fc, hipStream_t stream);
+// level 0 of a pinhole frame traced as packets: the queue holds only directions (rd); every
+// valid ray starts at the camera (x, y, z) with tnear 0.001, in air
+struct PinholeOrigin {
+    float x, y, z;
+    int on;
+};
 void launch_shade(const SceneView& s, const FrameParams& fp, int level, Queue q, Queue next, LevelNodes nodes,
-                  ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect = 0);
+                  ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect,
+                  const PinholeOrigin& l0);
 // level L's final colours from its shadow hits and level L+1's colours (child)
 void launch_combine(const SceneView& s, int level, LevelNodes nodes, const float4* child, ShadowQueue sq,
                     const FrameCounters* fc, int max_count, hipStream_t stream, int expect = 0);

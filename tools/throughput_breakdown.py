@@ -5,7 +5,9 @@ Window: the middle 80 % of the trace's render calls (a call ends with one k_expo
 pipeline slot); per kernel: launches, device us per frame (durations overlap across calls in
 flight, so the column sums above the wall time), and, when given, HBM-side bytes per frame
 (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction).
-usage: python tools/throughput_breakdown.py <kernel_trace.csv> <frames_per_call> [fetch.csv write.csv]"""
+Further counter CSVs (extra arguments after fetch / write) are reported per kernel as the counter
+per frame (mean per launch x launches per frame), e.g. SQ_INSTS_VALU: wave-instructions per frame.
+usage: python tools/throughput_breakdown.py <kernel_trace.csv> <frames_per_call> [fetch.csv write.csv [more.csv ...]]"""
 import collections
 import csv
 import re
@@ -28,13 +30,14 @@ def load_trace(path):
     return rows
 
 
-def load_pmc(path, counter):
-    v = {}
+def load_pmc(path, counter=None):
+    """counter given: {kernel: [per-dispatch values]}; else {counter: {kernel: [values]}}"""
+    per = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(float)))
     with open(path) as f:
-        for r in csv.DictReader(f):
-            if r["Counter_Name"] == counter:
-                v.setdefault(short(r["Kernel_Name"]), []).append(float(r["Counter_Value"]))
-    return v
+        for r in csv.DictReader(f):  # one row per dispatch x counter (x instance: summed)
+            per[r["Counter_Name"]][short(r["Kernel_Name"])][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    out = {c: {k: list(d.values()) for k, d in kd.items()} for c, kd in per.items()}
+    return out.get(counter, {}) if counter else out
 
 
 def main():
@@ -80,6 +83,16 @@ def main():
             line += f"  {(2 * f_kb + w_kb) * 1024 * c / frames / 1e6:8.1f}"
         print(line)
     print(f"{'sum of kernel durations':40s} {'':7s} {tot / frames:9.2f}")
+    for extra in sys.argv[5:]:
+        for counter, kd in sorted(load_pmc(extra).items()):
+            print(f"\n{counter} per frame (launch-weighted):")
+            total = 0.0
+            for n, (c, _) in sorted(per.items(), key=lambda kv: -kv[1][1]):
+                if n in kd:
+                    v = sum(kd[n]) / len(kd[n]) * c / frames
+                    total += v
+                    print(f"  {n:40s} {v:14.4g}")
+            print(f"  {'total':40s} {total:14.4g}")
 
 
 if __name__ == "__main__":
