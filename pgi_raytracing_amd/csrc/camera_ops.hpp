@@ -22,6 +22,32 @@ __device__ __forceinline__ void tile_pixel(int slot_pix, const int4* tiles, int&
     py = tr.y + ly;
 }
 
+// Write the finished pixel o of batch slot pixel p (image pixel px, py) to fo.
+__device__ __forceinline__ void store_pixel(const FrameParams& fp, const int4* tiles, const FrameOut& fo, int p,
+                                            int px, int py, float4 o) {
+    if (fo.mode == 0) {
+        float* dst = fo.out + (size_t)frame_of_tile(fp, p / (kTile * kTile)) * fp.frame_stride +
+                     ((size_t)(py - fo.oy) * (size_t)fo.pitch + (size_t)(px - fo.ox)) * 4;
+        *reinterpret_cast<float4*>(dst) = o;
+        return;
+    }
+    const int tile = p / (kTile * kTile);
+    const int4 tr = tiles[tile];
+    size_t gtile = (size_t)tile * fo.K + fo.j;  // position in the caller's tile list
+    if (fp.frame_tiles > 0) {  // multi-frame call: frame f's tiles start at f * frame_out_tiles
+        const size_t f = gtile / fp.frame_tiles;
+        gtile += f * (size_t)(fp.frame_out_tiles - fp.frame_tiles);
+    }
+    const size_t q = gtile * kTile * kTile + (size_t)(py - tr.y) * kTile + (size_t)(px - tr.x);
+    if (fo.mode == 1) {
+        *reinterpret_cast<float4*>(fo.out + q * 4) = o;
+    } else {  // 2: RGB only (alpha is always 1): the multi-GPU gather moves 12 B per pixel
+        fo.out[q * 3 + 0] = o.x;
+        fo.out[q * 3 + 1] = o.y;
+        fo.out[q * 3 + 2] = o.z;
+    }
+}
+
 // Ray i of the batch (samples innermost): get_pixel's stratified sample position + jitter
 // (APP/raytracer.cpp:396-416) through Camera::GenerateRay, pinhole (PinHoleCamera.cpp:31-63) or
 // thin lens (:65-105).  ro = (org, tnear), rd = (dir, tfar).  Returns false for a padding slot
@@ -95,6 +121,22 @@ struct PrimaryGen {
     float4* store_rd;
     float* store_time;
     int* store_count;  // the level-0 ray count (FrameCounters::count0), k_raygen's other output
+    // 1-spp batches (L0Final): hit records are stored only for the rays that hit, and per wave
+    // the mask of those lanes (NULL: a hit record for every ray)
+    unsigned long long* hitmask;
 };
+
+// get_pixel's last step for batch slot pixel p of a 1-spp pixel whose sample colour is v:
+// final_color = 0 + v (raytracer.cpp:422-429, the "+=" onto a zero colour is kept: -0 -> +0),
+// gamma(Color4f{b, g, r}) (:431-435), written to fo (k_finish's output modes).
+__device__ __forceinline__ void store_final_1spp(const FrameParams& fp, const int4* tiles, const FrameOut& fo, int p,
+                                                 float4 v) {
+    int px, py;
+    bool valid;
+    tile_pixel(p, tiles, px, py, valid);
+    if (!valid) return;
+    const float4 acc = make_float4(0.0f + v.x, 0.0f + v.y, 0.0f + v.z, 1.0f);
+    store_pixel(fp, tiles, fo, p, px, py, gamma_rgba(acc.z, acc.y, acc.x, fp.gamma));
+}
 
 }  // namespace pgrt

@@ -111,6 +111,7 @@ struct FrameSlot {
     DevBuf<int4> tiles;
     DevBuf<float4> q_ro[2], q_rd[2], q_hit[2];
     DevBuf<float> q_time[2];
+    DevBuf<unsigned long long> l0_hit, l0_pending;  // 1-spp level-0 wave masks (L0Final)
     int q_cap = 0;
     std::vector<std::unique_ptr<DevBuf<float4>>> n_color, n_att;
     std::vector<std::unique_ptr<DevBuf<int4>>> n_link;
@@ -514,6 +515,8 @@ void ensure_frame_buffers(FrameSlot* sl, int n0, int levels, int nlight, int bat
             sl->q_hit[b].alloc(n0);
             sl->q_time[b].alloc(n0);
         }
+        sl->l0_hit.alloc((size_t)n0 / 64 + 1);
+        sl->l0_pending.alloc((size_t)n0 / 64 + 1);
         sl->q_cap = n0;
     }
     if ((int)sl->level_cap.size() < levels) sl->level_cap.resize(levels, 0);
@@ -745,8 +748,14 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             // pinhole level 0: the traversal stores directions only (the shade takes the origin,
             // tnear and medium from the camera: 20 B per primary ray written and read fewer)
             const bool dir_only = fuse && !p->dof;
+            // one sample per pixel: a pixel whose primary ray misses is finished by the level-0
+            // shade (L0Final), the finish completes the others
+            const bool l0final = fuse && spp == 1;
+            const FrameOut fo{fs->out, fs->out_mode, fs->ox, fs->oy, fs->pitch, K, j};
+            const L0Final l0f{l0final ? sl->l0_hit.p : nullptr, l0final ? sl->l0_pending.p : nullptr, fo,
+                              sl->tiles.p};
             const PrimaryGen gen{ctx->cam, fp, sl->tiles.p, dir_only ? nullptr : q[0].ro, q[0].rd,
-                                 dir_only ? nullptr : q[0].time, &fcd->count0};
+                                 dir_only ? nullptr : q[0].time, &fcd->count0, l0f.hit};
             int id = ctx->timer.begin(s, CAT_RAYGEN);
             if (!fuse) launch_raygen(ctx->cam, fp, sl->tiles.p, q[0], n0, fcd, s);
             debug_sync(s, "raygen", 0, bi);
@@ -781,7 +790,8 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 ++trace_launches;
                 id = ctx->timer.begin(s, CAT_SHADE, CAT_LSHADE + L);
                 const PinholeOrigin l0{ctx->cam.from[0], ctx->cam.from[1], ctx->cam.from[2], L == 0 && dir_only ? 1 : 0};
-                launch_shade(view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex, l0);
+                launch_shade(view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex, l0,
+                             L == 0 ? l0f : L0Final{nullptr, nullptr, fo, nullptr});
                 debug_sync(s, "shade", L, bi);
                 ctx->timer.end(s, id);
             }
@@ -822,8 +832,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                                n0);
             debug_sync(s, "combine", 0, bi);
             launch_finish(view, fp, sl->tiles.p, l0, levels > 1 ? sl->n_color[1]->p : sl->n_color[0]->p, sq,
-                          sl->accum.p, fs->out, fs->out_mode, fs->ox, fs->oy, fs->pitch, (int)npix, s0 == 0,
-                          s0 + fp.nsb >= spp, K, j, resolve_l0, s);
+                          sl->accum.p, fo, (int)npix, s0 == 0, s0 + fp.nsb >= spp, resolve_l0, l0f.pending, s);
             debug_sync(s, "finish", 0, bi);
             ctx->timer.end(s, id);
         }

@@ -55,11 +55,16 @@ void launch_raygen(const CameraView& cam, const FrameParams& fp, const int4* til
 // unconstrained 98 VGPRs allow -- r2c C2 A/B: 0.1938 -> 0.1901 ms/frame (5 waves 0.1907)
 constexpr int kShadeBlock = 256;
 static_assert(kShadeBlock % kBlock == 0, "k_shade blocks are whole multiples of kBlock");
+#ifndef PGRT_SHADE_L0F_WAVES
+#define PGRT_SHADE_L0F_WAVES 5
+#endif
+constexpr int kShadeL0fWaves = PGRT_SHADE_L0F_WAVES;
 
-template <bool LDS_TABLES>
-__global__ __launch_bounds__(kShadeBlock, 6) void k_shade(SceneView s, FrameParams fp, int level, Queue q, Queue next,
+// L0F: level 0 of a 1-spp batch (L0Final) -- final-colour pixels written here
+template <bool LDS_TABLES, bool L0F>
+__global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : 6) void k_shade(SceneView s, FrameParams fp, int level, Queue q, Queue next,
                                                        LevelNodes nodes, ShadowQueue sq, FrameCounters* fc,
-                                                       PinholeOrigin l0) {
+                                                       PinholeOrigin l0, L0Final l0f) {
     __shared__ float lut255[256];
     __shared__ DevMaterial smat[LDS_TABLES ? kLdsMats : 1];
     __shared__ DevTexture stex[LDS_TABLES ? kLdsTex : 1];
@@ -86,11 +91,19 @@ __global__ __launch_bounds__(kShadeBlock, 6) void k_shade(SceneView s, FramePara
     // level 0 of a pinhole frame: only the directions were stored (camera_ops.hpp PrimaryGen)
     const bool from_cam = l0.on != 0;
     const float4 cam_o = make_float4(l0.x, l0.y, l0.z, 0.001f);
+    // 1-spp level 0 (L0Final): a miss has no hit record (its mask bit is clear) and is finished here
+    constexpr bool l0final = L0F;
+    const float4 no_hit = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
+    auto load_hit = [&](int k) {
+        if (!l0final) return q.hit[k];
+        const unsigned long long hm = l0f.hit[__builtin_amdgcn_readfirstlane(k >> 6)];
+        return ((hm >> (k & 63)) & 1ull) ? q.hit[k] : no_hit;
+    };
     {
         const int i0 = blockIdx.x * kShadeBlock + tid;
         if (i0 < n) {
             nx_d = q.rd[i0];
-            nx_h = q.hit[i0];
+            nx_h = load_hit(i0);
             if (!from_cam) {
                 nx_o = q.ro[i0];
                 nx_t = q.time[i0];
@@ -105,7 +118,7 @@ __global__ __launch_bounds__(kShadeBlock, 6) void k_shade(SceneView s, FramePara
         const float cur_t = from_cam ? (cur_d.w >= 0.0f ? PGRT_IOR_AIR : 0.0f) : nx_t;
         if (i + stride < n) {
             nx_d = q.rd[i + stride];
-            nx_h = q.hit[i + stride];
+            nx_h = load_hit(i + stride);
             if (!from_cam) {
                 nx_o = q.ro[i + stride];
                 nx_t = q.time[i + stride];
@@ -114,22 +127,36 @@ __global__ __launch_bounds__(kShadeBlock, 6) void k_shade(SceneView s, FramePara
         ShadeOut r;
         shade_eval(s, mats, lut255, level, fp.max_level, active, cur_o, cur_d, cur_t, cur_h, r);
         const ShadeSlots sl = shade_alloc<kShadeBlock>(alds, it_par, fc, level, sq_base, sbits, r);
-        if (active) shade_emit(s, mats, level, i, r, sl, next, nodes, sq, fc);
+        if constexpr (l0final) {
+            // a final colour (environment texel; padding; a hit at max_level) -> the pixel, now;
+            // the others are completed by the finish (n is a multiple of 64: whole waves)
+            const bool fin = active && r.kind == 0;
+            const unsigned long long pend = __ballot(active && !fin);
+            if (active && __lane_id() == 0) l0f.pending[i >> 6] = pend;
+            if (fin) store_final_1spp(fp, l0f.tiles, l0f.fo, i, r.color);
+            if (active && !fin) shade_emit(s, mats, level, i, r, sl, next, nodes, sq, fc);
+        } else if (active) {
+            shade_emit(s, mats, level, i, r, sl, next, nodes, sq, fc);
+        }
     }
 }
 
 void launch_shade(const SceneView& s, const FrameParams& fp, int level, Queue q, Queue next, LevelNodes nodes,
                   ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect,
-                  const PinholeOrigin& l0) {
+                  const PinholeOrigin& l0, const L0Final& l0f) {
     if (max_count <= 0) return;
     const int per_block = kShadeBlock / kBlock;  // grid_for counts kBlock-thread blocks
     const int grid = std::max(1, grid_for(max_count, expect) / per_block);
-    if (s.nmat <= kLdsMats && s.ntex <= kLdsTex)
-        hipLaunchKernelGGL((k_shade<true>), dim3(grid), dim3(kShadeBlock), 0, stream, s, fp, level, q, next, nodes, sq,
-                           fc, l0);
-    else
-        hipLaunchKernelGGL((k_shade<false>), dim3(grid), dim3(kShadeBlock), 0, stream, s, fp, level, q, next, nodes, sq,
-                           fc, l0);
+    const bool lds = s.nmat <= kLdsMats && s.ntex <= kLdsTex;
+#define PGRT_LAUNCH_SHADE(T, F)                                                                                   \
+    hipLaunchKernelGGL((k_shade<T, F>), dim3(grid), dim3(kShadeBlock), 0, stream, s, fp, level, q, next, nodes, sq, \
+                       fc, l0, l0f)
+    if (l0f.hit) {
+        if (lds) PGRT_LAUNCH_SHADE(true, true); else PGRT_LAUNCH_SHADE(false, true);
+    } else {
+        if (lds) PGRT_LAUNCH_SHADE(true, false); else PGRT_LAUNCH_SHADE(false, false);
+    }
+#undef PGRT_LAUNCH_SHADE
 }
 
 // ------------------------------------------------------------------ combine + finish
@@ -198,9 +225,8 @@ void launch_combine(const SceneView& s, int level, LevelNodes nodes, const float
 
 __global__ __launch_bounds__(kBlock) void k_finish(SceneView s, FrameParams fp, const int4* __restrict__ tiles,
                                                    LevelNodes l0, const float4* __restrict__ child, ShadowQueue sq,
-                                                   float4* __restrict__ accum, float* __restrict__ out, int out_mode,
-                                                   int ox, int oy, int pitch, int npix, int first, int last, int K,
-                                                   int j, int resolved) {
+                                                   float4* __restrict__ accum, FrameOut fo, int npix, int first,
+                                                   int last, int resolved) {
     const int p = blockIdx.x * kBlock + threadIdx.x;
     if (p >= npix) return;
     float4 acc = first ? make_float4(0.0f, 0.0f, 0.0f, 1.0f) : accum[p];
@@ -225,35 +251,33 @@ __global__ __launch_bounds__(kBlock) void k_finish(SceneView s, FrameParams fp, 
     // x / 1 == x exactly: the (correctly rounded, ~10-instruction) divisions only for S > 1
     const float4 o = area == 1 ? gamma_rgba(acc.z, acc.y, acc.x, fp.gamma)
                                : gamma_rgba(acc.z / (float)area, acc.y / (float)area, acc.x / (float)area, fp.gamma);
-    if (out_mode == 0) {
-        float* dst = out + (size_t)frame_of_tile(fp, p / (kTile * kTile)) * fp.frame_stride +
-                     ((size_t)(py - oy) * (size_t)pitch + (size_t)(px - ox)) * 4;
-        *reinterpret_cast<float4*>(dst) = o;
-        return;
-    }
-    const int tile = p / (kTile * kTile);
-    const int4 tr = tiles[tile];
-    size_t gtile = (size_t)tile * K + j;  // position in the caller's tile list
-    if (fp.frame_tiles > 0) {  // multi-frame call: frame f's tiles start at f * frame_out_tiles
-        const size_t f = gtile / fp.frame_tiles;
-        gtile += f * (size_t)(fp.frame_out_tiles - fp.frame_tiles);
-    }
-    const size_t q = gtile * kTile * kTile + (size_t)(py - tr.y) * kTile + (size_t)(px - tr.x);
-    if (out_mode == 1) {
-        *reinterpret_cast<float4*>(out + q * 4) = o;
-    } else {  // 2: RGB only (alpha is always 1): the multi-GPU gather moves 12 B per pixel
-        out[q * 3 + 0] = o.x;
-        out[q * 3 + 1] = o.y;
-        out[q * 3 + 2] = o.z;
-    }
+    store_pixel(fp, tiles, fo, p, px, py, o);
+}
+
+// 1-spp batch whose level-0 shade finished every final-colour pixel (L0Final): the pixels of the
+// pending masks only
+__global__ __launch_bounds__(kBlock) void k_finish_pending(SceneView s, FrameParams fp, const int4* __restrict__ tiles,
+                                                           LevelNodes l0, const float4* __restrict__ child,
+                                                           ShadowQueue sq, FrameOut fo,
+                                                           const unsigned long long* __restrict__ pending, int npix) {
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= npix) return;
+    const unsigned long long pm = pending[__builtin_amdgcn_readfirstlane(p >> 6)];
+    if (((pm >> (p & 63)) & 1ull) == 0ull) return;
+    store_final_1spp(fp, tiles, fo, p, node_color(s, sq, l0, child, p));
 }
 
 void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles, LevelNodes l0, const float4* child,
-                   ShadowQueue sq, float4* accum, float* out, int out_mode, int ox, int oy, int pitch, int npix,
-                   bool first, bool last, int K, int j, bool resolved, hipStream_t stream) {
+                   ShadowQueue sq, float4* accum, const FrameOut& fo, int npix, bool first, bool last, bool resolved,
+                   const unsigned long long* pending, hipStream_t stream) {
     if (npix <= 0) return;
+    if (pending) {
+        hipLaunchKernelGGL(k_finish_pending, dim3(ceil_div(npix, kBlock)), dim3(kBlock), 0, stream, s, fp, tiles, l0,
+                           child, sq, fo, pending, npix);
+        return;
+    }
     hipLaunchKernelGGL(k_finish, dim3(ceil_div(npix, kBlock)), dim3(kBlock), 0, stream, s, fp, tiles, l0, child, sq,
-                       accum, out, out_mode, ox, oy, pitch, npix, first ? 1 : 0, last ? 1 : 0, K, j, resolved ? 1 : 0);
+                       accum, fo, npix, first ? 1 : 0, last ? 1 : 0, resolved ? 1 : 0);
 }
 
 // ------------------------------------------------------------------ multi-GPU unpack

@@ -736,6 +736,19 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const fl
                 node = sp > 0 ? wstack[wib][--sp] : kSentinel;
             }
         }
+        if constexpr (GEN) {
+            if (gen.hitmask) {  // 1-spp level 0 (L0Final): hit records of the hits only + the wave's mask
+                const bool hit = live && best_prim >= 0;
+                const unsigned long long hm = __ballot(hit);
+                if (hit) hits[i] = make_float4(best_t, best_u, best_v, __int_as_float(best_prim));
+                if (lane == 0) gen.hitmask[base >> 6] = hm;
+                if (COUNT && lane == 0) {
+                    nvis += rvis;
+                    ntest += rtest;
+                }
+                continue;
+            }
+        }
         if (valid) hits[i] = make_float4(live ? best_t : tfar, best_u, best_v, __int_as_float(best_prim));
         if (COUNT && lane == 0) {
             nvis += rvis;

@@ -75,6 +75,27 @@ struct Queue {
     int cap;
 };
 
+// Where a batch's finished pixels go (k_finish; the level-0 packet traversal for primary-ray
+// misses of a 1-spp frame).  mode 0: framebuffer (rect origin ox,oy, row pitch in pixels);
+// 1: tile-compact RGBA; 2: tile-compact RGB (the multi-GPU gather format).  The launch's tiles
+// are tiles j, j + K, ... of the caller's list (pipeline slot j of K).
+struct FrameOut {
+    float* out;
+    int mode, ox, oy, pitch, K, j;
+};
+
+// Level 0 of a 1-spp batch traced as packets (PrimaryGen): a pixel whose primary ray misses has
+// one colour, the environment texel (raytracer.cpp:390-393), so get_pixel's sum and gamma
+// (:422-435) follow in the level-0 shade, which writes it to fo at once -- no node record, no
+// finish.  hit: per 64-ray wave, the lanes whose ray hit (the traversal stores no hit record for
+// a miss); pending: per wave, the lanes the finish still has to complete (set by the shade).
+struct L0Final {
+    unsigned long long* hit;
+    unsigned long long* pending;
+    FrameOut fo;
+    const int4* tiles;
+};
+
 struct LevelNodes {  // per-level node records kept until the combine pass
     float4* color;
     int4* link;      // dielectric: (refl child, refr child or -1, -, -); opaque: (-1,-1,shadow base, n)
@@ -144,21 +165,20 @@ struct PinholeOrigin {
     float x, y, z;
     int on;
 };
+// l0f.hit != NULL: level 0 of a 1-spp batch (L0Final)
 void launch_shade(const SceneView& s, const FrameParams& fp, int level, Queue q, Queue next, LevelNodes nodes,
                   ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect,
-                  const PinholeOrigin& l0);
+                  const PinholeOrigin& l0, const L0Final& l0f);
 // level L's final colours from its shadow hits and level L+1's colours (child)
 void launch_combine(const SceneView& s, int level, LevelNodes nodes, const float4* child, ShadowQueue sq,
                     const FrameCounters* fc, int max_count, hipStream_t stream, int expect = 0);
-// level-0 combine + sample accumulation (+ gamma and framebuffer write on the last batch).
-// out_mode 0: framebuffer (rect origin ox,oy, row pitch in pixels); 1: tile-compact RGBA;
-// 2: tile-compact RGB (the multi-GPU gather format)
-// tiles of this launch are tiles j, j + K, ... of the caller's list (pipeline slot j of K):
-// out_mode 1 writes local tile t at tile-compact position t * K + j.  resolved: level 0's final
-// colours were written by launch_combine(level 0) (several samples per pixel)
+// level-0 combine + sample accumulation (+ gamma and the output write on the last batch, fo).
+// resolved: level 0's final colours were written by launch_combine(level 0) (several samples
+// per pixel).  l0f.pending != NULL (1 spp, L0Final): only the pixels whose bit is set there are
+// finished (the others were written by the level-0 shade).
 void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles, LevelNodes l0, const float4* child,
-                   ShadowQueue sq, float4* accum, float* out, int out_mode, int ox, int oy, int pitch, int npix,
-                   bool first, bool last, int K, int j, bool resolved, hipStream_t stream);
+                   ShadowQueue sq, float4* accum, const FrameOut& fo, int npix, bool first, bool last,
+                   bool resolved, const unsigned long long* pending, hipStream_t stream);
 // frame sink: sum += frame (count-th frame; count == 1 resets), mean = sum / count
 void launch_accumulate_frame(const float* frame, float* sum, float* mean, long long pixels, int count,
                              hipStream_t stream);
