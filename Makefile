@@ -10,7 +10,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off \
             -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -I$(SRC) -Wall -Wno-unused-result
 OBJS := $(BUILD)/trace.o $(BUILD)/render.o $(BUILD)/bvh.o $(BUILD)/ploc.o $(BUILD)/split.o $(BUILD)/bvh8.o $(BUILD)/context.o $(BUILD)/objloader.o
 
-all: $(LIBDIR)/libpgrt.so oracle $(BUILD)/pg1_pgrt
+all: $(LIBDIR)/libpgrt.so $(LIBDIR)/libpgrt_image.so oracle $(BUILD)/pg1_pgrt
 
 $(BUILD) $(LIBDIR):
 	mkdir -p $@
@@ -25,6 +25,12 @@ $(BUILD)/%.o: $(SRC)/%.cpp $(HDRS) | $(BUILD)
 
 $(LIBDIR)/libpgrt.so: $(OBJS) | $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+
+# JPEG textures decoded like the reference's FreeImage JPEG_DEFAULT load (IJG libjpeg 9, IFAST
+# IDCT, no fancy upsampling; csrc/image_jpeg.c).  libjpeg 9 ships with this image under /opt/conda.
+JPEG_PREFIX ?= /opt/conda
+$(LIBDIR)/libpgrt_image.so: $(SRC)/image_jpeg.c | $(LIBDIR)
+	gcc -O2 -std=c11 -Wall -shared -fPIC -I$(JPEG_PREFIX)/include -o $@ $< -L$(JPEG_PREFIX)/lib -ljpeg -Wl,-rpath,$(JPEG_PREFIX)/lib
 
 # C++ host example over the C ABI (include/pgrt_raytracer.hpp)
 $(BUILD)/pg1_pgrt: examples/pg1_pgrt.cpp include/pgrt_raytracer.hpp include/pgrt.h $(LIBDIR)/libpgrt.so | $(BUILD)

@@ -21,12 +21,47 @@ def freeimage_pitch(width: int, bpp: int) -> int:
     return ((width * bpp * 8 + 31) // 32) * 4
 
 
+_JPEG = None
+
+
+def _jpeg_lib():
+    """libpgrt_image.so (csrc/image_jpeg.c): IJG libjpeg 9 with FreeImage's JPEG_DEFAULT load
+    settings (IFAST IDCT, no fancy upsampling)."""
+    global _JPEG
+    if _JPEG is None:
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libpgrt_image.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} is missing: build it with `make` (JPEG textures are decoded like "
+                               "FreeImage's JPEG_DEFAULT load, texture.cpp:5-54)")
+        lib = C.CDLL(path)
+        lib.pgrt_jpeg_decode.argtypes = [C.c_char_p, C.c_int] + [C.POINTER(C.c_int)] * 4 + [C.c_void_p, C.c_size_t]
+        lib.pgrt_jpeg_decode.restype = C.c_int
+        lib.pgrt_jpeg_error.restype = C.c_char_p
+        _JPEG = lib
+    return _JPEG
+
+
+def decode_jpeg(path: str, accurate: bool = False):
+    """(width, height, bpp, pitch, bytes): BGR, top-down, FreeImage pitch.  accurate=False is
+    FreeImage's JPEG_DEFAULT (IFAST); True its JPEG_ACCURATE (ISLOW + fancy upsampling)."""
+    lib = _jpeg_lib()
+    w, h, b, p = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    args = (path.encode(), 1 if accurate else 0, C.byref(w), C.byref(h), C.byref(b), C.byref(p))
+    if lib.pgrt_jpeg_decode(*args, None, 0) != 0:
+        raise RuntimeError(lib.pgrt_jpeg_error().decode())
+    buf = np.zeros(p.value * h.value, np.uint8)
+    if lib.pgrt_jpeg_decode(*args, buf.ctypes.data, buf.size) != 0:
+        raise RuntimeError(lib.pgrt_jpeg_error().decode())
+    return w.value, h.value, b.value, p.value, buf
+
+
 @dataclass
 class TextureData:
     """Texture::Texture (texture.cpp:5-54): raw BGR(A), top-down, FreeImage pitch.
 
-    Decoded with PIL (FreeImage is not available).  PNG is lossless, so test3/test4 texels
-    are exact; JPEG bytes can differ from FreeImage's JPEG_DEFAULT (IFAST DCT) decode."""
+    JPEG: FreeImage_Load with flags 0 = JPEG_DEFAULT (FreeImage.h:693-695), i.e. IJG libjpeg's
+    fast integer IDCT without fancy upsampling (decode_jpeg, libpgrt_image.so).  PNG: PIL
+    (lossless, so the bytes are FreeImage's)."""
 
     width: int
     height: int
@@ -37,7 +72,10 @@ class TextureData:
 
     @staticmethod
     def from_file(path: str) -> "TextureData":
-        from PIL import Image  # host-side decode only
+        if path.lower().endswith((".jpg", ".jpeg")):
+            w, h, bpp, pitch, buf = decode_jpeg(path)
+            return TextureData(w, h, pitch, bpp, buf, os.path.basename(path))
+        from PIL import Image  # host-side PNG decode only
 
         im = Image.open(path)
         if im.mode not in ("RGB", "RGBA"):

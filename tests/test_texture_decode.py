@@ -1,0 +1,63 @@
+"""JPEG texture decode as the reference gets it (§8 A15 / f1).
+
+Texture::Texture (APP/texture.cpp:5-54) loads through FreeImage_Load(fif, file, 0): flags 0 is
+JPEG_DEFAULT = "loading (see JPEG_FAST)" (FreeImage.h:693-695), i.e. IJG libjpeg's fast integer
+IDCT without fancy upsampling, then FreeImage_ConvertToRawBits(top-down) -> BGR rows of
+FreeImage_GetPitch bytes.  libpgrt_image.so (csrc/image_jpeg.c) drives IJG libjpeg 9 with those
+settings.  The wrapper itself is checked against an independent decoder (PIL/libjpeg-turbo) in
+its accurate mode on the 4:4:4 environment map, where both decoders implement the same ISLOW
+IDCT; FreeImage itself is absent, so the IFAST bytes are pinned by the decoder settings, not by
+a FreeImage-produced fixture.
+"""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from pgi_raytracing_amd.scene import TextureData, decode_jpeg
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ENV = os.path.join(ROOT, "assets", "spherical_map_windows.jpg")
+JPEGS = [ENV, os.path.join(ROOT, "assets", "avenger", "4150p04.jpg"),
+         os.path.join(ROOT, "assets", "avenger", "3069bp13.jpg")]
+
+
+def _rgb(w, h, pitch, buf):
+    return buf.reshape(h, pitch)[:, : w * 3].reshape(h, w, 3)[:, :, ::-1]
+
+
+def test_wrapper_matches_independent_decoder_in_accurate_mode():
+    from PIL import Image
+
+    w, h, bpp, pitch, buf = decode_jpeg(ENV, accurate=True)
+    assert (w, h, bpp, pitch) == (4000, 2000, 3, 12000)
+    pil = np.asarray(Image.open(ENV).convert("RGB")).astype(int)
+    d = np.abs(_rgb(w, h, pitch, buf).astype(int) - pil)
+    assert d.max() <= 1 and (d > 0).mean() < 1e-4  # libjpeg 9 vs libjpeg-turbo ISLOW rounding
+
+
+def test_default_load_is_the_fast_idct():
+    fast = decode_jpeg(ENV)[4]
+    slow = decode_jpeg(ENV, accurate=True)[4]
+    diff = np.abs(fast.astype(int) - slow.astype(int))
+    assert 0.01 < (diff > 0).mean() < 0.2  # IFAST's scaled-integer rounding, not a different image
+    assert diff.max() <= 8
+
+
+@pytest.mark.parametrize("path", JPEGS)
+def test_texture_and_sidecar_are_the_ifast_decode(path):
+    w, h, bpp, pitch, buf = decode_jpeg(path)
+    assert pitch % 4 == 0 and pitch >= w * 3
+    t = TextureData.from_file(path)
+    assert (t.width, t.height, t.bpp, t.pitch) == (w, h, bpp, pitch)
+    assert np.array_equal(t.data, buf)
+    side = path + ".pgrttex"
+    if not os.path.exists(side):
+        pytest.skip("sidecars are written by __graft_entry__.build()")
+    with open(side, "rb") as f:
+        assert f.read(8) == b"PGRTTEX1"
+        sw, sh, sp, sb = struct.unpack("<4i", f.read(16))
+        data = np.frombuffer(f.read(), np.uint8)
+    assert (sw, sh, sp, sb) == (w, h, pitch, bpp)
+    assert np.array_equal(data, buf)
