@@ -400,17 +400,59 @@ def main():
             dist.destroy_process_group()
         return
 
-    host_fb = None
+    host = None
     if world == 1 and not args.no_roofline:
-        # PCIe-inclusive rate: the same frame through pgrt_render into a host
-        # framebuffer (device -> host copy of W*H*16 B per frame); never the headline value
-        for _ in range(2):
-            ctx.render(params)
-        t1 = time.perf_counter()
-        nh = max(3, min(args.steps // 2, 100))
-        for _ in range(nh):
-            ctx.render(params)
-        host_fb = round((time.perf_counter() - t1) / nh * 1e3, 4)
+        # host-framebuffer figures (PCIe-inclusive; never the headline value).  SURVEY §8(d)'s
+        # ms/frame: pgrt_render from camera upload to the framebuffer on the host, median of >= 10
+        # frames after 2 warm-ups (into page-locked memory, as a D3D upload heap would be);
+        # throughput: pgrt_render_frames_host_async, F frames per call, their D2H copy (W*H*16 B
+        # per frame) queued behind them and overlapped with the calls in flight
+        fb_host = ctx.host_array((args.height, args.width, 4))
+        try:
+            for _ in range(2):
+                ctx.render(params, out=fb_host)
+            lat_h = []
+            for _ in range(max(10, min(args.steps, 30))):
+                t1 = time.perf_counter()
+                ctx.render(params, out=fb_host)
+                lat_h.append(time.perf_counter() - t1)
+        finally:
+            ctx.host_free(fb_host)
+        ring = min(in_flight, 4)
+        bufs = [ctx.host_array((F, args.height, args.width, 4)) for _ in range(ring)]
+        try:
+            ctx.set_frames_in_flight(ring)
+            calls = max(2 * ring, 96 // F)
+
+            def host_calls(n):
+                pend = deque()
+                for k in range(n):
+                    pend.append(ctx.render_frames_host_async(params, F, bufs[k % ring]))
+                    if len(pend) >= ring:
+                        ctx.render_wait(pend.popleft())
+                while pend:
+                    ctx.render_wait(pend.popleft())
+
+            host_calls(ring)
+            t1 = time.perf_counter()
+            host_calls(calls)
+            dt = time.perf_counter() - t1
+        finally:
+            ctx.set_frames_in_flight(in_flight)
+            for b in bufs:
+                ctx.host_free(b)
+        fb_bytes = args.width * args.height * 16
+        host = {
+            "ms_per_frame_sync_median": round(sorted(lat_h)[len(lat_h) // 2] * 1e3, 4),
+            "ms_per_frame_async": round(dt / (calls * F) * 1e3, 4),
+            "async_frames": calls * F,
+            "async_calls_in_flight": ring,
+            "frame_bytes": fb_bytes,
+            "pcie_d2h_gbs": round(calls * F * fb_bytes / dt / 1e9, 2),
+            "note": "sync: SURVEY 8(d) definition (pgrt_render into a page-locked host framebuffer, median of "
+                    f"{len(lat_h)} after 2 warm-ups); async: pgrt_render_frames_host_async throughput, bound by "
+                    "the device-to-host copy of W*H*16 B per frame",
+        }
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -450,7 +492,8 @@ def main():
             "gather_ms_per_call": round(sum(gather_ms) / len(gather_ms), 4) if gather_ms else None,
             "rank0_share": f"{share[0]}/{share[1]}" if share else None,
             "roofline": roof,
-            "host_framebuffer_ms_per_step": host_fb,
+            "host_framebuffer_ms_per_step": host["ms_per_frame_sync_median"] if host else None,
+            "host_framebuffer": host,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -244,6 +244,18 @@ int pgrt_render_frames_device_async(pgrt_ctx* ctx, const pgrt_render_params* p, 
 /* Synchronous form of the batched frames (profile allowed: stage timings cover all nframes). */
 int pgrt_render_frames_device(pgrt_ctx* ctx, const pgrt_render_params* p, int nframes,
                               void* rgba_device, pgrt_stats* st);
+/* Batched frames to a HOST framebuffer (the reference's Producer hands every finished frame to
+ * the host-side D3D texture, APP/simpleguidx11.cpp:105-124): frames are rendered into a device
+ * staging buffer owned by the frame in flight, then ONE device-to-host copy of nframes * W*H*4
+ * floats into rgba_host is queued behind them, so the PCIe transfer of one call overlaps the
+ * rendering of the calls in flight behind it.  rgba_host must stay valid until the ticket is
+ * waited for; pinned memory from pgrt_host_alloc makes the copy a true asynchronous DMA (pageable
+ * memory works but copies synchronously).  Same pixels as pgrt_render_frames_device. */
+int pgrt_render_frames_host_async(pgrt_ctx* ctx, const pgrt_render_params* p, int nframes,
+                                  float* rgba_host, unsigned long long* ticket);
+/* Page-locked host memory for framebuffers (pgrt_render, pgrt_render_frames_host_async). */
+int pgrt_host_alloc(pgrt_ctx* ctx, size_t bytes, void** out);
+int pgrt_host_free(pgrt_ctx* ctx, void* ptr);
 
 /* ---- batched closest-hit query with rtcIntersect1 semantics ----
  * rays: n x 8 floats {org.xyz, tnear, dir.xyz, tfar}; hits: n x 4 {t, u, v, prim} where prim

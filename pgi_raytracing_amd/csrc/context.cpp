@@ -183,6 +183,12 @@ struct FrameSet {
     TileDeal deal{1, 1, 1};  // distributed: the tile deal this frame was rendered with
     float* dist_fb = nullptr;
     DevBuf<float> tilebuf;  // distributed: this rank's tiles, tile-compact
+    // host-output frames (pgrt_render_frames_host_async): rendered into host_stage, then ONE
+    // device-to-host copy of host_bytes into host_dst on the set's first slot stream, overlapped
+    // with the frames in flight behind it
+    DevBuf<float> host_stage;
+    float* host_dst = nullptr;
+    size_t host_bytes = 0;
     int cam_w = 0, cam_h = 0;  // image size at submission (the gather's layout)
     pgrt_stats stats{};
     std::chrono::steady_clock::time_point t0;
@@ -842,6 +848,12 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
         debug_sync(s, "export", 0, 0);
         PGRT_HIP(hipEventRecord(sl->ev_done, s));
     }
+    if (fs->host_dst && K > 0) {  // host output: after every slot, on slot 0's stream
+        FrameSlot* s0 = fs->slots[0].get();
+        for (int j = 1; j < K; ++j) PGRT_HIP(hipStreamWaitEvent(s0->stream, fs->slots[j]->ev_done, 0));
+        PGRT_HIP(hipMemcpyAsync(fs->host_dst, fs->host_stage.p, fs->host_bytes, hipMemcpyDeviceToHost, s0->stream));
+        PGRT_HIP(hipEventRecord(s0->ev_done, s0->stream));
+    }
     PGRT_HIP(hipGetLastError());
     fs->stats.trace_launches = trace_launches;
 }
@@ -1097,6 +1109,7 @@ void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<
                   long long frame_stride = 0) {
     drain_frames(ctx);
     FrameSet* fs = frame_set(ctx, 0);
+    fs->host_dst = nullptr;
     PGRT_HIP(hipEventRecord(fs->ev_ready, ctx->stream));  // prior context-stream work first
     start_frame(ctx, fs, p, tiles, out, out_mode, ox, oy, pitch, false, nullptr, nframes, frame_stride);
     finish_frame(ctx, fs);
@@ -1555,8 +1568,8 @@ int pgrt_set_frames_in_flight(pgrt_ctx* ctx, int n) {
 
 namespace {
 int submit_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device, unsigned long long* ticket,
-                 bool distributed, int nframes = 1) {
-    if (!ctx || !p || !ticket || (!distributed && !rgba_device)) return PGRT_ERR_INVALID_ARGUMENT;
+                 bool distributed, int nframes = 1, float* rgba_host = nullptr) {
+    if (!ctx || !p || !ticket || (!distributed && !rgba_device && !rgba_host)) return PGRT_ERR_INVALID_ARGUMENT;
     if (nframes < 1 || nframes > kMaxFramesPerCall) return PGRT_ERR_INVALID_ARGUMENT;
     return guarded(ctx, [&] {
         PGRT_REQUIRE(ctx->has_cam, PGRT_ERR_NO_CAMERA, "pgrt_set_camera has not been called");
@@ -1565,6 +1578,7 @@ int submit_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device, 
                      "rank 0 needs an output buffer");
         FrameSet* fs = frame_set(ctx, (int)(ctx->next_ticket % (unsigned long long)ctx->frames_in_flight));
         if (fs->pending) finish_through(ctx, fs->ticket);  // the set's previous frame completes first
+        fs->host_dst = nullptr;
         // pgrt_config.max_batches_in_flight: bound the sample batches queued across frames in
         // flight (this frame's own count estimated with one slot per frame, as enqueue_frame deals
         // them when frames are in flight)
@@ -1600,6 +1614,12 @@ int submit_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device, 
         } else {
             int x, y, w, h;
             frame_rect(ctx, p, x, y, w, h);
+            fs->host_dst = rgba_host;
+            fs->host_bytes = (size_t)nframes * w * h * 4 * sizeof(float);
+            if (rgba_host) {
+                fs->host_stage.alloc((size_t)nframes * w * h * 4);
+                rgba_device = fs->host_stage.p;
+            }
             start_frame(ctx, fs, p, rect_tiles(x, y, w, h), static_cast<float*>(rgba_device), 0, x, y, w, false,
                         nullptr, nframes, (long long)w * h * 4);
         }
@@ -1611,6 +1631,25 @@ int submit_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device, 
 int pgrt_render_frames_device_async(pgrt_ctx* ctx, const pgrt_render_params* p, int nframes, void* rgba_device,
                                     unsigned long long* ticket) {
     return submit_async(ctx, p, rgba_device, ticket, false, nframes);
+}
+
+int pgrt_render_frames_host_async(pgrt_ctx* ctx, const pgrt_render_params* p, int nframes, float* rgba_host,
+                                  unsigned long long* ticket) {
+    if (!rgba_host) return PGRT_ERR_INVALID_ARGUMENT;
+    return submit_async(ctx, p, nullptr, ticket, false, nframes, rgba_host);
+}
+
+int pgrt_host_alloc(pgrt_ctx* ctx, size_t bytes, void** out) {
+    if (!ctx || !out) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault);
+        if (e != hipSuccess) throw Error(PGRT_ERR_OUT_OF_MEMORY, hipGetErrorString(e));
+    });
+}
+
+int pgrt_host_free(pgrt_ctx* ctx, void* ptr) {
+    if (!ctx) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] { PGRT_HIP(hipHostFree(ptr)); });
 }
 
 int pgrt_render_frames_distributed_device_async(pgrt_ctx* ctx, const pgrt_render_params* p, int nframes,

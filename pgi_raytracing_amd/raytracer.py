@@ -69,6 +69,9 @@ def lib():
         "pgrt_render_frames_device": (ip, [vp, C.POINTER(abi.RenderParams), ip, vp, C.POINTER(abi.Stats)]),
         "pgrt_render_frames_distributed_device_async": (ip, [vp, C.POINTER(abi.RenderParams), ip, vp,
                                                              C.POINTER(C.c_ulonglong)]),
+        "pgrt_render_frames_host_async": (ip, [vp, C.POINTER(abi.RenderParams), ip, fp, C.POINTER(C.c_ulonglong)]),
+        "pgrt_host_alloc": (ip, [vp, C.c_size_t, C.POINTER(vp)]),
+        "pgrt_host_free": (ip, [vp, vp]),
         "pgrt_tile_count": (ip, [ip, ip, ip, ip, ip]),
         "pgrt_tile_index": (ip, [ip, ip, ip, ip, ip, ip]),
         "pgrt_tile_share": (ip, [ip, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
@@ -173,10 +176,14 @@ class Context:
         _check(self.h, self.L.pgrt_set_camera(self.h, C.byref(cam)))
         self.camera = cam
 
-    def render(self, params: abi.RenderParams):
+    def render(self, params: abi.RenderParams, out: np.ndarray | None = None):
+        """One frame to a host framebuffer (pgrt_render); `out` (h, w, 4) float32, e.g. pinned
+        memory from host_array, is written in place."""
         w = params.rect_w if params.rect_w > 0 else self.camera.width
         h = params.rect_h if params.rect_h > 0 else self.camera.height
-        out = np.empty((h, w, 4), np.float32)
+        if out is None:
+            out = np.empty((h, w, 4), np.float32)
+        assert out.dtype == np.float32 and out.flags.c_contiguous and out.size == h * w * 4
         st = abi.Stats()
         _check(self.h, self.L.pgrt_render(self.h, C.byref(params), abi.fptr(out), C.byref(st)))
         return out, st
@@ -193,6 +200,16 @@ class Context:
 
     def free(self, ptr: int):
         _check(self.h, self.L.pgrt_device_free(self.h, C.c_void_p(ptr)))
+
+    def host_array(self, shape) -> np.ndarray:
+        """float32 array in page-locked host memory (pgrt_host_alloc); free with host_free."""
+        n = int(np.prod(shape))
+        p = C.c_void_p()
+        _check(self.h, self.L.pgrt_host_alloc(self.h, n * 4, C.byref(p)))
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_float)), shape=(n,)).reshape(shape)
+
+    def host_free(self, arr: np.ndarray):
+        _check(self.h, self.L.pgrt_host_free(self.h, C.c_void_p(arr.ctypes.data)))
 
     def to_host(self, ptr: int, shape, dtype=np.float32) -> np.ndarray:
         out = np.empty(shape, dtype)
@@ -276,6 +293,15 @@ class Context:
         _check(self.h, self.L.pgrt_render_frames_device(self.h, C.byref(params), nframes, C.c_void_p(dev_ptr),
                                                         C.byref(st)))
         return st
+
+    def render_frames_host_async(self, params, nframes: int, out: np.ndarray) -> int:
+        """Enqueue nframes frames whose pixels are copied to the host array `out` (nframes, h, w, 4)
+        behind them (pgrt_render_frames_host_async); `out` must live until the ticket is waited."""
+        assert out.dtype == np.float32 and out.flags.c_contiguous
+        t = C.c_ulonglong()
+        _check(self.h, self.L.pgrt_render_frames_host_async(self.h, C.byref(params), nframes, abi.fptr(out),
+                                                            C.byref(t)))
+        return t.value
 
     def render_frames_distributed_device_async(self, params, nframes: int, dev_ptr: int | None) -> int:
         t = C.c_ulonglong()

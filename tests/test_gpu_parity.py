@@ -344,6 +344,21 @@ def test_batched_frames_match_single(gpu_ctx, avenger_scene):
             if not rect[2]:  # the distributed form renders the whole camera image
                 gpu_ctx.render_wait(gpu_ctx.render_frames_distributed_device_async(p, F, dbuf))
                 checks.append(("distributed frames", gpu_ctx.to_host(dbuf, (F, H, W, 4))))
+            # host output (pinned): two calls in flight, then one call on the 2-slot synchronous set
+            for n_in_flight in (2, 1):
+                gpu_ctx.set_frames_in_flight(n_in_flight)
+                hb = [gpu_ctx.host_array((F, h, w, 4)) for _ in range(2)]
+                try:
+                    for a in hb:
+                        a.fill(-7.0)
+                    ts = [gpu_ctx.render_frames_host_async(p, F, a) for a in hb]
+                    assert gpu_ctx.render_wait(ts[-1]).rays() == st0.rays()
+                    for k, a in enumerate(hb):
+                        checks.append((f"host frames {n_in_flight}/{k}", a.copy()))
+                finally:
+                    for a in hb:
+                        gpu_ctx.host_free(a)
+            gpu_ctx.set_frames_in_flight(2)
             for f, (ref, _) in enumerate(refs):
                 for name, o in ((n, a[f]) for n, a in checks):
                     same = (o == ref) | (np.isnan(o) & np.isnan(ref))
