@@ -88,6 +88,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (multi-thread leg)")
     ap.add_argument("--packet-levels", type=int, default=None,
                     help="A/B only: pgrt_config.packet_levels (default AUTO: chosen per level by libpgrt)")
+    ap.add_argument("--group-max", type=int, default=None,
+                    help="A/B only: pgrt_config.group_max (queues up to it: 8 lanes per ray)")
     a = ap.parse_args()
     for k, v in CONFIGS[a.config].items():
         if getattr(a, k, None) is None:
@@ -252,6 +254,8 @@ def main():
     ctx = Context(local_rank)
     if args.packet_levels is not None:
         ctx.configure(packet_levels=args.packet_levels)
+    if args.group_max is not None:
+        ctx.configure(group_max=args.group_max)
     ctx.set_scene(scene)
     ctx.set_camera(cam)
     bvh = ctx.bvh_info()
