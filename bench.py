@@ -90,6 +90,8 @@ def parse():
                     help="A/B only: pgrt_config.packet_levels (default AUTO: chosen per level by libpgrt)")
     ap.add_argument("--group-max", type=int, default=None,
                     help="A/B only: pgrt_config.group_max (queues up to it: 8 lanes per ray)")
+    ap.add_argument("--cfg", action="append", default=[],
+                    help="A/B only: pgrt_config field=value (repeatable), e.g. --cfg bvh_width=8")
     a = ap.parse_args()
     for k, v in CONFIGS[a.config].items():
         if getattr(a, k, None) is None:
@@ -256,6 +258,9 @@ def main():
         ctx.configure(packet_levels=args.packet_levels)
     if args.group_max is not None:
         ctx.configure(group_max=args.group_max)
+    for kv in args.cfg:
+        k, v = kv.split("=", 1)
+        ctx.configure(**{k: float(v) if "." in v else int(v)})
     ctx.set_scene(scene)
     ctx.set_camera(cam)
     bvh = ctx.bvh_info()

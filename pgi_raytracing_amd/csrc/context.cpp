@@ -421,7 +421,7 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
     PGRT_HIP(hipMemcpyAsync(ctx->mats.p, mats.data(), mats.size() * sizeof(DevMaterial), hipMemcpyHostToDevice, st));
     ctx->texd.alloc(texs.size());
     PGRT_HIP(hipMemcpyAsync(ctx->texd.p, texs.data(), texs.size() * sizeof(DevTexture), hipMemcpyHostToDevice, st));
-    ctx->texels.alloc((size_t)std::max(1ll, pool));
+    ctx->texels.alloc((size_t)std::max(1ll, pool) + 16);  // + the 12-byte texel window's overhang (shade_ops.hpp)
     for (int i = 0; i < d->num_textures; ++i)
         PGRT_HIP(hipMemcpyAsync(ctx->texels.p + texs[i].offset, d->textures[i].data, (size_t)texs[i].size,
                                 hipMemcpyHostToDevice, st));

@@ -377,8 +377,8 @@ __global__ void k_selftest(const float* in, int n, float* out) {
     o[1] = a / b;
     o[2] = gamma_pow(a, b);  // == pg_powf(a, b), with k_finish's exact y = 0.5 shortcut
     o[3] = pg_expf(a);
-    o[4] = pg_atan2f(a, b);
-    o[5] = pg_asinf(a);
+    o[4] = atan2f_env(a, b);  // == pg_atan2f(a, b): the env map's fast path with its rounding test
+    o[5] = asinf_env(a);      // == pg_asinf(a)
     o[6] = 1 / sqrtf(a);
     o[7] = (float)pg_pow_d((double)a, (double)b);
 }

@@ -66,6 +66,24 @@ __device__ __forceinline__ V3 tex_pixel(const DevTexture& t, const unsigned char
     return v3(lut[p[0]], lut[p[1]], lut[p[2]]);
 }
 
+// Two horizontally adjacent texels whose bytes start at offset off (both in bounds): the bytes
+// off .. off + 7 from three aligned dwords (v_alignbyte_b32 funnel shifts), the same values as
+// two tex_pixel calls.  Reads up to 12 bytes past off & ~3: set_scene pads the texel pool for it.
+__device__ __forceinline__ void tex_row_pair(const DevTexture& t, const unsigned char* pool, const float* lut,
+                                             long long off, V3& a, V3& b) {
+    const unsigned char* p = pool + t.offset + off;
+    const unsigned k = (unsigned)((uintptr_t)p & 3u);
+    const unsigned* w = reinterpret_cast<const unsigned*>((uintptr_t)p & ~(uintptr_t)3);
+    const unsigned w0 = w[0], w1 = w[1], w2 = w[2];
+    const unsigned lo = __builtin_amdgcn_alignbyte(w1, w0, k);  // bytes off .. off + 3
+    const unsigned hi = __builtin_amdgcn_alignbyte(w2, w1, k);  // bytes off + 4 .. off + 7
+    a = v3(lut[lo & 0xffu], lut[(lo >> 8) & 0xffu], lut[(lo >> 16) & 0xffu]);
+    if (t.bpp == 3)
+        b = v3(lut[lo >> 24], lut[hi & 0xffu], lut[(hi >> 8) & 0xffu]);
+    else
+        b = v3(lut[hi & 0xffu], lut[(hi >> 8) & 0xffu], lut[(hi >> 16) & 0xffu]);
+}
+
 // Texture::get_texel (APP/texture.cpp:77-130): bilinear with the reference's edge quirks.
 __device__ inline V3 tex_texel(const DevTexture& t, const unsigned char* pool, const float* lut, float u, float v) {
     const float x = u * (float)t.width;
@@ -78,8 +96,20 @@ __device__ inline V3 tex_texel(const DevTexture& t, const unsigned char* pool, c
     const int y1 = (tmp_y1 < 1) ? tmp_y1 + 1 : tmp_y1;
     const int y2 = (tmp_y2 == t.height) ? tmp_y1 : tmp_y2;
     if (x1 == x2 || y1 == y2) return v3(0, 0, 0);
-    const V3 x1y1 = tex_pixel(t, pool, lut, x1, y1), x2y1 = tex_pixel(t, pool, lut, x2, y1);
-    const V3 x1y2 = tex_pixel(t, pool, lut, x1, y2), x2y2 = tex_pixel(t, pool, lut, x2, y2);
+    V3 x1y1, x2y1, x1y2, x2y2;
+    const long long o1 = (long long)y1 * t.pitch + (long long)x1 * t.bpp;
+    const long long o2 = (long long)y2 * t.pitch + (long long)x1 * t.bpp;
+    if (x2 == x1 + 1 && t.bpp <= 4 && o1 >= 0 && o2 >= 0 && o1 + t.bpp + 2 < t.size && o2 + t.bpp + 2 < t.size) {
+        // the usual case: both taps of a row are neighbours inside the texture -> one aligned
+        // 12-byte window per row (the texel pool is padded for it) instead of 6 byte loads
+        tex_row_pair(t, pool, lut, o1, x1y1, x2y1);
+        tex_row_pair(t, pool, lut, o2, x1y2, x2y2);
+    } else {
+        x1y1 = tex_pixel(t, pool, lut, x1, y1);
+        x2y1 = tex_pixel(t, pool, lut, x2, y1);
+        x1y2 = tex_pixel(t, pool, lut, x1, y2);
+        x2y2 = tex_pixel(t, pool, lut, x2, y2);
+    }
     // the denominators are 1 except at the wrap / clamp quirks: q / 1 == q exactly, so the
     // (correctly rounded, ~10-instruction) division only runs where it can change the value
     const float dx = (float)(x2 - x1), dy = (float)(y2 - y1);
@@ -93,12 +123,71 @@ __device__ inline V3 tex_texel(const DevTexture& t, const unsigned char* pool, c
     return v3(f1.x * wy2 + f2.x * wy1, f1.y * wy2 + f2.y * wy1, f1.z * wy2 + f2.z * wy1);
 }
 
+// ---- env-map angles, fast and still bit-identical to pg_atan2f / pg_asinf ----
+// atan2 in double with FMA, a Newton-refined v_rcp_f64 instead of the correctly rounded divides,
+// a 10-term series after the same pi/6 reduction (truncation < 5e-14 absolute) and a hardware
+// sqrt for asin's cosine: within 1e-12 relative of the exact double pg_atan2_d computes (itself
+// within 5e-15 of atan2).  Ziv's rounding test then decides: when a +- 1e-12 |a| rounds to ONE
+// float, that float is (float)pg_atan2_d's result (rounding is monotonic); otherwise (about 3e-5
+// of the lookups) the exact pgrt_detmath.h function runs.  Tested bit for bit against the
+// exact functions on the device (pgrt_selftest_env, tests/test_gpu_parity.py).
+__device__ __forceinline__ double rcp_refined(double d) {  // d normal and > 0: ~1 ulp
+    double r = __builtin_amdgcn_rcp(d);
+    r = fma(r, fma(-d, r, 1.0), r);
+    return fma(r, fma(-d, r, 1.0), r);
+}
+__device__ __forceinline__ double atan2_approx(double y, double x) {  // x, y finite, nonzero
+    const double ay = fabs(y), ax = fabs(x);
+    const bool swap = ay > ax;
+    double q = (swap ? ax : ay) * rcp_refined(swap ? ay : ax);  // in (0, 1]
+    double base = 0.0;
+    if (q > 0.26794919243112270647) {  // tan(pi/12): atan q = pi/6 + atan((q sqrt3 - 1) / (q + sqrt3))
+        q = fma(q, 1.73205080756887729353, -1.0) * rcp_refined(q + 1.73205080756887729353);
+        base = PG_PI_D / 6.0;
+    }
+    const double z = q * q;  // <= 0.0718
+    double p = -1.0 / 19.0;
+    p = fma(p, z, 1.0 / 17.0);
+    p = fma(p, z, -1.0 / 15.0);
+    p = fma(p, z, 1.0 / 13.0);
+    p = fma(p, z, -1.0 / 11.0);
+    p = fma(p, z, 1.0 / 9.0);
+    p = fma(p, z, -1.0 / 7.0);
+    p = fma(p, z, 1.0 / 5.0);
+    p = fma(p, z, -1.0 / 3.0);
+    p = fma(p, z, 1.0);
+    double r = fma(q, p, base);
+    if (swap) r = PG_PI_D / 2.0 - r;
+    if (x < 0.0) r = PG_PI_D - r;
+    return y < 0.0 ? -r : r;
+}
+// (float)a's value when it is decided by a +- 1e-12 |a| (else NaN: undecided)
+__device__ __forceinline__ float round_decided(double a) {
+    const double e = fabs(a) * 1e-12;
+    const float lo = (float)(a - e), hi = (float)(a + e);
+    return lo == hi ? lo : __builtin_nanf("");
+}
+__device__ inline float atan2f_env(float y, float x) {  // == pg_atan2f(y, x)
+    const float ay = fabsf(y), ax = fabsf(x);
+    float f = __builtin_nanf("");
+    if (ay > 1e-30f && ax > 1e-30f && ay < 1e30f && ax < 1e30f) f = round_decided(atan2_approx(y, x));
+    return f == f ? f : pg_atan2f(y, x);
+}
+__device__ inline float asinf_env(float x) {  // == pg_asinf(x)
+    float f = __builtin_nanf("");
+    if (fabsf(x) > 1e-30f && fabsf(x) < 0.9999f) {
+        const double xd = (double)x;
+        f = round_decided(atan2_approx(xd, sqrt(1.0 - xd * xd)));
+    }
+    return f == f ? f : pg_asinf(x);
+}
+
 // SphericalMap::get_texel (APP/SphericalMap.cpp:17-29): returns RGBA with a = 1.
 __device__ inline float4 env_texel(const SceneView& s, const float* lut, V3 d) {
     if (s.env < 0) return make_float4(0, 0, 0, 1);
     const V3 vec = normalize(v3(d.x, d.z, d.y));
-    const float u = (float)(0.5 + (double)pg_atan2f(vec.x, vec.z) / (2 * 3.14159265358979323846));
-    const float v = (float)(0.5 - (double)pg_asinf(vec.y) / 3.14159265358979323846);
+    const float u = (float)(0.5 + (double)atan2f_env(vec.x, vec.z) / (2 * 3.14159265358979323846));
+    const float v = (float)(0.5 - (double)asinf_env(vec.y) / 3.14159265358979323846);
     const V3 c = tex_texel(s.tex[s.env], s.texels, lut, u, v);
     return make_float4(c.z, c.y, c.x, 1.0f);
 }

@@ -46,6 +46,29 @@ def test_device_math_bit_exact(gpu_ctx):
     assert same.all(), f"{len(bad)} mismatches, first {bad[:5]}: dev {dev[tuple(bad[0])]} host {host[tuple(bad[0])]}"
 
 
+def test_env_angles_fast_path_bit_exact(gpu_ctx):
+    """The env-map lookup's atan2f / asinf (columns 4, 5: a double-precision approximation with
+    Ziv's rounding test, the exact pgrt_detmath.h function when undecided) equal the host's exact
+    functions bit for bit on 4M unit-vector-like arguments -- about 3e-5 of them take the exact
+    fallback, so both branches run -- plus signed zeros, tiny, huge and near-1 values."""
+    rng = np.random.default_rng(11)
+    v = rng.normal(size=(1 << 22, 3))
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    a = v[:, 0].astype(np.float32)
+    b = v[:, 2].astype(np.float32)
+    edge = np.array([0.0, -0.0, 1e-31, -1e-31, 1e-20, 0.9998999, 0.9999, -0.9999001, 1.0, -1.0, 1e31, 3e38,
+                     np.inf, -np.inf, np.nan, 0.5, -0.5], np.float32)
+    ea, eb = np.meshgrid(edge, edge)
+    pairs = np.ascontiguousarray(np.stack([np.concatenate([a, ea.ravel()]), np.concatenate([b, eb.ravel()])], 1))
+    dev = gpu_ctx.selftest_math(pairs)[:, 4:6]
+    host = np.zeros((pairs.shape[0], 8), np.float32)
+    pyoracle.lib().orc_detmath_eval(abi.fptr(pairs.reshape(-1)), pairs.shape[0], abi.fptr(host.reshape(-1)))
+    host = host[:, 4:6]
+    same = (dev.view(np.uint32) == host.view(np.uint32)) | (np.isnan(dev) & np.isnan(host))
+    bad = np.argwhere(~same)
+    assert same.all(), f"{len(bad)} mismatches, first {bad[:5]}: pairs {pairs[bad[:5, 0]]}"
+
+
 def test_tutorial1_kat_on_gpu(gpu_ctx):
     gpu_ctx.set_scene(single_triangle_scene())
     ray = np.array([0.1, 0.2, 2.0, FLT_MIN, 0.0, 0.0, -1.0, FLT_MAX], np.float32)
