@@ -6,10 +6,12 @@ cd "$(dirname "$0")/.."
 TAG=${1:-r1}
 OUT=gpurun_out/bench_$TAG.txt
 : > "$OUT"
+echo "=== C2 driver-style (--steps 20 --warmup 5)" >&2
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > "gpurun_out/bench_${TAG}_C2_k20.json" 2> "gpurun_out/bench_${TAG}_C2_k20.err" || exit $?
 for cfg in C2 C3 C4 C5; do
-    extra="--no-cpu-baseline"
+    extra=""
     steps=""
-    [ $cfg = C2 ] && extra=""
+    [ $cfg = C4 ] && extra="--no-cpu-baseline"
     [ $cfg = C3 ] && steps="--steps 20 --warmup 3"
     [ $cfg = C4 ] && steps="--steps 6 --warmup 2"
     [ $cfg = C5 ] && steps="--steps 20 --warmup 3"
