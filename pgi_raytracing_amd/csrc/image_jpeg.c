@@ -19,6 +19,8 @@
 
 #include <jpeglib.h>
 
+#include "pgrt_image.h"
+
 struct err_mgr {
     struct jpeg_error_mgr pub;
     jmp_buf jb;

@@ -23,6 +23,17 @@ JPEGS = [ENV, os.path.join(ROOT, "assets", "avenger", "4150p04.jpg"),
          os.path.join(ROOT, "assets", "avenger", "3069bp13.jpg")]
 
 
+def test_image_library_exports_its_header():
+    import ctypes as C
+    import re
+
+    text = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "pgrt_image.h")).read(), flags=re.S)
+    names = sorted(set(re.findall(r"\b(pgrt_[a-z0-9_]+)\s*\(", text)))
+    lib = C.CDLL(os.path.join(ROOT, "pgi_raytracing_amd", "lib", "libpgrt_image.so"))
+    assert names == ["pgrt_jpeg_decode", "pgrt_jpeg_error"]
+    assert all(hasattr(lib, n) for n in names)
+
+
 def _rgb(w, h, pitch, buf):
     return buf.reshape(h, pitch)[:, : w * 3].reshape(h, w, 3)[:, :, ::-1]
 
