@@ -8,14 +8,14 @@ SRC     := pgi_raytracing_amd/csrc
 # -ffp-contract=off: no implicit FMA, so every float op rounds exactly like the CPU restatement
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off \
             -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -I$(SRC) -Wall -Wno-unused-result
-OBJS := $(BUILD)/trace.o $(BUILD)/render.o $(BUILD)/bvh.o $(BUILD)/ploc.o $(BUILD)/split.o $(BUILD)/bvh8.o $(BUILD)/context.o $(BUILD)/objloader.o
+OBJS := $(BUILD)/trace.o $(BUILD)/render.o $(BUILD)/bvh.o $(BUILD)/ploc.o $(BUILD)/split.o $(BUILD)/bvh8.o $(BUILD)/path.o $(BUILD)/context.o $(BUILD)/objloader.o
 
 all: $(LIBDIR)/libpgrt.so $(LIBDIR)/libpgrt_image.so oracle $(BUILD)/pg1_pgrt
 
 $(BUILD) $(LIBDIR):
 	mkdir -p $@
 
-HDRS := include/pgrt.h include/pgrt_detmath.h $(SRC)/common.hpp $(SRC)/trace.hpp $(SRC)/shade_ops.hpp $(SRC)/camera_ops.hpp $(SRC)/shade_ray.hpp $(SRC)/tiles.hpp
+HDRS := include/pgrt.h include/pgrt_detmath.h $(SRC)/common.hpp $(SRC)/trace.hpp $(SRC)/shade_ops.hpp $(SRC)/camera_ops.hpp $(SRC)/shade_ray.hpp $(SRC)/tiles.hpp $(SRC)/path.hpp
 
 $(BUILD)/%.o: $(SRC)/%.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@

@@ -53,6 +53,14 @@ extern "C" {
 /* Jitter modes for the stratified sample offsets r1,r2 (raytracer.cpp:407-410) and the lens
  * offsets (PinHoleCamera.cpp:77-81).  The reference seeds std::mt19937 from the wall clock,
  * which is not reproducible; these modes are counter-based and deterministic. */
+/* render modes: the reference's recursive Whitted trace (raytracer.cpp:237-437), or the path
+ * tracer of its README "To do" list (README.md:17-21; semantics in DESIGN.md §2 "Path tracing"):
+ * one continuation ray per hit -- a cosine-weighted diffuse bounce off Phong/Lambert materials,
+ * reflection OR refraction of a dielectric chosen with the reference's Fresnel-like R -- and
+ * next-event estimation with hard shadow rays from the hit point to every light */
+#define PGRT_MODE_WHITTED 0
+#define PGRT_MODE_PATH 1
+
 #define PGRT_JITTER_NONE 0            /* r1 = r2 = 0, lens offset 0 */
 #define PGRT_JITTER_HASH 1            /* independent hashed uniforms per (pixel, sample) */
 #define PGRT_JITTER_HASH_CORRELATED 2 /* lens uniforms == jitter uniforms, as when both
@@ -124,6 +132,7 @@ typedef struct pgrt_render_params {
     uint32_t frame;
     int rect_x, rect_y, rect_w, rect_h; /* sub-rectangle; rect_w==0 -> full frame */
     int profile;          /* 0 off, 1 per-stage HIP-event timing, 2 + traversal counters */
+    int mode;             /* PGRT_MODE_WHITTED (0, the reference's trace) or PGRT_MODE_PATH */
 } pgrt_render_params;
 
 typedef struct pgrt_stats {

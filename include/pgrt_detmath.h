@@ -316,4 +316,19 @@ PGRT_HD float pg_jitter_u01(uint32_t seed, uint32_t frame, uint32_t pixel, uint3
     return (float)(h >> 8) * (1.0f / 16777216.0f);
 }
 
+/* ---- path tracing random numbers (PGRT_MODE_PATH) ----
+ * key = counter hash of (seed, frame, global pixel, sample) -- a stream of its own, apart from
+ * pg_jitter_u01's; u = U[0,1) for (bounce, k) of that path: k = 0 the dielectric choice,
+ * k = 1 + 2j, 2 + 2j the j-th disk-sample candidate of a diffuse bounce. */
+PGRT_HD uint32_t pg_path_key(uint32_t seed, uint32_t frame, uint32_t pixel, uint32_t sample)
+{
+    return pg_hash32(pg_hash32(pg_hash32(pg_hash32(seed ^ 0x68bc21ebu) ^ frame) ^ pixel) ^ sample);
+}
+
+PGRT_HD float pg_path_u01(uint32_t key, uint32_t bounce, uint32_t k)
+{
+    uint32_t h = pg_hash32(key ^ pg_hash32(bounce * 64u + k + 1u));
+    return (float)(h >> 8) * (1.0f / 16777216.0f);
+}
+
 #endif /* PGRT_DETMATH_H_ */

@@ -770,6 +770,174 @@ static C4 get_pixel(const orc_scene* s, const Cam* k, const pgrt_render_params* 
     return gamma4(in, p->gamma_level);
 }
 
+/* ------------------------------------------------------------------ path tracing
+ * PGRT_MODE_PATH: the "Whole pathtracing" item of the reference's README to-do list
+ * (README.md:17-21).  The reference has no path tracer; the semantics are this project's
+ * (DESIGN.md §2 "Path tracing") built from the reference's own pieces: trace()'s hit setup
+ * (raytracer.cpp:241-288), the dielectric's reflection / refraction rays, attenuation and
+ * Fresnel-like R (:294-316, :178-235), the Phong term of shade_phong (:355-382) and the
+ * environment lookup on a miss (:390-393).  Per path, in this order per bounce b:
+ *   miss                -> L += T * env(dir), end
+ *   hit, b >= max_level -> end (raytracer.cpp:282-283)
+ *   dielectric          -> T *= attenuation; reflect if TIR or u < R, else refract
+ *   other               -> for every light with n . (Lp - H) > 0: a hard shadow ray from H
+ *                          towards the light (tnear 0.01, tfar |Lp - H|; a dielectric occluder
+ *                          lets the light through, raytracer.cpp:166-172); lit -> L += T * Phong
+ *                          term; then T *= albedo and a cosine-weighted bounce (Malley's method,
+ *                          rejection-sampled disk, Duff et al.'s orthonormal basis); T == 0 ends
+ * Colours use trace()'s channel convention (C4.r carries Kd[0] / the texel's .b, as in
+ * shade_phong's "blue" variable).  Random numbers: pg_path_u01 (pgrt_detmath.h). */
+
+/* Building an orthonormal basis, revisited (Duff et al. 2017) */
+static void onb(V3 n, V3* b1, V3* b2)
+{
+    const float sign = copysignf(1.0f, n.z);
+    const float a = -1.0f / (sign + n.z);
+    const float b = n.x * n.y * a;
+    *b1 = v3(1.0f + sign * n.x * n.x * a, sign * b, -sign * n.x);
+    *b2 = v3(b, sign + n.y * n.y * a, -n.y);
+}
+
+/* cosine-weighted direction about n: a uniform point of the unit disk (up to 8 rejection
+ * candidates, else the pole) lifted to the hemisphere */
+static V3 cosine_dir(uint32_t key, uint32_t bounce, V3 n)
+{
+    float x = 0.0f, y = 0.0f;
+    for (uint32_t j = 0; j < 8u; ++j) {
+        const float a = 2.0f * pg_path_u01(key, bounce, 1u + 2u * j) - 1.0f;
+        const float c = 2.0f * pg_path_u01(key, bounce, 2u + 2u * j) - 1.0f;
+        if (a * a + c * c < 1.0f) { x = a; y = c; break; }
+    }
+    const float z = sqrtf(1.0f - (x * x + y * y));
+    V3 b1, b2;
+    onb(n, &b1, &b2);
+    return v3(x * b1.x + y * b2.x + z * n.x, x * b1.y + y * b2.y + z * n.y, x * b1.z + y * b2.z + z * n.z);
+}
+
+static C4 path_sample(const orc_scene* s, Ray r, int max_level, uint32_t key, Counters* cn)
+{
+    C4 L = {0.0f, 0.0f, 0.0f, 1.0f};
+    float tr = 1.0f, tg = 1.0f, tb = 1.0f; /* throughput, C4 channel order */
+    for (int b = 0;; ++b) {
+        Hit h = scene_intersect(s, &r, &cn->tests);
+        V3 d = v_normalize(r.dir);
+        if (h.prim < 0) {
+            C4 e = env_texel(s, d.x, d.y, d.z);
+            L.r = L.r + tr * e.r;
+            L.g = L.g + tg * e.g;
+            L.b = L.b + tb * e.b;
+            break;
+        }
+        const float* nn = s->nrm + 9 * h.prim;
+        V3 n = v3(interp1(nn[0], nn[3], nn[6], h.u, h.v), interp1(nn[1], nn[4], nn[7], h.u, h.v),
+                  interp1(nn[2], nn[5], nn[8], h.u, h.v));
+        const pgrt_material* m = &s->mats[s->mat[h.prim]];
+        n = v_normalize(n);
+        V3 hit = v_add(r.org, v_scale(h.t, r.dir));
+        float n1, n2;
+        if (r.time == PGRT_IOR_AIR) { n1 = PGRT_IOR_AIR; n2 = m->ior; }
+        else { n1 = m->ior; n2 = PGRT_IOR_AIR; }
+        if (v_dot(n, d) > 0) n = v_neg(n);
+        if (b >= max_level) break;
+        if (m->type == PGRT_MATERIAL_DIELECTRIC) {
+            Ray rr = reflection_ray(d, n, hit, n1);
+            const float ar = M_EXPF(-(1 - m->diffuse[0]) * h.t);
+            const float ag = M_EXPF(-(1 - m->diffuse[1]) * h.t);
+            const float ab = M_EXPF(-(1 - m->diffuse[2]) * h.t);
+            Ray fr = refraction_ray(d, n, n1, n2, hit);
+            int refract = 0;
+            if (fr.dir.x == fr.dir.x) { /* no total internal reflection */
+                float cos1 = fabsf(v_dot(n, v_neg(d)));
+                float alpha = (n1 - n2) / (n1 + n2);
+                float R = (float)((double)(alpha * alpha + (1 - (alpha * alpha))) * M_POWD((double)(1 - cos1), 5.0));
+                refract = !(pg_path_u01(key, (uint32_t)b, 0u) < R);
+            }
+            tr = tr * ar;
+            tg = tg * ag;
+            tb = tb * ab;
+            if (refract) { r = fr; cn->refract++; }
+            else { r = rr; cn->reflect++; }
+            continue;
+        }
+        /* diffuse colour as shade_phong (raytracer.cpp:337-349) */
+        float m_d_r, m_d_g, m_d_b;
+        if (m->diffuse_tex < 0) {
+            m_d_r = m->diffuse[2]; m_d_g = m->diffuse[1]; m_d_b = m->diffuse[0];
+        } else {
+            const float* t = s->uv + 6 * h.prim;
+            float tu = interp1(t[0], t[2], t[4], h.u, h.v);
+            float tv = interp1(t[1], t[3], t[5], h.u, h.v);
+            C3 texel = tex_texel(&s->tex[m->diffuse_tex], tu, 1.0f - tv);
+            m_d_r = texel.r; m_d_g = texel.g; m_d_b = texel.b;
+        }
+        for (int li = 0; li < s->nlight; ++li) { /* next-event estimation, hard shadows */
+            const pgrt_light* Lt = &s->lights[li];
+            V3 lp = v3(Lt->position[0], Lt->position[1], Lt->position[2]);
+            V3 tol = v3(lp.x - hit.x, lp.y - hit.y, lp.z - hit.z);
+            if (!(v_dot(n, tol) > 0)) continue;
+            V3 lv = v_normalize(tol);
+            Ray sr;
+            sr.org = hit; sr.dir = lv; sr.tnear = 0.01f; sr.tfar = v_len(tol); sr.time = 0.0f;
+            cn->shadow++;
+            Hit sh = scene_intersect(s, &sr, &cn->tests);
+            if (sh.prim >= 0 && s->mats[s->mat[sh.prim]].type != PGRT_MATERIAL_DIELECTRIC) continue;
+            V3 cv = v_normalize(v3(r.org.x - r.dir.x, r.org.y - r.dir.y, r.org.z - r.dir.z));
+            float i_d_r = Lt->diffuse[2], i_d_g = Lt->diffuse[1], i_d_b = Lt->diffuse[0];
+            float i_s_r = Lt->specular[2], i_s_g = Lt->specular[1], i_s_b = Lt->specular[0];
+            float m_s_r = m->specular[2], m_s_g = m->specular[1], m_s_b = m->specular[0];
+            float nl = v_dot(n, lv);
+            V3 l_r = v_sub(v_scale(2 * nl, n), lv);
+            l_r = v_normalize(l_r);
+            float spec = M_POWF(v_dot(cv, l_r), m->shininess);
+            float blue = i_d_b * m_d_b * v_dot(n, lv) + i_s_b * m_s_b * spec;
+            float green = i_d_g * m_d_g * v_dot(n, lv) + i_s_g * m_s_g * spec;
+            float red = i_d_r * m_d_r * v_dot(n, lv) + i_s_r * m_s_r * spec;
+            L.r = L.r + tr * blue;
+            L.g = L.g + tg * green;
+            L.b = L.b + tb * red;
+        }
+        tr = tr * m_d_b;
+        tg = tg * m_d_g;
+        tb = tb * m_d_r;
+        if (!(tr > 0.0f || tg > 0.0f || tb > 0.0f)) break;
+        V3 nd = cosine_dir(key, (uint32_t)b, n);
+        Ray next;
+        next.org = hit; next.dir = nd; next.tnear = 0.01f; next.tfar = FLT_MAX; next.time = r.time;
+        r = next;
+        cn->reflect++;
+    }
+    return L;
+}
+
+/* get_pixel (raytracer.cpp:396-437) with path_sample in place of trace */
+static C4 get_pixel_path(const orc_scene* s, const Cam* k, const pgrt_render_params* p, int px, int py,
+                         Counters* cn)
+{
+    const int S = p->spp_side;
+    C4 sum = {0.0f, 0.0f, 0.0f, 1.0f};
+    uint32_t pixel = (uint32_t)py * (uint32_t)k->width + (uint32_t)px;
+    for (int sx = 0; sx < S; ++sx) {
+        for (int sy = 0; sy < S; ++sy) {
+            float j[4];
+            const uint32_t sample = (uint32_t)(sx * S + sy);
+            jitter4(p, pixel, sample, (float)S, j);
+            float nx = (float)px + ((float)sx * (1.0f / (float)S)) + j[0];
+            float ny = (float)py + ((float)sy * (1.0f / (float)S)) + j[1];
+            Ray r = p->dof ? cam_ray_dof(k, nx, ny, p->focal_distance, j[2], j[3])
+                           : cam_ray_pinhole(k, nx, ny);
+            r.time = PGRT_IOR_AIR;
+            cn->primary++;
+            C4 c = path_sample(s, r, p->max_level, pg_path_key(p->seed, p->frame, pixel, sample), cn);
+            sum.r += c.r;
+            sum.g += c.g;
+            sum.b += c.b;
+        }
+    }
+    const int area = S * S;
+    C4 in = {sum.b / (float)area, sum.g / (float)area, sum.r / (float)area, 1.0f};
+    return gamma4(in, p->gamma_level);
+}
+
 /* ------------------------------------------------------------------ API */
 orc_scene* orc_scene_create(const pgrt_scene_desc* d, int accel)
 {
@@ -844,7 +1012,7 @@ int orc_render(const orc_scene* s, const pgrt_camera* cam, const pgrt_render_par
         Counters cn = {0, 0, 0, 0, 0, 0};
         int y = ry + ri * row_step;
         for (int x = rx; x < rx + rw; ++x) {
-            C4 c = get_pixel(s, &k, p, x, y, &cn);
+            C4 c = p->mode == PGRT_MODE_PATH ? get_pixel_path(s, &k, p, x, y, &cn) : get_pixel(s, &k, p, x, y, &cn);
             float* o = rgba + ((size_t)(y - ry) * (size_t)rw + (size_t)(x - rx)) * 4;
             o[0] = c.r; o[1] = c.g; o[2] = c.b; o[3] = c.a;
         }

@@ -19,6 +19,7 @@ PGRT_OK = 0
 PGRT_MATERIAL_DIELECTRIC = 4
 PGRT_IOR_AIR = np.float32(1.000293)
 PGRT_JITTER_NONE, PGRT_JITTER_HASH, PGRT_JITTER_HASH_CORRELATED = 0, 1, 2
+PGRT_MODE_WHITTED, PGRT_MODE_PATH = 0, 1
 
 ERRORS = {
     -1: "PGRT_ERR_INVALID_ARGUMENT",
@@ -105,6 +106,7 @@ class RenderParams(C.Structure):
         ("rect_w", C.c_int),
         ("rect_h", C.c_int),
         ("profile", C.c_int),
+        ("mode", C.c_int),
     ]
 
 
@@ -195,7 +197,8 @@ def iptr(a: np.ndarray):
 
 
 def make_params(spp_side=1, max_level=5, dof=0, focal_distance=200.0, aperture=5.0, gamma_level=0.5,
-                jitter=PGRT_JITTER_NONE, seed=1234, frame=0, rect=(0, 0, 0, 0), profile=0) -> RenderParams:
+                jitter=PGRT_JITTER_NONE, seed=1234, frame=0, rect=(0, 0, 0, 0), profile=0,
+                mode=PGRT_MODE_WHITTED) -> RenderParams:
     p = RenderParams()
     p.spp_side = spp_side
     p.max_level = max_level
@@ -208,6 +211,7 @@ def make_params(spp_side=1, max_level=5, dof=0, focal_distance=200.0, aperture=5
     p.frame = frame
     p.rect_x, p.rect_y, p.rect_w, p.rect_h = rect
     p.profile = profile
+    p.mode = mode
     return p
 
 

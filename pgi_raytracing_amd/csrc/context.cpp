@@ -17,6 +17,7 @@
 #include "trace.hpp"
 #include "camera_ops.hpp"
 #include "shade_ray.hpp"
+#include "path.hpp"
 #include "tiles.hpp"
 
 using namespace pgrt;
@@ -667,6 +668,86 @@ int group_max(const pgrt_ctx* ctx) {
     return ctx->frames_in_flight > 1 ? kDefaultGroupMaxInFlight : kDefaultGroupMax;
 }
 
+// One sample batch of a PGRT_MODE_PATH frame (path.hip): raygen, then per bounce L the closest
+// hits of the path queue, the bounce's shading, its shadow rays and their resolve; the finish
+// sums each pixel's path accumulators (a resolved level 0) and writes the output like a Whitted
+// frame.  Per-path state lives in the level node buffers: n_color[0] = accumulators,
+// n_link[L] (as int) = path index, n_att[L] = throughput of bounce L's queue.
+void enqueue_path_batch(pgrt_ctx* ctx, FrameSlot* sl, const SceneView& view, const FrameParams& fp,
+                        const pgrt_render_params* p, const Queue* q, FrameCounters* fcd, int n0, const FrameOut& fo,
+                        int npix, bool first, bool last, int bi, int& trace_launches) {
+    hipStream_t s = sl->stream;
+    const int levels = p->max_level + 1;
+    int id = ctx->timer.begin(s, CAT_RAYGEN);
+    launch_raygen(ctx->cam, fp, sl->tiles.p, q[0], n0, fcd, s);
+    ctx->timer.end(s, id);
+    debug_sync(s, "path raygen", 0, bi);
+    const ShadowQueue sq{sl->s_ro.p, sl->s_rd.p, sl->s_hit.p, sl->s_contrib.p, sl->s_cap, nullptr};
+    float4* acc = sl->n_color[0]->p;
+    const int nl = std::max(1, view.nlight);
+    for (int L = 0; L < levels; ++L) {
+        Queue qc = q[L & 1], qn = q[(L + 1) & 1];
+        const int maxc = L == 0 ? n0 : std::min(sl->q_cap, sl->level_cap[L]);
+        qc.cap = maxc;
+        qn.cap = std::min(sl->q_cap, L + 1 < levels ? sl->level_cap[L + 1] : sl->q_cap);
+        const int ex = L == 0 ? n0 : sl->expect_count[L];
+        TraceLaunch tl;
+        tl.ro = qc.ro;
+        tl.rd = qc.rd;
+        tl.hits = qc.hit;
+        tl.count_dev = fc_count_ptr(fcd, L);
+        tl.max_count = maxc;
+        tl.expect = ex;
+        tl.gstack = sl->gstack.p;
+        tl.gstack_threads = kTraceGridThreads;
+        tl.counters = fcd->trav[L];
+        tl.count = p->profile >= 2;
+        tl.packets = packet_level(ctx, L);
+        tl.pkt_util = fcd->pkt[L];
+        id = ctx->timer.begin_kernel(CAT_TRACE, CAT_LTRACE + L);
+        const bool launched = launch_trace(view, tl, s);
+        ctx->timer.end_kernel(s, id, launched);
+        ++trace_launches;
+        debug_sync(s, "path trace", L, bi);
+        const PathState ps{L > 0 ? reinterpret_cast<const int*>(sl->n_link[L]->p) : nullptr,
+                           L > 0 ? sl->n_att[L]->p : nullptr,
+                           L + 1 < levels ? reinterpret_cast<int*>(sl->n_link[L + 1]->p) : nullptr,
+                           L + 1 < levels ? sl->n_att[L + 1]->p : nullptr, acc};
+        id = ctx->timer.begin(s, CAT_SHADE, CAT_LSHADE + L);
+        launch_path_shade(view, fp, ctx->cam.width, sl->tiles.p, L, qc, qn, ps, sq, fcd, maxc, ex, s);
+        ctx->timer.end(s, id);
+        debug_sync(s, "path shade", L, bi);
+        if (view.nlight > 0 && L < p->max_level) {  // this bounce's hard shadow rays
+            TraceLaunch st;
+            st.ro = sq.ro;
+            st.rd = sq.rd;
+            st.hits = sq.hit;
+            st.count_dev = fc_shadow_counts(fcd) + 2 * L;
+            st.max_count = sq.cap;
+            st.expect = (int)std::min<long long>((long long)ex * nl, sq.cap);
+            st.gstack = sl->gstack.p;
+            st.gstack_threads = kTraceGridThreads;
+            st.counters = fcd->trav[kMaxLevels];
+            st.count = p->profile >= 2;
+            st.allow_group = false;
+            id = ctx->timer.begin_kernel(CAT_TRACE, CAT_SHADOW);
+            const bool sl_launched = launch_trace(view, st, s);
+            ctx->timer.end_kernel(s, id, sl_launched);
+            ++trace_launches;
+            debug_sync(s, "path shadow trace", L, bi);
+            id = ctx->timer.begin(s, CAT_COMBINE);
+            launch_path_resolve(view, L, sq, ps, fcd, sq.cap, st.expect, s);
+            ctx->timer.end(s, id);
+            debug_sync(s, "path resolve", L, bi);
+        }
+    }
+    id = ctx->timer.begin(s, CAT_COMBINE);
+    launch_finish(view, fp, sl->tiles.p, LevelNodes{acc, nullptr, nullptr}, acc, sq, sl->accum.p, fo, npix, first, last,
+                  true, nullptr, s);
+    ctx->timer.end(s, id);
+    debug_sync(s, "path finish", 0, bi);
+}
+
 // Enqueue the frame described by fs (params, tiles, output) on fs's slot streams after
 // fs->ev_ready.  Tiles are <= kTile x kTile; out_mode 0 writes a framebuffer (origin ox,oy, pitch
 // in pixels), 1 tile-compact buffers.  No host synchronisation.
@@ -758,6 +839,11 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             // shade (L0Final), the finish completes the others
             const bool l0final = fuse && spp == 1;
             const FrameOut fo{fs->out, fs->out_mode, fs->ox, fs->oy, fs->pitch, K, j};
+            if (p->mode == PGRT_MODE_PATH) {
+                enqueue_path_batch(ctx, sl, view, fp, p, q, fcd, n0, fo, (int)npix, s0 == 0, s0 + fp.nsb >= spp, bi,
+                                   trace_launches);
+                continue;
+            }
             const L0Final l0f{l0final ? sl->l0_hit.p : nullptr, l0final ? sl->l0_pending.p : nullptr, fo,
                               sl->tiles.p};
             const PrimaryGen gen{ctx->cam, fp, sl->tiles.p, dir_only ? nullptr : q[0].ro, q[0].rd,
@@ -1061,6 +1147,8 @@ void check_frame(const pgrt_ctx* ctx, const pgrt_render_params* p) {
     PGRT_REQUIRE(p->spp_side >= 1 && p->spp_side <= 64, PGRT_ERR_INVALID_ARGUMENT, "spp_side must be in [1, 64]");
     PGRT_REQUIRE(p->max_level >= 0 && p->max_level <= kMaxLevels - 2, PGRT_ERR_INVALID_ARGUMENT,
                  "max_level must be in [0, 14]");
+    PGRT_REQUIRE(p->mode == PGRT_MODE_WHITTED || p->mode == PGRT_MODE_PATH, PGRT_ERR_INVALID_ARGUMENT,
+                 "mode must be PGRT_MODE_WHITTED or PGRT_MODE_PATH");
 }
 
 // Start a frame on set fs (its previous frame must be finished).  distributed: out is ignored,

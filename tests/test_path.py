@@ -1,0 +1,142 @@
+"""PGRT_MODE_PATH: the path tracer of the reference's README to-do list (README.md:17-21).
+
+The reference has no path tracer, so parity is against this project's CPU restatement
+(oracle/oracle.c path_sample, DESIGN.md §2 "Path tracing"): bit-exact, like the Whitted frames.
+The restatement itself is pinned only through the pieces it shares with the Whitted oracle
+(hit setup, dielectric rays, Phong term, environment lookup); its own sampling rules are
+checked here by properties: d = 0 equals the Whitted frame, determinism under a seed, and the
+dielectric choice on the all-glass geosphere (one of two outcomes per path, both sampled).
+"""
+import numpy as np
+import pytest
+
+import pyoracle
+from conftest import assert_frames_match
+from pgi_raytracing_amd import abi
+from pgi_raytracing_amd.scene import LightData, Scene
+
+PATH = abi.PGRT_MODE_PATH
+
+
+def _oracle(scene, cache={}):  # noqa: B006 (per-session cache keyed by scene id)
+    k = id(scene)
+    if k not in cache:
+        cache[k] = (scene, pyoracle.OracleScene(scene, accel=1))
+    return cache[k][1]
+
+
+# ---------------------------------------------------------------- CPU (oracle) properties
+
+def test_path_depth0_equals_whitted(avenger_scene):
+    """At d = 0 a hit is black and a miss is the environment texel in both modes."""
+    cam = abi.default_camera(64, 48)
+    w, _ = _oracle(avenger_scene).render(cam, abi.make_params(max_level=0))
+    p, st = _oracle(avenger_scene).render(cam, abi.make_params(max_level=0, mode=PATH))
+    assert (np.nan_to_num(w, nan=9).view(np.uint32) == np.nan_to_num(p, nan=9).view(np.uint32)).all()
+    assert st.rays_primary == 64 * 48 and st.rays_shadow == 0
+
+
+def test_path_deterministic_and_seeded(avenger_scene):
+    cam = abi.default_camera(48, 36)
+    a, sa = _oracle(avenger_scene).render(cam, abi.make_params(max_level=4, mode=PATH, seed=5))
+    b, _ = _oracle(avenger_scene).render(cam, abi.make_params(max_level=4, mode=PATH, seed=5))
+    c, _ = _oracle(avenger_scene).render(cam, abi.make_params(max_level=4, mode=PATH, seed=6))
+    assert (a.view(np.uint32) == b.view(np.uint32)).all()
+    assert (a != c).any()
+    # every hit below max_level continues (diffuse bounce or dielectric): more rays than pixels
+    assert sa.rays_reflect + sa.rays_refract > 0 and sa.rays_shadow > 0
+
+
+def test_path_glass_two_outcomes(geosphere_scene):
+    """All-glass icosphere, d = 1: a path reflects with probability R and refracts otherwise
+    (raytracer.cpp:314-316's R), so over many seeds a pixel takes at most two values -- the
+    reflected environment texel times the attenuation, or black (the refracted ray's next hit is
+    at level 1 >= d, raytracer.cpp:282-283) -- and near the silhouette, where R is large, both
+    occur."""
+    cam = abi.make_camera(9, 9, abi.deg2rad(90.0), (2.0, 0.0, 0.0), (0.0, 0.0, 0.0))
+    orc = _oracle(geosphere_scene)
+    imgs = np.array([orc.render(cam, abi.make_params(max_level=1, mode=PATH, seed=seed))[0][..., :3]
+                     for seed in range(64)])
+    nvals = np.array([[len(np.unique(imgs[:, y, x], axis=0)) for x in range(9)] for y in range(9)])
+    assert nvals.max() == 2 and (nvals == 2).sum() >= 4, nvals
+
+
+# ---------------------------------------------------------------- GPU parity
+
+PATH_CONFIGS = [
+    dict(spp_side=1, max_level=1),
+    dict(spp_side=1, max_level=5),
+    dict(spp_side=2, max_level=7, dof=1, jitter=abi.PGRT_JITTER_HASH, seed=77, frame=2),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", PATH_CONFIGS, ids=["d1", "d5", "S2d7dof"])
+def test_path_avenger_parity(gpu_ctx, avenger_scene, cfg):
+    gpu_ctx.set_scene(avenger_scene)
+    cam = abi.default_camera(128, 96)
+    gpu_ctx.set_camera(cam)
+    p = abi.make_params(mode=PATH, **cfg)
+    img, st = gpu_ctx.render(p)
+    ref, sto = _oracle(avenger_scene).render(cam, p)
+    diff, exact = assert_frames_match(img, ref)
+    assert exact == 1.0, f"max diff {diff}, exact fraction {exact}"
+    assert (st.rays_primary, st.rays_shadow, st.rays_reflect, st.rays_refract) == \
+        (sto.rays_primary, sto.rays_shadow, sto.rays_reflect, sto.rays_refract)
+
+
+@pytest.mark.gpu
+def test_path_geosphere_parity(gpu_ctx, geosphere_scene):
+    gpu_ctx.set_scene(geosphere_scene)
+    cam = abi.make_camera(96, 72, abi.deg2rad(90.0), (2.0, 0.0, 0.0), (0.0, 0.0, 0.0))
+    gpu_ctx.set_camera(cam)
+    p = abi.make_params(mode=PATH, spp_side=3, max_level=8, jitter=abi.PGRT_JITTER_HASH)
+    img, st = gpu_ctx.render(p)
+    ref, sto = _oracle(geosphere_scene).render(cam, p)
+    _, exact = assert_frames_match(img, ref)
+    assert exact == 1.0
+    assert st.rays_refract == sto.rays_refract > 0 and st.rays_reflect == sto.rays_reflect > 0
+
+
+@pytest.mark.gpu
+def test_path_multiple_lights_parity(gpu_ctx, avenger_scene):
+    lights = [LightData((-500.0, -100.0, 500.0)), LightData((300.0, -400.0, 200.0), (0.8, 0.2, 0.2), (0.8, 0.2, 0.2)),
+              LightData((0.0, 0.0, -300.0), (0.2, 0.2, 0.8), (0.2, 0.8, 0.2))]
+    sc = Scene(avenger_scene.positions, avenger_scene.normals, avenger_scene.uvs, avenger_scene.material_ids,
+               avenger_scene.materials, avenger_scene.textures, avenger_scene.env_texture, lights)
+    gpu_ctx.set_scene(sc)
+    cam = abi.default_camera(80, 60)
+    gpu_ctx.set_camera(cam)
+    p = abi.make_params(mode=PATH, max_level=4, spp_side=2, jitter=abi.PGRT_JITTER_HASH)
+    img, st = gpu_ctx.render(p)
+    ref, sto = pyoracle.OracleScene(sc).render(cam, p)
+    _, exact = assert_frames_match(img, ref)
+    assert exact == 1.0 and st.rays_shadow == sto.rays_shadow > 0
+
+
+@pytest.mark.gpu
+def test_path_batched_frames_equal_single_frames(gpu_ctx, avenger_scene):
+    """One call of 3 frames (frame indices f, f+1, f+2 key the path random numbers) equals three
+    single-frame renders, and the sample-batch split (max_batch_rays) changes nothing."""
+    gpu_ctx.set_scene(avenger_scene)
+    W, H = 96, 64
+    gpu_ctx.set_camera(abi.default_camera(W, H))
+    p = abi.make_params(mode=PATH, max_level=5, spp_side=2, jitter=abi.PGRT_JITTER_HASH, frame=10)
+    buf = gpu_ctx.alloc(3 * W * H * 16)
+    try:
+        gpu_ctx.render_frames_device(p, 3, buf)
+        many = gpu_ctx.to_host(buf, (3, H, W, 4))
+    finally:
+        gpu_ctx.free(buf)
+    for f in range(3):
+        one, _ = gpu_ctx.render(abi.make_params(mode=PATH, max_level=5, spp_side=2, jitter=abi.PGRT_JITTER_HASH,
+                                                frame=10 + f))
+        assert (np.nan_to_num(one, nan=9).view(np.uint32) == np.nan_to_num(many[f], nan=9).view(np.uint32)).all()
+    cfg = gpu_ctx.get_config()
+    try:
+        gpu_ctx.configure(max_batch_rays=4096)  # 2 samples per batch over 2 batches
+        split, _ = gpu_ctx.render(abi.make_params(mode=PATH, max_level=5, spp_side=2, jitter=abi.PGRT_JITTER_HASH,
+                                                  frame=10))
+    finally:
+        gpu_ctx.set_config(cfg)
+    assert (np.nan_to_num(split, nan=9).view(np.uint32) == np.nan_to_num(many[0], nan=9).view(np.uint32)).all()
