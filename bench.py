@@ -76,6 +76,9 @@ def parse():
     ap.add_argument("--max-level", type=int, default=None)
     ap.add_argument("--spp-side", type=int, default=None)
     ap.add_argument("--dof", type=int, default=None)
+    ap.add_argument("--mode", default="whitted", choices=["whitted", "path"],
+                    help="render mode: the reference's Whitted trace (the metric) or PGRT_MODE_PATH "
+                         "(the README to-do path tracer; a separate workload line)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--roofline-only", action="store_true",
@@ -212,7 +215,8 @@ def cpu_baseline(args, scene, cam, params):
 
 def workload(args) -> str:
     return (f"{args.config} {'avenger-proxy' if args.scene == 'avenger' else '1M random triangles'} "
-            f"{args.width}x{args.height} Whitted d={args.max_level} + env map, "
+            f"{args.width}x{args.height} {'path tracing' if args.mode == 'path' else 'Whitted'} d={args.max_level} "
+            f"+ env map, "
             f"{args.spp_side ** 2} spp {'DoF' if args.dof else 'pinhole'}")
 
 
@@ -252,7 +256,8 @@ def main():
         scene = scenes.random_scene(1_000_000, 42, env)
         cam = abi.make_camera(args.width, args.height, abi.deg2rad(42.185), (-140.0, -175.0, 80.0), (0.0, 0.0, 0.0))
     params = abi.make_params(spp_side=args.spp_side, max_level=args.max_level, dof=args.dof,
-                             jitter=abi.PGRT_JITTER_HASH if (args.spp_side > 1 or args.dof) else abi.PGRT_JITTER_NONE)
+                             jitter=abi.PGRT_JITTER_HASH if (args.spp_side > 1 or args.dof) else abi.PGRT_JITTER_NONE,
+                             mode=abi.PGRT_MODE_PATH if args.mode == "path" else abi.PGRT_MODE_WHITTED)
     ctx = Context(local_rank)
     if args.packet_levels is not None:
         ctx.configure(packet_levels=args.packet_levels)
@@ -389,12 +394,13 @@ def main():
             "tri_tests_per_ray": round(s2.tri_tests / max(1, frame_rays), 2),
             "bytes_per_ray": round(alg_bytes / max(1, frame_rays), 1),
         }
-        tf = os.path.join(ROOT, TRAFFIC.get(args.config, "-"))
+        tkey = args.config if args.mode == "whitted" else f"{args.config}-path"
+        tf = os.path.join(ROOT, TRAFFIC.get(tkey, "-"))
         if world == 1 and os.path.exists(tf):
             with open(tf) as fh:
                 t = json.load(fh)
             roof["traffic"] = t.get("bytes_per_launch")
-            roof["traffic_source"] = f"{TRAFFIC[args.config]} ({t.get('round')}; FETCH_SIZE x2 + WRITE_SIZE per launch)"
+            roof["traffic_source"] = f"{TRAFFIC[tkey]} ({t.get('round')}; FETCH_SIZE x2 + WRITE_SIZE per launch)"
             roof["traffic_frac"] = round(roof["traffic"] / (avg_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
             if t.get("valu_issue"):
                 roof["valu_issue"] = t["valu_issue"]
