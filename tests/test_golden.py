@@ -1,0 +1,112 @@
+"""Golden fixtures (tests/golden/, written by tests/golden/make_golden.py).
+
+reference_kats.json holds the reference's own known-answer demos as data (tutorial_1,
+tutorial_2, the camera basis); oracle_vectors.npz freezes the CPU restatement's outputs on
+seeded inputs.  The CPU tests check the restatement against both; the GPU test checks the HIP
+path's frames against the frozen frames bit for bit.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle
+from conftest import ASSETS, ROOT
+from pgi_raytracing_amd import abi
+from pgi_raytracing_amd.scene import TextureData, single_triangle_scene
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+@pytest.fixture(scope="module")
+def kats():
+    with open(os.path.join(GOLDEN, "reference_kats.json")) as fh:
+        return json.load(fh)
+
+
+@pytest.fixture(scope="module")
+def vec():
+    return np.load(os.path.join(GOLDEN, "oracle_vectors.npz"))  # allow_pickle=False (default)
+
+
+def bits_equal(a, b):
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    return a.shape == b.shape and ((a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))).all()
+
+
+def test_tutorial1_fixture(kats):
+    k = kats["tutorial_1"]
+    sc = single_triangle_scene()
+    assert np.allclose(sc.positions.reshape(3, 3), k["triangle"]) and np.allclose(sc.uvs.reshape(3, 2), k["uvs"])
+    o = pyoracle.OracleScene(sc, accel=0)
+    ray = np.array([*k["ray"]["org"], np.float32(1.17549435e-38), *k["ray"]["dir"], np.float32(3.402823466e38)],
+                   np.float32)
+    t, u, v, prim = o.intersect(ray)[0]
+    assert t == k["expect"]["t"] and f"{u:0.3f}" == k["expect"]["u_print"] and abs(v - k["expect"]["v"]) < 1e-6
+    assert prim.view(np.int32) == k["expect"]["primID"]
+
+
+def test_tutorial2_fixture(kats):
+    k = kats["tutorial_2"]
+    tex = TextureData.from_file(os.path.join(ASSETS, k["texture"]))
+    c = pyoracle.get_texel(tex, (np.float32(1.0) / np.float32(64)) * np.float32(2.5), 0.0)
+    assert "(r = %0.3f, g = %0.3f, b = %0.3f)" % tuple(c) == k["expect"]["printed"]
+
+
+def test_camera_basis_fixture(kats):
+    k = kats["camera_basis"]
+    for h, fy in k["f_y"].items():
+        h = int(h)
+        assert abs(pyoracle.camera_basis(abi.default_camera(h * 4 // 3, h))[0] - fy) < 2e-3
+    m = pyoracle.camera_basis(abi.default_camera(640, 480))[1:].reshape(3, 3)
+    for j, key in enumerate(("x_c", "y_c", "z_c")):
+        assert np.allclose(m[:, j], k[key], atol=k["atol"])
+
+
+def test_oracle_reproduces_texel_vectors(vec):
+    for name in ("test3", "test4"):
+        tex = TextureData.from_file(os.path.join(ASSETS, f"{name}.png"))
+        got = np.array([pyoracle.get_texel(tex, float(u), float(v)) for u, v in vec[f"texel_{name}_uv"]], np.float32)
+        assert bits_equal(got, vec[f"texel_{name}_out"]), name
+
+
+def test_oracle_reproduces_env_vectors(vec):
+    env = TextureData.from_file(os.path.join(ASSETS, "spherical_map_windows.jpg"))
+    got = np.array([pyoracle.env_texel(env, *map(float, d)) for d in vec["env_dir"]], np.float32)
+    assert bits_equal(got, vec["env_out"])
+
+
+def test_oracle_reproduces_ray_and_colour_vectors(vec):
+    cam = abi.default_camera(1920, 1080)
+    xy = vec["ray_xy"]
+    assert bits_equal([pyoracle.generate_ray(cam, float(x), float(y)) for x, y in xy], vec["ray_pinhole"])
+    assert bits_equal([pyoracle.generate_ray(cam, float(x), float(y), 1, 200.0, 5.0, 1.25, -2.0) for x, y in xy],
+                      vec["ray_dof"])
+    c = vec["mix_in"]
+    assert bits_equal([pyoracle.mix_srgb(x[0:4], x[4:8], float(x[8])) for x in c], vec["mix_out"])
+    assert bits_equal([pyoracle.gamma(x[0:4], 0.5) for x in c], vec["gamma_out"])
+
+
+def _frames(scene):
+    osc = pyoracle.OracleScene(scene)
+    cam = abi.default_camera(48, 36)
+    w = osc.render(cam, abi.make_params(max_level=5))[0]
+    p = osc.render(cam, abi.make_params(max_level=5, spp_side=2, mode=abi.PGRT_MODE_PATH,
+                                        jitter=abi.PGRT_JITTER_HASH, seed=7))[0]
+    return cam, w, p
+
+
+def test_oracle_reproduces_frames(vec, avenger_scene):
+    _, w, p = _frames(avenger_scene)
+    assert bits_equal(w, vec["frame_whitted_d5"]) and bits_equal(p, vec["frame_path_d5_s2"])
+
+
+@pytest.mark.gpu
+def test_gpu_frames_equal_golden(gpu_ctx, vec, avenger_scene):
+    gpu_ctx.set_scene(avenger_scene)
+    gpu_ctx.set_camera(abi.default_camera(48, 36))
+    w, _ = gpu_ctx.render(abi.make_params(max_level=5))
+    p, _ = gpu_ctx.render(abi.make_params(max_level=5, spp_side=2, mode=abi.PGRT_MODE_PATH,
+                                          jitter=abi.PGRT_JITTER_HASH, seed=7))
+    assert bits_equal(w, vec["frame_whitted_d5"]) and bits_equal(p, vec["frame_path_d5_s2"])
