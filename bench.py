@@ -59,7 +59,8 @@ CONFIGS = {
 }
 # PMC-measured HBM traffic per closest-hit launch of the bench's profiled configuration
 # (tools/profile.sh + tools/traffic.py, committed under profiles/)
-TRAFFIC = {"C2": "profiles/r2/traffic_C2.json", "C5": "profiles/r2/traffic_C5.json"}
+TRAFFIC = {"C2": "profiles/r2/traffic_C2.json", "C5": "profiles/r2/traffic_C5.json",
+           "C2-path": "profiles/r2/traffic_C2-path.json"}
 
 
 def parse():
