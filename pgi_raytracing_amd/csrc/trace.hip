@@ -635,27 +635,22 @@ typedef const __attribute__((address_space(4))) float* cfloat_ptr;
 __device__ __forceinline__ float4 cload4(cfloat_ptr p) { return make_float4(p[0], p[1], p[2], p[3]); }
 constexpr int kPktStack = 64;  // wave-uniform stack entries (>= BVH depth + 2)
 
-template <bool COUNT, bool GEN>
-__global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const float4* __restrict__ ro,
-                                                           const float4* __restrict__ rd, float4* __restrict__ hits,
-                                                           const int* __restrict__ count_dev, int count_terms,
-                                                           int count_host, int cap,
-                                                           unsigned long long* __restrict__ counters, PrimaryGen gen,
-                                                           unsigned long long* __restrict__ util) {
-    __shared__ int wstack[kTraceBlock / 64][kPktStack];
+// SAMPLE: this block measures packet utilisation (a block-uniform choice; the loop without the
+// counters is a separate copy, so unsampled blocks pay nothing for them)
+template <bool COUNT, bool GEN, bool SAMPLE>
+__device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __restrict__ ro,
+                                          const float4* __restrict__ rd, float4* __restrict__ hits, int n,
+                                          unsigned long long* __restrict__ counters, const PrimaryGen& gen,
+                                          unsigned long long* __restrict__ util, int (*wstack)[kPktStack]) {
     const int wib = threadIdx.x >> 6;
     const int lane = __lane_id();
-    const int n = ray_count(count_dev, count_terms, count_host, cap);
-    if constexpr (GEN) {
-        if (gen.store_count && blockIdx.x == 0 && threadIdx.x == 0) *gen.store_count = n;
-    }
     const cfloat_ptr nodes = (cfloat_ptr)(const void*)s.nodes;  // 16 floats per node
     const cfloat_ptr tris = (cfloat_ptr)(const void*)s.tri;     // 12 floats per triangle
     unsigned long long nvis = 0, ntest = 0;
     // packet utilisation (sampled: every 8th block): internal-node steps at which this lane's ray
     // hit a child box, and steps it spent live -- their ratio is the fraction of the wave's node
     // stream the ray needed (pgrt_config.packet_levels AUTO decides per level from it)
-    const bool sample = util != nullptr && (blockIdx.x & 7) == 0;
+    constexpr bool sample = SAMPLE;
     unsigned useful = 0, live_steps = 0;
     for (int base = (blockIdx.x * kTraceBlock) + wib * 64; base < n; base += gridDim.x * kTraceBlock) {
         const int i = base + lane;
@@ -693,25 +688,32 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const fl
         int node = s.root;
         if (__ballot(live) == 0ull) node = kSentinel;
         unsigned rvis = 0, rtest = 0;
+        node = __builtin_amdgcn_readfirstlane(node);  // wave-uniform by construction
         for (;;) {
-            node = __builtin_amdgcn_readfirstlane(node);  // wave-uniform by construction
-            if (node == kSentinel) break;
-            if (node >= 0) {  // internal node (wave-uniform)
+            // internal nodes (0 <= node < kSentinel) in a loop of their own: the leaf code, which
+            // updates the closest hits, stays out of it (no register copies of them per step)
+            // best_t is constant over this loop: canonicalised once (IEEE min/max would re-quiet it
+            // every step)
+            const float bt = __builtin_canonicalizef(best_t);
+            while ((unsigned)node < (unsigned)kSentinel) {
                 const cfloat_ptr nd = nodes + 16 * node;
                 const float4 a = cload4(nd), b = cload4(nd + 4), c = cload4(nd + 8);
                 const int4 d = make_int4(__float_as_int(nd[12]), __float_as_int(nd[13]), __float_as_int(nd[14]),
                                          __float_as_int(nd[15]));
+                // the child indices with the boxes, in one scalar-load wait (not a second one after
+                // the box tests)
+                asm volatile("" ::"s"(d.x), "s"(d.y));
                 if (COUNT) ++rvis;
                 float t0, t1;
-                const bool h0 = box_hit(a.x, a.y, a.z, a.w, c.x, c.y, idx, idy, idz, oix, oiy, oiz, best_t, t0);
-                const bool h1 = box_hit(b.x, b.y, b.z, b.w, c.z, c.w, idx, idy, idz, oix, oiy, oiz, best_t, t1);
+                const bool h0 = box_hit(a.x, a.y, a.z, a.w, c.x, c.y, idx, idy, idz, oix, oiy, oiz, bt, t0);
+                const bool h1 = box_hit(b.x, b.y, b.z, b.w, c.z, c.w, idx, idy, idz, oix, oiy, oiz, bt, t1);
                 if (sample && live) {
                     ++live_steps;
                     useful += (h0 || h1) ? 1u : 0u;
                 }
                 const unsigned long long b0 = __ballot(h0), b1 = __ballot(h1);
                 if (b0 == 0ull && b1 == 0ull) {
-                    node = sp > 0 ? wstack[wib][--sp] : kSentinel;
+                    node = sp > 0 ? __builtin_amdgcn_readfirstlane(wstack[wib][--sp]) : kSentinel;
                 } else if (b0 != 0ull && b1 != 0ull) {
                     // nearer first, by majority of the lanes that hit both
                     const unsigned long long near0 = __ballot(h0 && h1 && t0 <= t1);
@@ -722,19 +724,20 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const fl
                 } else {
                     node = b0 != 0ull ? d.x : d.y;
                 }
-            } else {  // leaf: its triangles against every lane's ray
-                const int first = leaf_first(node), end = first + leaf_count(node);
-                for (int k = first; k < end; ++k) {
-                    const cfloat_ptr q = tris + 12 * k;
-                    const float4 q0 = cload4(q), q1 = cload4(q + 4), q2 = cload4(q + 8);
-                    if (COUNT) ++rtest;
-                    const float4 ng = cload4((cfloat_ptr)(const void*)s.tri_ng + 4 * k);  // precomputed Ng
-                    if (live)
-                        tri_test_ng(q0, q1, q2, ng, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v,
-                                    best_prim);
-                }
-                node = sp > 0 ? wstack[wib][--sp] : kSentinel;
             }
+            if (node == kSentinel) break;
+            // leaf: its triangles against every lane's ray
+            const int first = leaf_first(node), end = first + leaf_count(node);
+            for (int k = first; k < end; ++k) {
+                const cfloat_ptr q = tris + 12 * k;
+                const float4 q0 = cload4(q), q1 = cload4(q + 4), q2 = cload4(q + 8);
+                if (COUNT) ++rtest;
+                const float4 ng = cload4((cfloat_ptr)(const void*)s.tri_ng + 4 * k);  // precomputed Ng
+                if (live)
+                    tri_test_ng(q0, q1, q2, ng, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v,
+                                best_prim);
+            }
+            node = sp > 0 ? __builtin_amdgcn_readfirstlane(wstack[wib][--sp]) : kSentinel;
         }
         if constexpr (GEN) {
             if (gen.hitmask) {  // 1-spp level 0 (L0Final): hit records of the hits only + the wave's mask
@@ -769,6 +772,28 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const fl
     if (COUNT && lane == 0) {  // per-wave counts (one packet step = one node visit)
         atomicAdd(&counters[0], nvis);
         atomicAdd(&counters[1], ntest);
+    }
+}
+
+template <bool COUNT, bool GEN>
+__global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const float4* __restrict__ ro,
+                                                           const float4* __restrict__ rd, float4* __restrict__ hits,
+                                                           const int* __restrict__ count_dev, int count_terms,
+                                                           int count_host, int cap,
+                                                           unsigned long long* __restrict__ counters, PrimaryGen gen,
+                                                           unsigned long long* __restrict__ util) {
+    __shared__ int wstack[kTraceBlock / 64][kPktStack];
+    const int n = ray_count(count_dev, count_terms, count_host, cap);
+    if constexpr (GEN) {
+        if (gen.store_count && blockIdx.x == 0 && threadIdx.x == 0) *gen.store_count = n;
+        // level 0 is always traced as packets: its utilisation is never sampled
+        pkt_trace<COUNT, GEN, false>(s, ro, rd, hits, n, counters, gen, util, wstack);
+    } else {
+        // packet utilisation sampled in every 8th block (pgrt_config.packet_levels AUTO)
+        if (util != nullptr && (blockIdx.x & 7) == 0)
+            pkt_trace<COUNT, GEN, true>(s, ro, rd, hits, n, counters, gen, util, wstack);
+        else
+            pkt_trace<COUNT, GEN, false>(s, ro, rd, hits, n, counters, gen, util, wstack);
     }
 }
 
