@@ -8,6 +8,12 @@ SRC     := pgi_raytracing_amd/csrc
 # -ffp-contract=off: no implicit FMA, so every float op rounds exactly like the CPU restatement
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off \
             -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -I$(SRC) -Wall -Wno-unused-result
+# shading kernels: no machine-level loop-invariant code motion -- it hoists the FP64 polynomial
+# constants of the exact math (pgrt_detmath.h: exp / log / atan, no VOP3 literals on gfx9) out of
+# the shading loop into SGPRs, which then spill (k_shade L0: 205 SGPR + 11 VGPR spills -> 73 + 0)
+HIPFLAGS_render := -mllvm -disable-machine-licm
+HIPFLAGS_path := -mllvm -disable-machine-licm
+HIPFLAGS_trace := -mllvm -disable-machine-licm
 OBJS := $(BUILD)/trace.o $(BUILD)/render.o $(BUILD)/bvh.o $(BUILD)/ploc.o $(BUILD)/split.o $(BUILD)/bvh8.o $(BUILD)/path.o $(BUILD)/context.o $(BUILD)/objloader.o
 
 all: $(LIBDIR)/libpgrt.so $(LIBDIR)/libpgrt_image.so oracle $(BUILD)/pg1_pgrt
@@ -18,7 +24,7 @@ $(BUILD) $(LIBDIR):
 HDRS := include/pgrt.h include/pgrt_detmath.h $(SRC)/common.hpp $(SRC)/trace.hpp $(SRC)/shade_ops.hpp $(SRC)/camera_ops.hpp $(SRC)/shade_ray.hpp $(SRC)/tiles.hpp $(SRC)/path.hpp
 
 $(BUILD)/%.o: $(SRC)/%.hip $(HDRS) | $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(HIPFLAGS_$*) -c $< -o $@
 
 $(BUILD)/%.o: $(SRC)/%.cpp $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@

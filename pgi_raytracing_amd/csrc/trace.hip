@@ -172,8 +172,13 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
             // ---- descend internal nodes until every active lane has parked a leaf ----
             long long tn0 = 0;
             if (COUNT) tn0 = clock64();
+            // best_t only changes in the leaf phase: canonicalised once per descent, not per step
+            const float bt = __builtin_canonicalizef(best_t);
             while ((unsigned)node < (unsigned)kSentinel) {
                 if (COUNT) ++witer;
+                // the stack top (the pop target when neither child is hit) is read before the node
+                // fetch, so its LDS latency hides behind the global loads
+                const int top = SPILL ? 0 : lstack[sp * kTraceBlock + tid];
                 const BvhNode* nd = s.nodes + node;
                 long long tq0 = 0;
                 if (COUNT) tq0 = clock64();
@@ -186,17 +191,18 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
                     rcyc_load += (unsigned long long)(clock64() - tq0);
                 }
                 float t0, t1;
-                const bool h0 = box_hit(a.x, a.y, a.z, a.w, c.x, c.y, idx, idy, idz, oix, oiy, oiz, best_t, t0);
-                const bool h1 = box_hit(b.x, b.y, b.z, b.w, c.z, c.w, idx, idy, idz, oix, oiy, oiz, best_t, t1);
+                const bool h0 = box_hit(a.x, a.y, a.z, a.w, c.x, c.y, idx, idy, idz, oix, oiy, oiz, bt, t0);
+                const bool h1 = box_hit(b.x, b.y, b.z, b.w, c.z, c.w, idx, idy, idz, oix, oiy, oiz, bt, t1);
                 if constexpr (!SPILL) {
-                    // branch-light form: the stack top is read unconditionally (it is the pop
-                    // target when neither child is hit), the far child pushed under exec mask
-                    const int top = lstack[sp * kTraceBlock + tid];
+                    // branch-free form: the far child is written above the top whether or not it is
+                    // pushed (that slot is free), the stack pointer moves by selects
                     const bool any = h0 || h1;
                     const bool first0 = h0 && (!h1 || t0 <= t1);
-                    if (h0 && h1) PUSH(first0 ? d.y : d.x);
+                    const bool both = h0 && h1;
+                    lstack[(sp + 1) * kTraceBlock + tid] = first0 ? d.y : d.x;
+                    if (COUNT && both && sp + 1 > msp) msp = sp + 1;
                     node = any ? (first0 ? d.x : d.y) : top;
-                    sp -= any ? 0 : 1;
+                    sp += both ? 1 : (any ? 0 : -1);
                 } else {
                     if (!h0 && !h1) {
                         node = POP();
