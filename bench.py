@@ -80,6 +80,9 @@ def parse():
     ap.add_argument("--mode", default="whitted", choices=["whitted", "path"],
                     help="render mode: the reference's Whitted trace (the metric) or PGRT_MODE_PATH "
                          "(the README to-do path tracer; a separate workload line)")
+    ap.add_argument("--dist-path", action="store_true",
+                    help="validation only: the multi-GPU code path (RCCL communicator, distributed frames, "
+                         "tuned tile share, gather + unpack) also at world 1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--roofline-only", action="store_true",
@@ -277,14 +280,16 @@ def main():
     F = max(1, min(64, args.frames_per_call or (8 * world if args.config == "C2" else 1)))
     fb = ctx.alloc(F * args.width * args.height * 16) if rank == 0 or world == 1 else None
     comm_ranks = 1
-    if world > 1:
+    distributed = world > 1 or args.dist_path
+    if distributed:
         uid = [Context.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
+        if dist:
+            dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(world, rank, uid[0])
         comm_ranks, _ = ctx.comm_info()
 
     def frame(p):  # synchronous frame (latency, profiled frames)
-        if world > 1:
+        if distributed:
             return ctx.render_distributed_device(p, fb)
         return ctx.render_device(p, fb)
 
@@ -300,13 +305,13 @@ def main():
 
         def wait_one():
             st = ctx.render_wait(pending.popleft())
-            if record and world > 1:
+            if record and distributed:
                 gather_ms.append(st.ms_gather)
             return st.rays()
 
         for f0 in range(0, n, F):
             nf = min(F, n - f0)
-            pending.append(ctx.render_frames_distributed_device_async(params, nf, fb) if world > 1
+            pending.append(ctx.render_frames_distributed_device_async(params, nf, fb) if distributed
                            else ctx.render_frames_device_async(params, nf, fb))
             if len(pending) >= in_flight:
                 rays_n += wait_one()
@@ -321,7 +326,7 @@ def main():
         args.warmup = max(args.warmup, in_flight * F)
     run_frames(args.warmup)
     share = None
-    if world > 1 and not args.roofline_only:
+    if distributed and not args.roofline_only:
         # rank 0's tile share from measured calls (libpgrt collective): its rendering against the
         # xGMI gather it receives and the unpack it runs
         share = ctx.tune_distribution(params, F, fb, calls=4)
