@@ -205,6 +205,18 @@ def cpu_baseline(args, scene, cam, params):
             if dt_c >= budget_s:
                 return rays_c / dt_c / 1e6, frames, rays_c, dt_c
 
+    # the reference's own per-sample RNG work, reported separately: two wall-clock
+    # seeded std::mt19937 per sample (raytracer.cpp:407-410, PinHoleCamera.cpp:77-80), 2 draws each
+    import ctypes as C
+    ol = pyoracle.lib()
+    ol.orc_mt19937_reseed.restype = C.c_uint32
+    ol.orc_mt19937_reseed.argtypes = [C.c_int, C.c_uint32]
+    n_rs, t_rs = 0, time.perf_counter()
+    while time.perf_counter() - t_rs < 0.5:
+        ol.orc_mt19937_reseed(20000, n_rs)
+        n_rs += 20000
+    reseed_us = (time.perf_counter() - t_rs) / n_rs * 1e6
+    samples = args.width * args.height * args.spp_side ** 2
     what = "whole C2 frames" if row_step == 1 else f"{args.config} frames, every 16th row"
     v_mt, f_mt, r_mt, t_mt = timed(threads, args.cpu_seconds)
     v_st, f_st, r_st, t_st = timed(1, args.cpu_seconds / 2)
@@ -212,6 +224,11 @@ def cpu_baseline(args, scene, cam, params):
             "sample": f"{f_mt} x {what} ({r_mt} rays, {t_mt:.1f} s) on {threads} host threads (OpenMP over rows); "
                       f"oracle/ CPU restatement with its own SAH BVH (built in {build_s:.1f} s, not timed)",
             "host": share,
+            "reference_rng": {"reseed_us": round(reseed_us, 3), "reseeds_per_sample": 2,
+                              "ms_per_frame_1_thread": round(reseed_us * 2 * samples / 1e3, 1),
+                              "note": "std::mt19937 seeding + 2 draws, restated in C (oracle/ orc_mt19937_reseed), "
+                                      "the reference's per-sample RNG cost on one thread, beside the restatement's "
+                                      "deterministic counter hash"},
             "single_thread_value": round(v_st, 3),
             "single_thread_sample": f"{f_st} x {what} ({r_st} rays, {t_st:.1f} s), 1 thread (the reference's "
                                     f"single Producer thread)"}

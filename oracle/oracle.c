@@ -1123,3 +1123,34 @@ void orc_detmath_eval(const float* in, int n, float* out)
         o[7] = (float)pg_pow_d((double)a, (double)b);
     }
 }
+
+/* ------------------------------------------------------------------ reference RNG cost
+ * The reference re-seeds a std::mt19937 from the wall clock for every sample, twice
+ * (raytracer.cpp:407-410 before the pixel jitter, PinHoleCamera.cpp:77-80 before the lens
+ * offset), and draws two uniform_real_distribution<float> values from each (one 32-bit output per
+ * float draw, libstdc++ generate_canonical<float, 24>).  This restates that work -- MT19937
+ * seeding (624-word init) and two tempered outputs (the first triggers the 624-word twist) -- n
+ * times, for bench.py's CPU baseline to report the reseeding cost separately.
+ * Returns a checksum of the outputs so the work is not optimised away. */
+uint32_t orc_mt19937_reseed(int n, uint32_t seed)
+{
+    uint32_t mt[624];
+    uint32_t acc = 0;
+    for (int r = 0; r < n; ++r) {
+        mt[0] = seed + (uint32_t)r;
+        for (int i = 1; i < 624; ++i) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
+        for (int i = 0; i < 624; ++i) { /* twist */
+            uint32_t y = (mt[i] & 0x80000000u) | (mt[(i + 1) % 624] & 0x7fffffffu);
+            mt[i] = mt[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        for (int k = 0; k < 2; ++k) {
+            uint32_t y = mt[k];
+            y ^= y >> 11;
+            y ^= (y << 7) & 0x9d2c5680u;
+            y ^= (y << 15) & 0xefc60000u;
+            y ^= y >> 18;
+            acc ^= y;
+        }
+    }
+    return acc;
+}

@@ -43,6 +43,8 @@ float orc_expand(float u);
 void orc_jitter(uint32_t seed, uint32_t frame, uint32_t pixel, uint32_t sample, float out[4]);
 int orc_uses_libm(void);
 void orc_detmath_eval(const float* in_pairs, int n, float* out8);
+/* n reseedings of std::mt19937 + two draws each (the reference's per-sample RNG work) */
+uint32_t orc_mt19937_reseed(int n, uint32_t seed);
 
 #ifdef __cplusplus
 }

@@ -234,3 +234,15 @@ def test_env_map_lookup_orientation():
     assert (axis[:3] == 0).all()
     side = pyoracle.env_texel(tex, 1.0, 0.3, 0.1)
     assert side[3] == 1.0 and side[:3].sum() > 0
+
+
+def test_mt19937_reseed_restatement():
+    """The reference's per-sample RNG (std::mt19937, raytracer.cpp:407-410) restated for the CPU
+    baseline's cost figure: the first two outputs for the standard's default seed 5489 are
+    3499211612 and 581869302 (the function returns their xor for n = 1)."""
+    import ctypes as C
+
+    ol = pyoracle.lib()
+    ol.orc_mt19937_reseed.restype = C.c_uint32
+    ol.orc_mt19937_reseed.argtypes = [C.c_int, C.c_uint32]
+    assert ol.orc_mt19937_reseed(1, 5489) == 3499211612 ^ 581869302
