@@ -627,13 +627,18 @@ long long batch_rays(const pgrt_ctx* ctx) {
 bool packet_level(const pgrt_ctx* ctx, int L) {
     const int k = ctx->cfg.packet_levels;
     if (k == PGRT_PACKETS_OFF) return false;
-    if (k == PGRT_PACKETS_AUTO) return L == 0 || ((ctx->auto_packets >> L) & 1u) != 0 || L == ctx->probe_level;
+    // (profiled frames never probe: their traversal counts describe the timed frames' choice)
+    if (k == PGRT_PACKETS_AUTO)
+        return L == 0 || ((ctx->auto_packets >> L) & 1u) != 0 || (L == ctx->probe_level && !ctx->timer.on);
     return L < k;
 }
 
 // PGRT_PACKETS_AUTO: a level stays on wave packets while its rays use at least this fraction of
 // the wave's node stream (calibrated on C2 / C5), re-probed while off
 constexpr double kPacketMinUtil = 0.4;
+// hysteresis: a level on packets leaves them only below this utilisation (C2's level 2 measures
+// ~0.44 and would otherwise flip with the sampling noise, and with it the traversal mode)
+constexpr double kPacketOffUtil = 0.3;
 constexpr unsigned long long kPacketProbeFrames = 32;
 
 void update_packet_choice(pgrt_ctx* ctx, const std::vector<FrameCounters>& fcs, int levels) {
@@ -648,7 +653,7 @@ void update_packet_choice(pgrt_ctx* ctx, const std::vector<FrameCounters>& fcs, 
         if (l < 4096) continue;  // not traced as packets (or too few rays to judge)
         ctx->packet_util[L] = (double)u / (double)l;
         if (ctx->packet_util[L] >= kPacketMinUtil) ctx->auto_packets |= 1u << L;
-        else ctx->auto_packets &= ~(1u << L);
+        else if (ctx->packet_util[L] < kPacketOffUtil) ctx->auto_packets &= ~(1u << L);
     }
     // re-probe the shallowest level that is off (its rays may have become coherent)
     if (++ctx->frames_collected % kPacketProbeFrames == 0)
