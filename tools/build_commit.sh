@@ -13,7 +13,9 @@ FLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fhip-fp32-c
 OBJS=""
 for src in "$OUT"/csrc/*.hip "$OUT"/csrc/*.cpp; do
   o="$OUT/$(basename "${src%.*}").o"
-  /opt/rocm/bin/hipcc $FLAGS -c "$src" -o "$o" &
+  # per-file flags of the revision's Makefile (HIPFLAGS_<name> := ...)
+  extra=$(git show "$REV:Makefile" | sed -n "s/^HIPFLAGS_$(basename "${src%.*}") := //p")
+  /opt/rocm/bin/hipcc $FLAGS $extra -c "$src" -o "$o" &
   OBJS="$OBJS $o"
 done
 wait
