@@ -270,6 +270,10 @@ int pgrt_host_free(pgrt_ctx* ctx, void* ptr);
  * rays: n x 8 floats {org.xyz, tnear, dir.xyz, tfar}; hits: n x 4 {t, u, v, prim} where prim
  * is the global triangle index stored as int32 bits, -1 on a miss (t = tfar, u = v = 0). */
 int pgrt_intersect_closest(pgrt_ctx* ctx, const float* rays, int n, float* hits);
+/* The same query on structure-of-arrays streams (SURVEY.md §8b's soa_rays / soa_hits; Embree's
+ * rtcIntersectNp layout): rays_soa = 8 arrays of n floats (org x, y, z, tnear, dir x, y, z,
+ * tfar), hits_soa = 4 arrays of n floats (t, u, v, primID as int bits, -1 = miss). */
+int pgrt_intersect_closest_soa(pgrt_ctx* ctx, const float* rays_soa, int n, float* hits_soa);
 
 /* ---- batched occlusion query with rtcOccluded1 semantics (rtcore_scene.h:120; Embree marks an
  * occluded ray by setting tfar = -inf): occluded[i] = 1 when ANY triangle is hit with t in

@@ -1418,21 +1418,18 @@ int pgrt_synchronize(pgrt_ctx* ctx) {
     return guarded(ctx, [&] { PGRT_HIP(hipStreamSynchronize(ctx->stream)); });
 }
 
-int pgrt_intersect_closest(pgrt_ctx* ctx, const float* rays, int n, float* hits) {
-    if (!ctx || n < 0 || (n > 0 && (!rays || !hits))) return PGRT_ERR_INVALID_ARGUMENT;
-    return guarded(ctx, [&] {
-        PGRT_REQUIRE(ctx->has_scene, PGRT_ERR_NO_SCENE, "pgrt_set_scene has not been called");
-        if (n == 0) return;
+extern "C++" {
+namespace {
+// closest hits of n rays: ray(i, a, b) fills ray i's (org, tnear) / (dir, tfar); the hit records
+// (t, u, v, prim bits) land in out (n float4, host)
+template <class RayFn>
+void intersect_rays(pgrt_ctx* ctx, int n, RayFn ray, float4* out) {
         DevBuf<float4> ro, rd, h;
         ro.alloc(n);
         rd.alloc(n);
         h.alloc(n);
         std::vector<float4> a(n), b(n);
-        for (int i = 0; i < n; ++i) {
-            const float* r = rays + 8 * (size_t)i;
-            a[i] = make_float4(r[0], r[1], r[2], r[3]);
-            b[i] = make_float4(r[4], r[5], r[6], r[7]);
-        }
+        for (int i = 0; i < n; ++i) ray(i, a[i], b[i]);
         PGRT_HIP(hipMemcpyAsync(ro.p, a.data(), sizeof(float4) * n, hipMemcpyHostToDevice, ctx->stream));
         PGRT_HIP(hipMemcpyAsync(rd.p, b.data(), sizeof(float4) * n, hipMemcpyHostToDevice, ctx->stream));
         if (ctx->gstack.n == 0) ctx->gstack.alloc((size_t)kTraceGridThreads * kGlobalStack);
@@ -1448,8 +1445,49 @@ int pgrt_intersect_closest(pgrt_ctx* ctx, const float* rays, int n, float* hits)
         view.group_max = group_max(ctx);  // batches up to it: 8 / 4 lanes per ray
         launch_trace(view, tl, ctx->stream);
         PGRT_HIP(hipGetLastError());
-        PGRT_HIP(hipMemcpyAsync(hits, h.p, sizeof(float4) * n, hipMemcpyDeviceToHost, ctx->stream));
+        PGRT_HIP(hipMemcpyAsync(out, h.p, sizeof(float4) * n, hipMemcpyDeviceToHost, ctx->stream));
         PGRT_HIP(hipStreamSynchronize(ctx->stream));
+}
+}  // namespace
+}  // extern "C++"
+
+int pgrt_intersect_closest(pgrt_ctx* ctx, const float* rays, int n, float* hits) {
+    if (!ctx || n < 0 || (n > 0 && (!rays || !hits))) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        PGRT_REQUIRE(ctx->has_scene, PGRT_ERR_NO_SCENE, "pgrt_set_scene has not been called");
+        if (n == 0) return;
+        intersect_rays(
+            ctx, n,
+            [&](int i, float4& a, float4& b) {
+                const float* r = rays + 8 * (size_t)i;
+                a = make_float4(r[0], r[1], r[2], r[3]);
+                b = make_float4(r[4], r[5], r[6], r[7]);
+            },
+            reinterpret_cast<float4*>(hits));
+    });
+}
+
+int pgrt_intersect_closest_soa(pgrt_ctx* ctx, const float* rays_soa, int n, float* hits_soa) {
+    if (!ctx || n < 0 || (n > 0 && (!rays_soa || !hits_soa))) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        PGRT_REQUIRE(ctx->has_scene, PGRT_ERR_NO_SCENE, "pgrt_set_scene has not been called");
+        if (n == 0) return;
+        const size_t N = (size_t)n;
+        std::vector<float4> h(N);
+        intersect_rays(
+            ctx, n,
+            [&](int i, float4& a, float4& b) {
+                const float* r = rays_soa + i;
+                a = make_float4(r[0], r[N], r[2 * N], r[3 * N]);
+                b = make_float4(r[4 * N], r[5 * N], r[6 * N], r[7 * N]);
+            },
+            h.data());
+        for (size_t i = 0; i < N; ++i) {
+            hits_soa[i] = h[i].x;
+            hits_soa[N + i] = h[i].y;
+            hits_soa[2 * N + i] = h[i].z;
+            hits_soa[3 * N + i] = h[i].w;
+        }
     });
 }
 

@@ -55,6 +55,7 @@ def lib():
         "pgrt_copy_to_host": (ip, [vp, vp, vp, C.c_size_t]),
         "pgrt_synchronize": (ip, [vp]),
         "pgrt_intersect_closest": (ip, [vp, fp, ip, fp]),
+        "pgrt_intersect_closest_soa": (ip, [vp, fp, ip, fp]),
         "pgrt_occluded": (ip, [vp, fp, ip, C.POINTER(C.c_int)]),
         "pgrt_accumulate_reset": (ip, [vp]),
         "pgrt_render_accumulate": (ip, [vp, C.POINTER(abi.RenderParams), fp, C.POINTER(C.c_int),
@@ -225,6 +226,14 @@ class Context:
         rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
         hits = np.zeros((rays.shape[0], 4), np.float32)
         _check(self.h, self.L.pgrt_intersect_closest(self.h, abi.fptr(rays), rays.shape[0], abi.fptr(hits)))
+        return hits
+
+    def intersect_soa(self, rays_soa: np.ndarray) -> np.ndarray:
+        """The same query on SoA streams: rays_soa (8, n) -> hits (4, n) {t, u, v, prim bits}."""
+        rays_soa = np.ascontiguousarray(rays_soa, np.float32).reshape(8, -1)
+        hits = np.zeros((4, rays_soa.shape[1]), np.float32)
+        _check(self.h, self.L.pgrt_intersect_closest_soa(self.h, abi.fptr(rays_soa), rays_soa.shape[1],
+                                                         abi.fptr(hits)))
         return hits
 
     def accumulate_reset(self) -> None:

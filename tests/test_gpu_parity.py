@@ -113,6 +113,15 @@ def test_closest_hit_bit_exact_vs_oracle(gpu_ctx, avenger_scene):
     assert (hg[:, 3].view(np.int32) >= 0).sum() > 10000
 
 
+def test_soa_query_equals_aos(gpu_ctx, avenger_scene):
+    """pgrt_intersect_closest_soa (SURVEY 8b's SoA streams) returns the AoS query's hit records."""
+    gpu_ctx.set_scene(avenger_scene)
+    rays = _random_rays(avenger_scene, 8000, 9)
+    aos = gpu_ctx.intersect(rays)
+    soa = gpu_ctx.intersect_soa(np.ascontiguousarray(rays.T))
+    assert (soa.T.view(np.int32) == aos.view(np.int32)).all()
+
+
 CONFIGS = [
     dict(spp_side=1, max_level=1),
     dict(spp_side=1, max_level=5),
