@@ -781,8 +781,12 @@ __device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __re
     }
 }
 
-template <bool COUNT, bool GEN>
-__global__ __launch_bounds__(kTraceBlock) void k_trace_pkt(SceneView s, const float4* __restrict__ ro,
+// MINW: minimum waves per SIMD the register allocation must allow (launch bound).  The level-0
+// kernel (GEN) uses 67 VGPRs -> 7 waves; big scenes (BVH + triangles far beyond the L2, fetches
+// that wait on the MALL / HBM) take the 8-wave build (59 VGPRs, more SGPR spills): C5 19.6 ->
+// 19.1 ms/frame, while the avenger proxy's issue-bound level 0 runs better at 7 (r2j A/B)
+template <bool COUNT, bool GEN, int MINW>
+__global__ __launch_bounds__(kTraceBlock, MINW) void k_trace_pkt(SceneView s, const float4* __restrict__ ro,
                                                            const float4* __restrict__ rd, float4* __restrict__ hits,
                                                            const int* __restrict__ count_dev, int count_terms,
                                                            int count_host, int cap,
@@ -825,6 +829,8 @@ constexpr int kGroup8Max = 150000;
 // queues up to kTailMax rays spread over more waves: kTailRpw rays per wave (r1 A/B: 64, i.e.
 // full waves, was best)
 constexpr int kTailMax = 131072, kTailRpw = 64;
+// scenes above this many triangles take the 8-wave level-0 packet kernel (k_trace_pkt MINW)
+constexpr int kPacketBigScene = 262144;
 
 bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) {
     const int max_count = t.max_count;
@@ -848,13 +854,16 @@ bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) 
         int grid = ceil_div(ex, kTraceBlock);
         if (grid > 16384) grid = 16384;
         const PrimaryGen g = t.gen ? *t.gen : PrimaryGen{};
-#define PGRT_LAUNCH_P(C, G)                                                                                   \
-    PGRT_TLAUNCH((k_trace_pkt<C, G>), dim3(grid), dim3(kTraceBlock), 0, stream, s, t.ro, t.rd, t.hits,        \
+#define PGRT_LAUNCH_P(C, G, W)                                                                                \
+    PGRT_TLAUNCH((k_trace_pkt<C, G, W>), dim3(grid), dim3(kTraceBlock), 0, stream, s, t.ro, t.rd, t.hits,     \
                  t.count_dev, t.count_terms, t.count_host, max_count, t.counters, g, t.pkt_util)
+        const bool big = s.ntri > kPacketBigScene;
         if (t.count) {
-            if (t.gen) PGRT_LAUNCH_P(true, true); else PGRT_LAUNCH_P(true, false);
+            if (t.gen) PGRT_LAUNCH_P(true, true, 1); else PGRT_LAUNCH_P(true, false, 1);
+        } else if (t.gen) {
+            if (big) PGRT_LAUNCH_P(false, true, 8); else PGRT_LAUNCH_P(false, true, 1);
         } else {
-            if (t.gen) PGRT_LAUNCH_P(false, true); else PGRT_LAUNCH_P(false, false);
+            PGRT_LAUNCH_P(false, false, 1);
         }
 #undef PGRT_LAUNCH_P
         return true;
