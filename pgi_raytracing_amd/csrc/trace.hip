@@ -39,6 +39,20 @@ __device__ __forceinline__ bool box_hit(float lox, float hix, float loy, float h
     tent = t0;
     return t0 <= t1 * 1.000001f;  // conservative: rounding never culls a box a hit lies in
 }
+// the same test with each axis's near and far planes already chosen from the sign of the ray's
+// inverse direction: fma is monotonic, so the near plane's t IS the fminf above (and the far's
+// the fmaxf) -- identical t0 / t1 without the 6 min / max that order them
+__device__ __forceinline__ bool box_hit_nf(float nx, float fx, float ny, float fy, float nz, float fz, float idx,
+                                           float idy, float idz, float oix, float oiy, float oiz, float tmax,
+                                           float& tent) {
+    const float txn = fmaf(nx, idx, -oix), txf = fmaf(fx, idx, -oix);
+    const float tyn = fmaf(ny, idy, -oiy), tyf = fmaf(fy, idy, -oiy);
+    const float tzn = fmaf(nz, idz, -oiz), tzf = fmaf(fz, idz, -oiz);
+    const float t0 = fmaxf(fmaxf(txn, tyn), fmaxf(tzn, 0.0f));
+    const float t1 = fminf(fminf(txf, tyf), fminf(tzf, tmax));
+    tent = t0;
+    return t0 <= t1 * 1.000001f;
+}
 
 // Moeller-Trumbore as Embree's closest-hit path evaluates it (see oracle/oracle.c): e1 = v0 - v1,
 // e2 = v2 - v0 (precomputed), Ng = e2 x e1, scaled edge tests, IEEE divisions.  Closest hit in
@@ -641,6 +655,55 @@ typedef const __attribute__((address_space(4))) float* cfloat_ptr;
 __device__ __forceinline__ float4 cload4(cfloat_ptr p) { return make_float4(p[0], p[1], p[2], p[3]); }
 constexpr int kPktStack = 64;  // wave-uniform stack entries (>= BVH depth + 2)
 
+// The packet's internal-node loop: from `node` down to the next leaf (returned) or kSentinel.
+// SGN 0-7: every live ray's direction has sign bits SGN (1 = x < 0, 2 = y, 4 = z), so each
+// axis's near / far plane is a fixed operand (box_hit_nf); SGN 8: mixed signs (box_hit).
+template <int SGN, bool COUNT, bool SAMPLE>
+__device__ __forceinline__ int pkt_nodes(const cfloat_ptr nodes, int node, int& sp, int* wstk, float bt, float idx,
+                                         float idy, float idz, float oix, float oiy, float oiz, bool live,
+                                         unsigned& rvis, unsigned& useful, unsigned& live_steps) {
+    while ((unsigned)node < (unsigned)kSentinel) {
+        const cfloat_ptr nd = nodes + 16 * node;
+        const float4 a = cload4(nd), b = cload4(nd + 4), c = cload4(nd + 8);
+        const int4 d = make_int4(__float_as_int(nd[12]), __float_as_int(nd[13]), __float_as_int(nd[14]),
+                                 __float_as_int(nd[15]));
+        // the child indices with the boxes, in one scalar-load wait (not a second one after the
+        // box tests)
+        asm volatile("" ::"s"(d.x), "s"(d.y));
+        if (COUNT) ++rvis;
+        float t0, t1;
+        bool h0, h1;
+        if constexpr (SGN < 8) {
+            constexpr bool nx = SGN & 1, ny = SGN & 2, nz = SGN & 4;
+            h0 = box_hit_nf(nx ? a.y : a.x, nx ? a.x : a.y, ny ? a.w : a.z, ny ? a.z : a.w, nz ? c.y : c.x,
+                            nz ? c.x : c.y, idx, idy, idz, oix, oiy, oiz, bt, t0);
+            h1 = box_hit_nf(nx ? b.y : b.x, nx ? b.x : b.y, ny ? b.w : b.z, ny ? b.z : b.w, nz ? c.w : c.z,
+                            nz ? c.z : c.w, idx, idy, idz, oix, oiy, oiz, bt, t1);
+        } else {
+            h0 = box_hit(a.x, a.y, a.z, a.w, c.x, c.y, idx, idy, idz, oix, oiy, oiz, bt, t0);
+            h1 = box_hit(b.x, b.y, b.z, b.w, c.z, c.w, idx, idy, idz, oix, oiy, oiz, bt, t1);
+        }
+        if (SAMPLE && live) {
+            ++live_steps;
+            useful += (h0 || h1) ? 1u : 0u;
+        }
+        const unsigned long long b0 = __ballot(h0), b1 = __ballot(h1);
+        if (b0 == 0ull && b1 == 0ull) {
+            node = sp > 0 ? __builtin_amdgcn_readfirstlane(wstk[--sp]) : kSentinel;
+        } else if (b0 != 0ull && b1 != 0ull) {
+            // nearer first, by majority of the lanes that hit both
+            const unsigned long long near0 = __ballot(h0 && h1 && t0 <= t1);
+            const unsigned long long both = b0 & b1;
+            const bool first0 = 2 * __popcll(near0) >= __popcll(both);
+            wstk[sp++] = first0 ? d.y : d.x;
+            node = first0 ? d.x : d.y;
+        } else {
+            node = b0 != 0ull ? d.x : d.y;
+        }
+    }
+    return node;
+}
+
 // SAMPLE: this block measures packet utilisation (a block-uniform choice; the loop without the
 // counters is a separate copy, so unsampled blocks pay nothing for them)
 template <bool COUNT, bool GEN, bool SAMPLE>
@@ -692,7 +755,17 @@ __device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __re
         int best_prim = -1;
         int sp = 0;
         int node = s.root;
-        if (__ballot(live) == 0ull) node = kSentinel;
+        const unsigned long long lmask = __ballot(live);
+        if (lmask == 0ull) node = kSentinel;
+        // direction signs shared by every live ray of the packet (coherent waves: nearly always)
+        // -> a copy of the node loop with each axis's near / far plane fixed at compile time;
+        // mixed signs (sgn 8) take the min / max form
+        const unsigned long long negx = __ballot(live && idx < 0.0f), negy = __ballot(live && idy < 0.0f),
+                                 negz = __ballot(live && idz < 0.0f);
+        const bool uni = (negx == 0ull || negx == lmask) && (negy == 0ull || negy == lmask) &&
+                         (negz == 0ull || negz == lmask);
+        const int sgn = __builtin_amdgcn_readfirstlane(
+            uni ? (negx != 0ull ? 1 : 0) | (negy != 0ull ? 2 : 0) | (negz != 0ull ? 4 : 0) : 8);
         unsigned rvis = 0, rtest = 0;
         node = __builtin_amdgcn_readfirstlane(node);  // wave-uniform by construction
         for (;;) {
@@ -701,36 +774,21 @@ __device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __re
             // best_t is constant over this loop: canonicalised once (IEEE min/max would re-quiet it
             // every step)
             const float bt = __builtin_canonicalizef(best_t);
-            while ((unsigned)node < (unsigned)kSentinel) {
-                const cfloat_ptr nd = nodes + 16 * node;
-                const float4 a = cload4(nd), b = cload4(nd + 4), c = cload4(nd + 8);
-                const int4 d = make_int4(__float_as_int(nd[12]), __float_as_int(nd[13]), __float_as_int(nd[14]),
-                                         __float_as_int(nd[15]));
-                // the child indices with the boxes, in one scalar-load wait (not a second one after
-                // the box tests)
-                asm volatile("" ::"s"(d.x), "s"(d.y));
-                if (COUNT) ++rvis;
-                float t0, t1;
-                const bool h0 = box_hit(a.x, a.y, a.z, a.w, c.x, c.y, idx, idy, idz, oix, oiy, oiz, bt, t0);
-                const bool h1 = box_hit(b.x, b.y, b.z, b.w, c.z, c.w, idx, idy, idz, oix, oiy, oiz, bt, t1);
-                if (sample && live) {
-                    ++live_steps;
-                    useful += (h0 || h1) ? 1u : 0u;
-                }
-                const unsigned long long b0 = __ballot(h0), b1 = __ballot(h1);
-                if (b0 == 0ull && b1 == 0ull) {
-                    node = sp > 0 ? __builtin_amdgcn_readfirstlane(wstack[wib][--sp]) : kSentinel;
-                } else if (b0 != 0ull && b1 != 0ull) {
-                    // nearer first, by majority of the lanes that hit both
-                    const unsigned long long near0 = __ballot(h0 && h1 && t0 <= t1);
-                    const unsigned long long both = b0 & b1;
-                    const bool first0 = 2 * __popcll(near0) >= __popcll(both);
-                    wstack[wib][sp++] = first0 ? d.y : d.x;
-                    node = first0 ? d.x : d.y;
-                } else {
-                    node = b0 != 0ull ? d.x : d.y;
-                }
+#define PGRT_PKT_NODES(S)                                                                                      \
+    node = pkt_nodes<S, COUNT, SAMPLE>(nodes, node, sp, wstack[wib], bt, idx, idy, idz, oix, oiy, oiz, live, rvis, \
+                                       useful, live_steps)
+            switch (sgn) {
+                case 0: PGRT_PKT_NODES(0); break;
+                case 1: PGRT_PKT_NODES(1); break;
+                case 2: PGRT_PKT_NODES(2); break;
+                case 3: PGRT_PKT_NODES(3); break;
+                case 4: PGRT_PKT_NODES(4); break;
+                case 5: PGRT_PKT_NODES(5); break;
+                case 6: PGRT_PKT_NODES(6); break;
+                case 7: PGRT_PKT_NODES(7); break;
+                default: PGRT_PKT_NODES(8); break;
             }
+#undef PGRT_PKT_NODES
             if (node == kSentinel) break;
             // leaf: its triangles against every lane's ray
             const int first = leaf_first(node), end = first + leaf_count(node);
