@@ -13,9 +13,10 @@
 
 namespace pgrt {
 
-// child order in the next level's queue: 1 = per wave, its reflections then its refractions
+// child order in the next level's queue: 2 = per block (256 parents), its reflections then its
+// refractions; 1 = the same per wave; 0 = interleaved
 #ifndef PGRT_CHILD_SPLIT
-#define PGRT_CHILD_SPLIT 1
+#define PGRT_CHILD_SPLIT 2
 #endif
 
 // shading tables in LDS when they fit (the hit -> attributes -> material -> texture chain has one
@@ -165,6 +166,7 @@ __device__ __forceinline__ void shade_eval(const SceneView& s, const DevMaterial
 template <int BLOCK>
 struct ShadeAllocLds {
     unsigned long long wtot[2][BLOCK / 64];
+    int wrefl[2][BLOCK / 64];  // reflection children per wave (PGRT_CHILD_SPLIT 2)
     unsigned long long bbase;
 };
 
@@ -183,8 +185,12 @@ __device__ __forceinline__ ShadeSlots shade_alloc(ShadeAllocLds<BLOCK>& lds, int
     const int rtot = (int)__popcll(__ballot(r.nchild == 2));
     const unsigned long long wtot = ((unsigned long long)(unsigned)stot << 32) | (unsigned)ctot;
     const int w = threadIdx.x >> 6;
+    const unsigned long long mrefl = __ballot(r.nchild >= 1), mrefr = __ballot(r.nchild == 2);
     if (__lane_id() == 0) {
         lds.wtot[it_par][w] = wtot;
+#if PGRT_CHILD_SPLIT == 2
+        lds.wrefl[it_par][w] = (int)__popcll(mrefl);
+#endif
         if (rtot && level + 1 < kMaxLevels) atomicAdd(&fc->refract[level + 1], rtot);  // statistics
     }
     __syncthreads();
@@ -196,14 +202,30 @@ __device__ __forceinline__ ShadeSlots shade_alloc(ShadeAllocLds<BLOCK>& lds, int
     __syncthreads();
     unsigned long long old = lds.bbase;
     for (int k = 0; k < w; ++k) old += lds.wtot[it_par][k];
+#if PGRT_CHILD_SPLIT == 2
+    int refl_below = 0, refl_block = 0;  // reflections of the block's waves below this one / all
+    for (int k = 0; k < BLOCK / 64; ++k) {
+        const int c = lds.wrefl[it_par][k];
+        refl_block += c;
+        if (k < w) refl_below += c;
+    }
+#endif
     it_par ^= 1;
     const int cb = __builtin_amdgcn_readfirstlane((int)(unsigned)(old & 0xffffffffull));
     const int sb = __builtin_amdgcn_readfirstlane((int)(unsigned)(old >> 32));
     ShadeSlots o;
-#if PGRT_CHILD_SPLIT
+#if PGRT_CHILD_SPLIT == 2
+    // the BLOCK's reflection rays first, then its refraction rays, each group in pixel order: a
+    // reflection leaves the surface and a refraction enters it, so a next-level wave that mixes
+    // the two spans > 90 degrees and its packet traversal visits the union of both paths
+    const int bb = __builtin_amdgcn_readfirstlane((int)(unsigned)(lds.bbase & 0xffffffffull));
+    const int rb = __builtin_amdgcn_readfirstlane(refl_below), rk = __builtin_amdgcn_readfirstlane(refl_block);
+    o.refl = bb + rb + lanes_below(mrefl);
+    o.refr = bb + rk + (cb - bb - rb) + lanes_below(mrefr);
+    (void)cpre;
+#elif PGRT_CHILD_SPLIT
     // the wave's reflection rays first, then its refraction rays, each group in pixel order:
     // the next level's waves are coherent bundles instead of alternating reflect / refract
-    const unsigned long long mrefl = __ballot(r.nchild >= 1), mrefr = __ballot(r.nchild == 2);
     o.refl = cb + lanes_below(mrefl);
     o.refr = cb + (int)__popcll(mrefl) + lanes_below(mrefr);
     (void)cpre;
