@@ -298,6 +298,29 @@ def test_packet_levels_bit_exact(gpu_ctx, avenger_scene, packets):
         gpu_ctx.set_config(old)
 
 
+@pytest.mark.parametrize("octant", range(8))
+def test_packet_sign_octants_bit_exact(gpu_ctx, avenger_scene, octant):
+    """The packet kernel runs one of 8 node loops per direction-sign combination (near / far
+    planes fixed at compile time) and a min / max loop for mixed-sign waves: a camera in each
+    octant around the model sends the primary waves through every combination (the waves on the
+    image's sign boundaries through the mixed loop), packets on every level, oracle bit for bit."""
+    gpu_ctx.set_scene(avenger_scene)
+    old = gpu_ctx.configure(packet_levels=16)
+    try:
+        W, H = 64, 48
+        sx, sy, sz = (1 if octant & 1 else -1), (1 if octant & 2 else -1), (1 if octant & 4 else -1)
+        cam = abi.make_camera(W, H, abi.deg2rad(42.185), (160.0 * sx, 190.0 * sy, 40.0 + 110.0 * sz),
+                              (0.0, 0.0, 40.0))
+        gpu_ctx.set_camera(cam)
+        p = abi.make_params(spp_side=1, max_level=3)
+        img, _ = gpu_ctx.render(p)
+        ref, _ = _oracle(avenger_scene).render(cam, p)
+        _, exact = assert_frames_match(img, ref)
+        assert exact == 1.0
+    finally:
+        gpu_ctx.set_config(old)
+
+
 def test_occluded_matches_closest_hit(gpu_ctx, avenger_scene):
     """rtcOccluded1 analogue: any hit in (tnear, tfar] exactly when the closest-hit query (oracle)
     finds one -- including finite-tfar shadow-style rays that stop short of the geometry."""
