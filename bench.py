@@ -46,6 +46,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # node visited, 80 B per 8-wide node visited (small queues), 48 B per triangle tested (our
 # triangle record: v0|id, e1, e2)
 RAY_BYTES, NODE_BYTES, WIDE_NODE_BYTES, TRI_BYTES = 48, 64, 80, 48
+# B_shade per shaded ray / hit / textured hit or env lookup / emitted ray
+SHADE_RAY_BYTES, SHADE_HIT_BYTES, SHADE_COLOUR_BYTES = 48, 16, 16
+SHADE_ATTR_BYTES, SHADE_TEXEL_BYTES, SHADE_EMIT_BYTES = 64, 12, 48
 
 # BASELINE.json configs (SURVEY.md §8d "Concrete inputs"); C2 is the headline bench line
 CONFIGS = {
@@ -83,6 +86,11 @@ def parse():
     ap.add_argument("--dist-path", action="store_true",
                     help="validation only: the multi-GPU code path (RCCL communicator, distributed frames, "
                          "tuned tile share, gather + unpack) also at world 1")
+    ap.add_argument("--frames", default="distinct", choices=["distinct", "identical"],
+                    help="distinct (default): every frame gets its own frame index and hash jitter (get_pixel's "
+                         "sub-pixel jitter, raytracer.cpp:407-413), so no two frames of the timed region are the same "
+                         "image, and every call in flight writes its own framebuffers; identical: the r2 workload "
+                         "(no jitter, one framebuffer shared by every call) -- A/B only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--roofline-only", action="store_true",
@@ -276,8 +284,10 @@ def main():
     else:  # C5: 10^6 random triangles, camera from (-140,-175,80) at the origin
         scene = scenes.random_scene(1_000_000, 42, env)
         cam = abi.make_camera(args.width, args.height, abi.deg2rad(42.185), (-140.0, -175.0, 80.0), (0.0, 0.0, 0.0))
+    distinct = args.frames == "distinct"
     params = abi.make_params(spp_side=args.spp_side, max_level=args.max_level, dof=args.dof,
-                             jitter=abi.PGRT_JITTER_HASH if (args.spp_side > 1 or args.dof) else abi.PGRT_JITTER_NONE,
+                             jitter=abi.PGRT_JITTER_HASH if (args.spp_side > 1 or args.dof or distinct)
+                             else abi.PGRT_JITTER_NONE,
                              mode=abi.PGRT_MODE_PATH if args.mode == "path" else abi.PGRT_MODE_WHITTED)
     ctx = Context(local_rank)
     if args.packet_levels is not None:
@@ -295,7 +305,15 @@ def main():
     # 0.39), emulated N=8 rank F=64 0.040 ms/frame (F=16 0.045)
     # (C3/C4/C5 frames are 15-250x heavier than C2's and fill the GPU on their own: 1 per call)
     F = max(1, min(64, args.frames_per_call or (8 * world if args.config == "C2" else 1)))
-    fb = ctx.alloc(F * args.width * args.height * 16) if rank == 0 or world == 1 else None
+    # calls in flight: a step is one whole frame (every rank's tiles rendered, gathered and
+    # unpacked on rank 0); up to `in_flight` calls overlap on the device, so one call's
+    # latency-bound deep levels share the CUs with the next call's wide levels
+    in_flight = args.in_flight or CONFIGS[args.config].get("in_flight", 6)
+    call_bytes = F * args.width * args.height * 16
+    # distinct frames: one framebuffer set per call in flight (a pending frame's framebuffer is
+    # never reused, pgrt.h); call k writes set k % in_flight, which call k - in_flight released
+    ring = in_flight if distinct else 1
+    fb = ctx.alloc(ring * call_bytes) if rank == 0 or world == 1 else None
     comm_ranks = 1
     distributed = world > 1 or args.dist_path
     if distributed:
@@ -310,12 +328,10 @@ def main():
             return ctx.render_distributed_device(p, fb)
         return ctx.render_device(p, fb)
 
-    # calls in flight: a step is one whole frame (every rank's tiles rendered, gathered and
-    # unpacked on rank 0); up to `in_flight` calls overlap on the device, so one call's
-    # latency-bound deep levels share the CUs with the next call's wide levels
-    in_flight = args.in_flight or CONFIGS[args.config].get("in_flight", 6)
     ctx.set_frames_in_flight(in_flight)
     gather_ms = []
+
+    next_frame = [0]  # frame index of the next submitted frame (jitter key of distinct frames)
 
     def run_frames(n, record=False):
         pending, rays_n = deque(), 0
@@ -326,10 +342,17 @@ def main():
                 gather_ms.append(st.ms_gather)
             return st.rays()
 
-        for f0 in range(0, n, F):
+        for k, f0 in enumerate(range(0, n, F)):
             nf = min(F, n - f0)
-            pending.append(ctx.render_frames_distributed_device_async(params, nf, fb) if distributed
-                           else ctx.render_frames_device_async(params, nf, fb))
+            pc = params
+            out = fb
+            if distinct:
+                pc = abi.RenderParams.from_buffer_copy(params)
+                pc.frame = next_frame[0]
+                out = fb + (k % ring) * call_bytes if fb else fb
+            next_frame[0] += nf
+            pending.append(ctx.render_frames_distributed_device_async(pc, nf, out) if distributed
+                           else ctx.render_frames_device_async(pc, nf, out))
             if len(pending) >= in_flight:
                 rays_n += wait_one()
         while pending:
@@ -417,6 +440,37 @@ def main():
             "tri_tests_per_ray": round(s2.tri_tests / max(1, frame_rays), 2),
             "bytes_per_ray": round(alg_bytes / max(1, frame_rays), 1),
         }
+        if args.mode == "whitted":
+            # whole-frame algorithmic bytes (B = 32 + 16 + 64 N_node + 36 N_tri + B_shade)
+            # over the timed region's ms per frame: the closest-hit bytes above (every level and the
+            # shadow queue) plus B_shade per shaded ray (every primary / reflection / refraction ray
+            # is shaded once, raytracer.cpp:241-393): ray + meta 48, hit 16, colour record 16; per
+            # hit the 64-B attribute record (n0 n1 n2 uv0 uv1 uv2 + material, rtcInterpolate0 and
+            # the geometry user data); 12 B of texel taps per textured hit and per environment
+            # lookup (every miss, SphericalMap::get_texel); 48 B per emitted child / shadow ray
+            shaded = s2.rays_primary + s2.rays_reflect + s2.rays_refract
+            misses = shaded - s2.shade_hits
+            emitted = s2.rays_reflect + s2.rays_refract + s2.rays_shadow
+            shade_bytes = ((SHADE_RAY_BYTES + SHADE_HIT_BYTES + SHADE_COLOUR_BYTES) * shaded
+                           + SHADE_ATTR_BYTES * s2.shade_hits + SHADE_TEXEL_BYTES * (s2.shade_textured_hits + misses)
+                           + SHADE_EMIT_BYTES * emitted)
+            frame_bytes = (alg_bytes + shade_bytes) / frames_per_prof
+            ms_frame = elapsed / max(1, args.steps) * 1e3 if args.steps else None
+            if ms_frame:
+                fa = frame_bytes / (ms_frame * 1e-3) / 1e9
+                roof["frame"] = {
+                    "achieved": round(fa, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(fa / HBM_PEAK_GBS, 4),
+                    "bytes_per_frame": int(frame_bytes),
+                    "trace_bytes_per_frame": int(alg_bytes / frames_per_prof),
+                    "shade_bytes_per_frame": int(shade_bytes / frames_per_prof),
+                    "ms_per_frame": round(ms_frame, 4),
+                    "shaded_rays_per_frame": int(shaded / frames_per_prof),
+                    "hits_per_frame": int(s2.shade_hits / frames_per_prof),
+                    "textured_hits_per_frame": int(s2.shade_textured_hits / frames_per_prof),
+                    "note": "SURVEY 8(d) B incl. B_shade (ray+meta 48, hit 16, colour 16 per shaded ray; attributes 64 "
+                            "per hit; texel taps 12 per textured hit and per env lookup; 48 per emitted child/shadow "
+                            "ray) over the timed region's ms per frame (every kernel of the frame, overlapped)",
+                }
         tkey = args.config if args.mode == "whitted" else f"{args.config}-path"
         tf = os.path.join(ROOT, TRAFFIC.get(tkey, "-"))
         if world == 1 and os.path.exists(tf):
@@ -512,6 +566,10 @@ def main():
             "frames_per_call": F,
             "frame_latency_ms": round(latency_ms, 4) if latency_ms else None,
             "higher_is_better": True,
+            "frames_distinct": distinct,
+            "frames_note": ("every frame its own frame index and hash jitter (get_pixel's sub-pixel jitter), every call "
+                            "in flight its own framebuffers" if distinct else
+                            "identical frames (no jitter) into one shared framebuffer: A/B only"),
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",

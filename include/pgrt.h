@@ -152,6 +152,9 @@ typedef struct pgrt_stats {
     int overflow_retries;            /* queue re-sizings this call */
     uint64_t wide_node_visits;       /* profile == 2: 8-wide (80-B) node visits; node_visits
                                         counts the binary (64-B) ones */
+    uint64_t shade_hits;             /* profile == 2 (Whitted): shaded rays that hit a triangle
+                                        (the others sample the environment map) */
+    uint64_t shade_textured_hits;    /* ... of which sampled a diffuse texture (map_Kd) */
 } pgrt_stats;
 
 typedef struct pgrt_bvh_info {
@@ -313,9 +316,11 @@ int pgrt_comm_init(pgrt_ctx* ctx, int world, int rank, const char id[128]); /* w
 int pgrt_comm_info(const pgrt_ctx* ctx, int* nranks, int* rank);
 /* Rank-local half of the distributed render, for callers that gather with their own
  * communicator: render the tiles of `rank` (of `world`) of the camera image into a tile-compact
- * device buffer of pgrt_tile_count(W, H, 64, rank, world) * 64 * 64 * 4 floats (local tile j is
- * tile pgrt_tile_index(W, H, 64, rank, world, j); edge tiles are padded).  The deal is the
- * context's (pgrt_config.rank0_share_*), which is pgrt_tile_share's unless those are set. */
+ * device buffer.  The deal is the CONTEXT's: with a = pgrt_config.rank0_share_a and
+ * b = pgrt_config.rank0_share_b (pgrt_get_config; pgrt_tune_distribution sets them), size the
+ * buffer as pgrt_tile_count_ex(W, H, 64, rank, world, a, b) * 64 * 64 * 4 floats; local tile j is
+ * tile pgrt_tile_index_ex(W, H, 64, rank, world, a, b, j) (edge tiles are padded).  Only when
+ * a = b = 0 (the default) are these pgrt_tile_count / pgrt_tile_index. */
 int pgrt_render_tiles_device(pgrt_ctx* ctx, const pgrt_render_params* p, int rank, int world,
                              void* tiles_device, pgrt_stats* st);
 /* Device form of pgrt_unpack_tiles_host_ex for callers that gather pgrt_render_tiles_device

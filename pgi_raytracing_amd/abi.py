@@ -150,6 +150,8 @@ class Stats(C.Structure):
         ("levels", C.c_int),
         ("overflow_retries", C.c_int),
         ("wide_node_visits", C.c_uint64),
+        ("shade_hits", C.c_uint64),
+        ("shade_textured_hits", C.c_uint64),
     ]
 
     def rays(self) -> int:

@@ -792,6 +792,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
     fp0.jitter = p->jitter;
     fp0.seed = p->seed;
     fp0.frame = p->frame;
+    fp0.count = p->profile >= 2 ? 1 : 0;
     for (int j = 0; j < K; ++j) {
         FrameSlot* sl = fs->slots[j].get();
         hipStream_t s = sl->stream;
@@ -957,6 +958,7 @@ void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
     const int spp = p->spp_side * p->spp_side;
     double ms[CAT_N] = {0};
     uint64_t rays_shadow = 0, rays_reflect = 0, rays_refract = 0, trav_nodes = 0, trav_tests = 0, trav_wide = 0;
+    uint64_t shade_hits = 0, shade_textured = 0;
     int retries = 0;
     for (;;) {
         const int K = fs->K;
@@ -1010,6 +1012,10 @@ void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
                     rays_reflect += (uint64_t)(fc_count(h, L) - h.refract[L]);
                 }
             }
+            for (int L = 0; L < kMaxLevels; ++L) {
+                shade_hits += h.shade[L][0];
+                shade_textured += h.shade[L][1];
+            }
             for (int k = 0; k < 2 * kMaxLevels; ++k) {
                 trav_wide += h.trav[k][14];
                 trav_nodes += h.trav[k][0];
@@ -1032,6 +1038,8 @@ void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
     st->node_visits = trav_nodes;
     st->wide_node_visits = trav_wide;
     st->tri_tests = trav_tests;
+    st->shade_hits = shade_hits;
+    st->shade_textured_hits = shade_textured;
     st->ms_raygen = ms[CAT_RAYGEN];
     st->ms_trace = ms[CAT_TRACE];
     st->ms_shade = ms[CAT_SHADE];
@@ -1049,6 +1057,8 @@ void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
 // this rank's tile count and every rank's list layout for a distributed frame of W x H
 UnpackSrc unpack_layout(const TileDeal& d, int W, int H) {
     const int total = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
+    PGRT_REQUIRE(d.world >= 1 && d.world <= kMaxRanks, PGRT_ERR_INVALID_ARGUMENT,
+                 "world size must be in [1, " + std::to_string(kMaxRanks) + "]");
     UnpackSrc u{};
     u.prefix[0] = 0;
     for (int r = 0; r < d.world; ++r) {
@@ -1164,6 +1174,8 @@ void start_frame(pgrt_ctx* ctx, FrameSet* fs, const pgrt_render_params* p, std::
     check_frame(ctx, p);
     PGRT_REQUIRE(nframes >= 1 && nframes <= kMaxFramesPerCall, PGRT_ERR_INVALID_ARGUMENT,
                  "frames per call must be in [1, 64]");
+    PGRT_REQUIRE(!fs->host_dst || (!distributed && out == fs->host_stage.p), PGRT_ERR_INVALID_ARGUMENT,
+                 "internal: a host destination is set for a frame that does not render into the staging buffer");
     fs->t0 = std::chrono::steady_clock::now();
     fs->params = *p;
     fs->nframes = nframes;
@@ -1275,7 +1287,7 @@ int pgrt_create(int hip_device, pgrt_ctx** out) {
     ctx->device = hip_device;
     if (const char* e = getenv("PGRT_EMULATE_RANK")) {
         int r = 0, w = 1;
-        if (sscanf(e, "%d/%d", &r, &w) == 2 && w >= 1 && r >= 0 && r < w) {
+        if (sscanf(e, "%d/%d", &r, &w) == 2 && w >= 1 && w <= kMaxRanks && r >= 0 && r < w) {
             ctx->world = w;
             ctx->rank = r;
             ctx->emulated = w > 1;
@@ -1319,6 +1331,9 @@ int pgrt_set_config(pgrt_ctx* ctx, const pgrt_config* cfg) {
         PGRT_REQUIRE(cfg->max_batch_rays >= 0 && cfg->max_batch_rays <= (1ll << 29), PGRT_ERR_INVALID_ARGUMENT,
                      "max_batch_rays must be in [0, 2^29]");
         PGRT_REQUIRE(cfg->max_batches_in_flight >= 0, PGRT_ERR_INVALID_ARGUMENT, "max_batches_in_flight must be >= 0");
+        PGRT_REQUIRE(cfg->rank0_share_a >= 0 && cfg->rank0_share_a <= 64 && cfg->rank0_share_b >= 0 &&
+                         cfg->rank0_share_b <= 64,
+                     PGRT_ERR_INVALID_ARGUMENT, "rank0_share_a / rank0_share_b must be in [0, 64]");
         drain_frames(ctx);  // pending frames were enqueued with the old choices
         ctx->cfg = *cfg;
     });
@@ -1669,6 +1684,9 @@ int pgrt_render_distributed_device(pgrt_ctx* ctx, const pgrt_render_params* p, v
         PGRT_REQUIRE(ctx->rank != 0 || rgba_device, PGRT_ERR_INVALID_ARGUMENT, "rank 0 needs an output buffer");
         drain_frames(ctx);
         FrameSet* fs = frame_set(ctx, 0);
+        // set 0 may last have served pgrt_render_frames_host_async: its host destination belongs
+        // to that call (the caller may have freed it), never to this frame
+        fs->host_dst = nullptr;
         PGRT_HIP(hipEventRecord(fs->ev_ready, ctx->stream));
         const TileDeal deal = ctx_deal(ctx, ctx->world);
         start_frame(ctx, fs, p, rank_tiles(ctx->cam.width, ctx->cam.height, ctx->rank, deal), nullptr, 1, 0, 0, 0,
@@ -1825,6 +1843,13 @@ int pgrt_tune_distribution(pgrt_ctx* ctx, const pgrt_render_params* p, int nfram
     // larger cost, above 1 the xGMI ingress of the gather into rank 0 is
     static const int kCand[] = {4, 5, 6, 7, 8, 10, 12, 14, 16, 20, 24, 32};
     const pgrt_config saved = ctx->cfg;
+    // every exit restores the caller's configuration unless a share was chosen
+    auto fail = [&](int rc) {
+        const std::string msg = ctx->err;
+        (void)pgrt_set_config(ctx, &saved);
+        ctx->err = msg;
+        return rc;
+    };
     double best = 1e300;
     int best_a = 0;
     for (int a : kCand) {
@@ -1832,10 +1857,9 @@ int pgrt_tune_distribution(pgrt_ctx* ctx, const pgrt_render_params* p, int nfram
         c.rank0_share_a = a;
         c.rank0_share_b = 8;
         int rc = pgrt_set_config(ctx, &c);
-        if (rc != PGRT_OK) return rc;
         std::vector<unsigned long long> tickets;
         unsigned long long t = 0;
-        rc = pgrt_render_frames_distributed_device_async(ctx, p, nframes, rgba_device, &t);  // warm: allocations
+        if (rc == PGRT_OK) rc = pgrt_render_frames_distributed_device_async(ctx, p, nframes, rgba_device, &t);  // warm
         if (rc == PGRT_OK) rc = pgrt_render_wait(ctx, t, nullptr);
         const auto t0 = std::chrono::steady_clock::now();
         for (int k = 0; k < calls && rc == PGRT_OK; ++k) {
@@ -1844,22 +1868,29 @@ int pgrt_tune_distribution(pgrt_ctx* ctx, const pgrt_render_params* p, int nfram
         }
         for (size_t k = 0; k < tickets.size() && rc == PGRT_OK; ++k)
             if (tickets.size() - k <= (size_t)ctx->frames_in_flight) rc = pgrt_render_wait(ctx, tickets[k], nullptr);
-        if (rc != PGRT_OK) return rc;
-        double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        // the slowest rank decides; every rank sees the same maxima, so all pick the same share
-        rc = guarded(ctx, [&] {
+        // the slowest rank decides; every rank sees the same maxima, so all pick the same share.
+        // A failed rank still joins the reduction with its error flag, so every rank stops here
+        // together instead of waiting in the next candidate's collectives
+        double v2[2] = {std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
+                        rc == PGRT_OK ? 0.0 : 1.0};
+        const int rrc = guarded(ctx, [&] {
             if (!ctx->comm) return;  // emulation: this rank's time alone
             DevBuf<double> v;
-            v.alloc(1);
-            PGRT_HIP(hipMemcpyAsync(v.p, &ms, sizeof(double), hipMemcpyHostToDevice, ctx->stream));
-            const ncclResult_t r = ncclAllReduce(v.p, v.p, 1, ncclFloat64, ncclMax, ctx->comm, ctx->stream);
+            v.alloc(2);
+            PGRT_HIP(hipMemcpyAsync(v.p, v2, sizeof(v2), hipMemcpyHostToDevice, ctx->stream));
+            const ncclResult_t r = ncclAllReduce(v.p, v.p, 2, ncclFloat64, ncclMax, ctx->comm, ctx->stream);
             if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
-            PGRT_HIP(hipMemcpyAsync(&ms, v.p, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+            PGRT_HIP(hipMemcpyAsync(v2, v.p, sizeof(v2), hipMemcpyDeviceToHost, ctx->stream));
             PGRT_HIP(hipStreamSynchronize(ctx->stream));
         });
-        if (rc != PGRT_OK) return rc;
-        if (ms < best) {
-            best = ms;
+        if (rc != PGRT_OK) return fail(rc);
+        if (rrc != PGRT_OK) return fail(rrc);
+        if (v2[1] != 0.0) {
+            ctx->err = "pgrt_tune_distribution: another rank failed";
+            return fail(PGRT_ERR_RCCL);
+        }
+        if (v2[0] < best) {
+            best = v2[0];
             best_a = a;
         }
     }
@@ -1867,7 +1898,7 @@ int pgrt_tune_distribution(pgrt_ctx* ctx, const pgrt_render_params* p, int nfram
     c.rank0_share_a = best_a;
     c.rank0_share_b = 8;
     const int rc = pgrt_set_config(ctx, &c);
-    if (rc != PGRT_OK) return rc;
+    if (rc != PGRT_OK) return fail(rc);
     if (a_out) *a_out = best_a;
     if (b_out) *b_out = 8;
     return PGRT_OK;

@@ -126,6 +126,14 @@ __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : 6) void k_shade
         }
         ShadeOut r;
         shade_eval(s, mats, lut255, level, fp.max_level, active, cur_o, cur_d, cur_t, cur_h, r);
+        if (fp.count) {  // profile == 2 only: one atomic pair per wave (the whole-frame roofline)
+            const bool hit = active && cur_d.w >= 0.0f && __float_as_int(cur_h.w) >= 0;
+            const unsigned long long hm = __ballot(hit), tm = __ballot(hit && r.kind == 2 && mats[r.mid].tex >= 0);
+            if (__lane_id() == 0 && hm) {
+                atomicAdd(&fc->shade[level][0], (unsigned long long)__popcll(hm));
+                atomicAdd(&fc->shade[level][1], (unsigned long long)__popcll(tm));
+            }
+        }
         const ShadeSlots sl = shade_alloc<kShadeBlock>(alds, it_par, fc, level, sq_base, sbits, r);
         if constexpr (l0final) {
             // a final colour (environment texel; padding; a hit at max_level) -> the pixel, now;

@@ -32,6 +32,9 @@ struct FrameCounters {
     // packet traversal utilisation per level (sampled blocks): {lane-steps whose ray hit a child
     // box, live lane-steps}; filled only by levels traced as packets
     alignas(128) unsigned long long pkt[kMaxLevels][2];
+    // profile == 2: per level, shaded rays that hit a triangle and, of those, the ones whose
+    // Phong branch sampled a texture (the whole-frame roofline's attribute / texel bytes)
+    alignas(128) unsigned long long shade[kMaxLevels][2];
 };
 
 __host__ __device__ inline int fc_count(const FrameCounters& f, int L) {
@@ -60,6 +63,7 @@ struct FrameParams {
     // writes a framebuffer at out + f * frame_stride floats (tile-compact outputs are frame-major).
     int slots, slot, frame_tiles, frame_out_tiles;  // frame_out_tiles: tiles per frame in a tile-compact output
     long long frame_stride;
+    int count;  // profile == 2: the shade kernels count hits / textured hits (FrameCounters::shade)
 };
 
 __host__ __device__ inline int frame_of_tile(const FrameParams& fp, int tile) {

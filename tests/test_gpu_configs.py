@@ -54,6 +54,43 @@ def test_c3_multi_batch_64spp_dof(gpu_ctx, avenger_scene):
         gpu_ctx.set_config(old)
 
 
+def test_c3_full_size_default_batching_rows(gpu_ctx, avenger_scene):
+    """C3 at its full size (1920x1080, DoF, 64 spp) through the default sample batching (16M
+    level-0 rays per batch: several batches per frame, each frame's accumulation over them) and
+    frames in flight: every 64th row equals the CPU restatement's bit for bit, and those rows
+    rendered as GPU rects give the oracle's ray counts per kind exactly (raytracer.cpp:396-437)."""
+    gpu_ctx.set_scene(avenger_scene)
+    W, H = 1920, 1080
+    cam = abi.default_camera(W, H)
+    gpu_ctx.set_camera(cam)
+    p = abi.make_params(spp_side=8, max_level=5, dof=1, jitter=abi.PGRT_JITTER_HASH, frame=3)
+    assert gpu_ctx.get_config().max_batch_rays == 0  # the default batching
+    osc = pyoracle.OracleScene(avenger_scene)
+    ref, sto = osc.render(cam, p, row_step=64, threads=16)
+    rows = np.arange(0, H, 64)
+    bufs = [gpu_ctx.alloc(W * H * 16) for _ in range(2)]
+    try:
+        gpu_ctx.set_frames_in_flight(2)
+        tickets = [gpu_ctx.render_device_async(p, b) for b in bufs]
+        stats = [gpu_ctx.render_wait(t) for t in tickets]
+        imgs = [gpu_ctx.to_host(b, (H, W, 4)) for b in bufs]
+    finally:
+        gpu_ctx.set_frames_in_flight(1)
+        for b in bufs:
+            gpu_ctx.free(b)
+    assert stats[0].rays() == stats[1].rays()
+    for img in imgs:
+        _, exact = assert_frames_match(img[rows], ref[rows])
+        assert exact == 1.0
+    got = np.zeros(4, np.int64)
+    for y in rows:
+        _, s = gpu_ctx.render(abi.make_params(spp_side=8, max_level=5, dof=1, jitter=abi.PGRT_JITTER_HASH, frame=3,
+                                              rect=(0, int(y), W, 1)))
+        got += (s.rays_primary, s.rays_shadow, s.rays_reflect, s.rays_refract)
+    assert tuple(got) == (sto.rays_primary, sto.rays_shadow, sto.rays_reflect, sto.rays_refract)
+    assert stats[0].rays_primary == W * H * 64
+
+
 def _tile_rect(W, H, t):
     tx = (W + 63) // 64
     x0, y0 = (t % tx) * 64, (t // tx) * 64

@@ -458,6 +458,65 @@ def test_full_size_c2_batched_bit_exact(gpu_ctx, avenger_scene):
     assert exact == 1.0
 
 
+def test_full_size_c2_distinct_frames_bit_exact(gpu_ctx, avenger_scene):
+    """The bench's default C2 workload (bench.py --frames distinct): a 2-frame call with hash
+    jitter at 1 spp (get_pixel's sub-pixel jitter, raytracer.cpp:407-413) and its own frame
+    indices, 3 calls in flight into separate framebuffers -- every frame equals the CPU
+    restatement's frame with the same frame index bit for bit, and the frames differ."""
+    gpu_ctx.set_scene(avenger_scene)
+    W, H = 1920, 1080
+    cam = abi.default_camera(W, H)
+    gpu_ctx.set_camera(cam)
+    F, calls = 2, 3
+    bufs = [gpu_ctx.alloc(F * W * H * 16) for _ in range(calls)]
+    try:
+        gpu_ctx.set_frames_in_flight(calls)
+        tickets = [gpu_ctx.render_frames_device_async(
+            abi.make_params(max_level=5, jitter=abi.PGRT_JITTER_HASH, frame=F * k), F, b) for k, b in enumerate(bufs)]
+        for t in tickets:
+            gpu_ctx.render_wait(t)
+        outs = [gpu_ctx.to_host(b, (F, H, W, 4)) for b in bufs]
+    finally:
+        gpu_ctx.set_frames_in_flight(1)
+        for b in bufs:
+            gpu_ctx.free(b)
+    for f in (0, 3, 5):  # first frame of call 0, second of call 1, last of call 2
+        ref, _ = _oracle(avenger_scene).render(cam, abi.make_params(max_level=5, jitter=abi.PGRT_JITTER_HASH, frame=f),
+                                               threads=16)
+        _, exact = assert_frames_match(outs[f // F][f % F], ref)
+        assert exact == 1.0, f"frame {f}"
+    assert not np.array_equal(outs[0][0], outs[0][1])
+
+
+def test_distributed_frame_after_host_output_leaves_host_buffer_alone(gpu_ctx, avenger_scene):
+    """Regression (r2 advisor): a synchronous distributed frame reuses frame set 0, which the
+    default one-frame-in-flight pgrt_render_frames_host_async also uses -- its host destination
+    must not be kept: the distributed frame would copy into a buffer the caller may have freed.
+    The old host buffer is refilled with a sentinel after its call and must keep it."""
+    gpu_ctx.set_scene(avenger_scene)
+    W, H = 128, 64
+    gpu_ctx.set_camera(abi.default_camera(W, H))
+    uid = gpu_ctx.comm_unique_id()
+    gpu_ctx.comm_init(1, 0, uid)
+    p = abi.make_params(max_level=3)
+    hb = gpu_ctx.host_array((1, H, W, 4))
+    fb = gpu_ctx.alloc(W * H * 16)
+    try:
+        gpu_ctx.set_frames_in_flight(1)
+        gpu_ctx.render_wait(gpu_ctx.render_frames_host_async(p, 1, hb))
+        ref, _ = gpu_ctx.render(p)
+        assert ((hb[0] == ref) | (np.isnan(hb[0]) & np.isnan(ref))).all()
+        hb.fill(-7.0)
+        gpu_ctx.render_distributed_device(p, fb)
+        out, _ = gpu_ctx.render_distributed(p)
+        gpu_ctx.synchronize()
+        assert (hb == -7.0).all(), "the distributed frame wrote the previous call's host buffer"
+        assert ((out == ref) | (np.isnan(out) & np.isnan(ref))).all()
+    finally:
+        gpu_ctx.host_free(hb)
+        gpu_ctx.free(fb)
+
+
 def test_new_frame_sets_start_clean(avenger_scene):
     """Regression (r1h): the first frame on each new frame set must see zeroed queue counters
     -- they were zeroed by a NULL-stream hipMemset, unordered with the slot streams, and a set's

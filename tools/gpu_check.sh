@@ -23,12 +23,18 @@ step() {  # name limit cmd...
 rocm-smi --showproductname > gpurun_out/rocm_smi.log 2>&1 || true
 for s in "$@"; do
     case $s in
-        tests) step gpu_tests 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+        tests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         tests_all) step gpu_tests_all 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
         bench_quick) step bench_quick 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
         diag) step diag 300 python tools/diag.py ;;
+        # the driver's line (--steps 20 --warmup 5), distinct frames (the default) and the r2
+        # identical-frame workload (A/B), and the long default run of each
+        bench_driver) step bench_driver 600 python bench.py --steps 20 --warmup 5 ;;
+        bench_ident) step bench_ident 300 python bench.py --steps 20 --warmup 5 --frames identical --no-cpu-baseline ;;
+        bench_long) step bench_long 300 python bench.py --no-cpu-baseline ;;
+        bench_long_ident) step bench_long_ident 300 python bench.py --no-cpu-baseline --frames identical ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done
