@@ -35,12 +35,14 @@ $(LIBDIR)/libpgrt.so: $(OBJS) | $(LIBDIR)
 # JPEG textures decoded like the reference's FreeImage JPEG_DEFAULT load (IJG libjpeg 9, IFAST
 # IDCT, no fancy upsampling; csrc/image_jpeg.c).  libjpeg 9 ships with this image under /opt/conda.
 JPEG_PREFIX ?= /opt/conda
-$(LIBDIR)/libpgrt_image.so: $(SRC)/image_jpeg.c include/pgrt_image.h | $(LIBDIR)
-	gcc -O2 -std=c11 -Wall -shared -fPIC -Iinclude -I$(JPEG_PREFIX)/include -o $@ $< -L$(JPEG_PREFIX)/lib -ljpeg -Wl,-rpath,$(JPEG_PREFIX)/lib
+# PNG through libpng 1.6 (also under /opt/conda), the format dispatch of Texture::Texture
+$(LIBDIR)/libpgrt_image.so: $(SRC)/image_jpeg.c $(SRC)/image_png.c include/pgrt_image.h | $(LIBDIR)
+	gcc -O2 -std=c11 -Wall -shared -fPIC -Iinclude -I$(JPEG_PREFIX)/include -o $@ $(SRC)/image_jpeg.c $(SRC)/image_png.c \
+	    -L$(JPEG_PREFIX)/lib -ljpeg -lpng16 -Wl,-rpath,$(JPEG_PREFIX)/lib
 
 # C++ host example over the C ABI (include/pgrt_raytracer.hpp)
-$(BUILD)/pg1_pgrt: examples/pg1_pgrt.cpp include/pgrt_raytracer.hpp include/pgrt.h $(LIBDIR)/libpgrt.so | $(BUILD)
-	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ $< -L$(LIBDIR) -lpgrt -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
+$(BUILD)/pg1_pgrt: examples/pg1_pgrt.cpp include/pgrt_raytracer.hpp include/pgrt.h include/pgrt_image.h $(LIBDIR)/libpgrt.so $(LIBDIR)/libpgrt_image.so | $(BUILD)
+	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ $< -L$(LIBDIR) -lpgrt -lpgrt_image -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
 
 oracle:
 	$(MAKE) -C oracle

@@ -21,6 +21,19 @@ int pgrt_jpeg_decode(const char* path, int dct, int* width, int* height, int* bp
                      unsigned char* out, size_t out_size);
 const char* pgrt_jpeg_error(void);
 
+/* PNG (lossless: FreeImage's bytes): RGB -> BGR (bpp 3), RGBA -> BGRA (bpp 4), palette / grey
+ * expanded to RGB(A), 16-bit samples reduced to 8; FreeImage pitch, top-down.  Same returns. */
+int pgrt_png_decode(const char* path, int* width, int* height, int* bpp, int* pitch,
+                    unsigned char* out, size_t out_size);
+const char* pgrt_png_error(void);
+
+/* Texture::Texture's load (texture.cpp:15-46): the format from the file signature, else the file
+ * name (FreeImage_GetFileType / FreeImage_GetFIFFromFilename), then the JPEG_DEFAULT or PNG
+ * decode above.  Same returns; pgrt_image_error describes a failure. */
+int pgrt_image_decode(const char* path, int* width, int* height, int* bpp, int* pitch,
+                      unsigned char* out, size_t out_size);
+const char* pgrt_image_error(void);
+
 #ifdef __cplusplus
 }
 #endif

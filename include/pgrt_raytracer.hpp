@@ -4,7 +4,7 @@
 // PinHoleCamera PinHoleCamera.h:14-41, LightSource LightSource.h, Material material.h:34-125,
 // Texture texture.h:14-33, SphericalMap SphericalMap.h) keep their names and argument meaning;
 // what changes is that a frame is rendered on the GPU in one call (Render) and get_pixel reads
-// it.  Header-only; link with -lpgrt.  Errors throw pgrt::Exception (this header is the C++
+// it.  Header-only; link with -lpgrt -lpgrt_image.  Errors throw pgrt::Exception (this header is the C++
 // side: exceptions never cross the C ABI itself).
 #pragma once
 
@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "pgrt.h"
+#include "pgrt_image.h"
 
 namespace pgrt {
 
@@ -43,9 +44,11 @@ struct Color4f {  // structs.h:11-14
 
 inline float deg2rad(const float x) { return x * float(3.14159265358979323846) / 180.0f; }  // mymath.h:27-30
 
-// Decoded texture in FreeImage's raw layout (texture.cpp:43-47): BGR(A), top-down, 4-byte
-// aligned pitch.  Files: the "PGRTTEX1" raw format written by tools/convert_textures.py, or
-// binary PPM (P6, RGB).
+// Texture(file_name) (texture.h:14-33, texture.cpp:5-54): the file decoded into FreeImage's raw
+// layout (texture.cpp:43-47) -- BGR(A), top-down, 4-byte aligned pitch -- by libpgrt_image
+// (pgrt_image.h): the format from the file signature, JPEG with FreeImage's JPEG_DEFAULT
+// settings (IJG libjpeg, IFAST IDCT, no fancy upsampling), PNG through libpng.  Link with
+// -lpgrt_image.
 class Texture {
 public:
     Texture() = default;
@@ -57,48 +60,18 @@ public:
 
 private:
     void load(const char* file_name) {
-        std::string f(file_name);
-        std::string raw = f + ".pgrttex";
-        FILE* fp = std::fopen(raw.c_str(), "rb");
-        if (fp) {
-            char magic[8];
-            int hdr[4];
-            if (std::fread(magic, 1, 8, fp) == 8 && std::memcmp(magic, "PGRTTEX1", 8) == 0 &&
-                std::fread(hdr, sizeof(int), 4, fp) == 4) {
-                width_ = hdr[0];
-                height_ = hdr[1];
-                pitch_ = hdr[2];
-                bpp_ = hdr[3];
-                data_.resize((size_t)pitch_ * height_);
-                if (std::fread(data_.data(), 1, data_.size(), fp) != data_.size()) data_.clear();
-            }
-            std::fclose(fp);
-            if (ok()) return;
+        int w = 0, h = 0, bpp = 0, pitch = 0;
+        if (pgrt_image_decode(file_name, &w, &h, &bpp, &pitch, nullptr, 0) != 0)
+            throw Exception(PGRT_ERR_IO, std::string("Texture: ") + pgrt_image_error());
+        data_.assign((size_t)pitch * h, 0);
+        if (pgrt_image_decode(file_name, &w, &h, &bpp, &pitch, data_.data(), data_.size()) != 0) {
+            data_.clear();
+            throw Exception(PGRT_ERR_IO, std::string("Texture: ") + pgrt_image_error());
         }
-        fp = std::fopen(file_name, "rb");
-        if (!fp) throw Exception(PGRT_ERR_IO, "cannot open texture " + f + " (run tools/convert_textures.py)");
-        int w = 0, h = 0, mx = 0;
-        if (std::fscanf(fp, "P6 %d %d %d", &w, &h, &mx) != 3 || mx != 255) {
-            std::fclose(fp);
-            throw Exception(PGRT_ERR_IO, f + ": not a PGRTTEX1/PPM texture (run tools/convert_textures.py)");
-        }
-        std::fgetc(fp);
         width_ = w;
         height_ = h;
-        bpp_ = 3;
-        pitch_ = ((w * 24 + 31) / 32) * 4;
-        data_.assign((size_t)pitch_ * h, 0);
-        std::vector<unsigned char> row((size_t)w * 3);
-        for (int y = 0; y < h; ++y) {
-            if (std::fread(row.data(), 1, row.size(), fp) != row.size()) break;
-            for (int x = 0; x < w; ++x) {
-                unsigned char* d = &data_[(size_t)y * pitch_ + (size_t)x * 3];
-                d[0] = row[3 * x + 2];
-                d[1] = row[3 * x + 1];
-                d[2] = row[3 * x];
-            }
-        }
-        std::fclose(fp);
+        pitch_ = pitch;
+        bpp_ = bpp;
     }
     int width_ = 0, height_ = 0, pitch_ = 0, bpp_ = 0;
     std::vector<unsigned char> data_;

@@ -126,7 +126,8 @@ class Config(C.Structure):
         ("max_batches_in_flight", C.c_int),
         ("rank0_share_a", C.c_int),
         ("rank0_share_b", C.c_int),
-        ("reserved", C.c_int * 3),
+        ("ray_binning", C.c_int),
+        ("reserved", C.c_int * 2),
     ]
 
 

@@ -93,7 +93,7 @@ struct StageTimer {
     }
 };
 
-enum { CAT_RAYGEN, CAT_TRACE, CAT_SHADE, CAT_SHADOW, CAT_COMBINE, CAT_LTRACE, CAT_LSHADE = CAT_LTRACE + kMaxLevels,
+enum { CAT_RAYGEN, CAT_TRACE, CAT_SHADE, CAT_SHADOW, CAT_COMBINE, CAT_BIN, CAT_LTRACE, CAT_LSHADE = CAT_LTRACE + kMaxLevels,
        CAT_N = CAT_LSHADE + kMaxLevels };
 
 }  // namespace
@@ -112,6 +112,8 @@ struct FrameSlot {
     DevBuf<int4> tiles;
     DevBuf<float4> q_ro[2], q_rd[2], q_hit[2];
     DevBuf<float> q_time[2];
+    DevBuf<unsigned char> q_key;  // binning key of the next level's rays (one level at a time)
+    DevBuf<int> q_perm;           // the binned level's traversal order
     DevBuf<unsigned long long> l0_hit, l0_pending;  // 1-spp level-0 wave masks (L0Final)
     int q_cap = 0;
     std::vector<std::unique_ptr<DevBuf<float4>>> n_color, n_att;
@@ -524,6 +526,8 @@ void ensure_frame_buffers(FrameSlot* sl, int n0, int levels, int nlight, int bat
         }
         sl->l0_hit.alloc((size_t)n0 / 64 + 1);
         sl->l0_pending.alloc((size_t)n0 / 64 + 1);
+        sl->q_key.alloc(n0);
+        sl->q_perm.alloc(n0);
         sl->q_cap = n0;
     }
     if ((int)sl->level_cap.size() < levels) sl->level_cap.resize(levels, 0);
@@ -577,6 +581,8 @@ void grow_after_overflow(FrameSlot* sl, int levels) {
                     sl->q_hit[b].alloc(need);
                     sl->q_time[b].alloc(need);
                 }
+                sl->q_key.alloc(need);
+                sl->q_perm.alloc(need);
                 sl->q_cap = need;
             }
         }
@@ -631,6 +637,11 @@ bool packet_level(const pgrt_ctx* ctx, int L) {
     if (k == PGRT_PACKETS_AUTO)
         return L == 0 || ((ctx->auto_packets >> L) & 1u) != 0 || (L == ctx->probe_level && !ctx->timer.on);
     return L < k;
+}
+
+// is level L >= 1 binned by direction octant before its packet traversal (pgrt_config.ray_binning)
+bool binned_level(const pgrt_ctx* ctx, const SceneView& view, int L) {
+    return L >= 1 && ctx->cfg.ray_binning == 0 && packet_level(ctx, L) && trace_packets_available(view);
 }
 
 // PGRT_PACKETS_AUTO: a level stays on wave packets while its rays use at least this fraction of
@@ -863,6 +874,11 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 const int maxc = L == 0 ? n0 : std::min(sl->q_cap, sl->level_cap[L]);
                 qc.cap = maxc;
                 qn.cap = std::min(sl->q_cap, L + 1 < levels ? sl->level_cap[L + 1] : sl->q_cap);
+                // the next level's rays get their binning key from this level's shade when the
+                // next level is traced as packets
+                const bool bin_next = L + 1 < levels && binned_level(ctx, view, L + 1);
+                qn.key = bin_next ? sl->q_key.p : nullptr;
+                const bool binned = L >= 1 && binned_level(ctx, view, L);
                 LevelNodes ln{sl->n_color[L]->p, sl->n_link[L]->p, sl->n_att[L]->p};
                 // grid hints: last frame's per-level counts (+25 %); level 0 is exact
                 const int ex = L == 0 ? n0 : sl->expect_count[L];
@@ -881,6 +897,13 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 tl.packets = packet_level(ctx, L);  // coherent 8x8-pixel waves -> packet traversal
                 tl.gen = L == 0 && fuse ? &gen : nullptr;
                 tl.pkt_util = fcd->pkt[L];
+                if (binned) {
+                    id = ctx->timer.begin(s, CAT_BIN);
+                    launch_bin_rays(sl->q_key.p, fcd, L, maxc, sl->q_perm.p, ex, s);
+                    ctx->timer.end(s, id);
+                    debug_sync(s, "bin", L, bi);
+                    tl.perm = sl->q_perm.p;
+                }
                 id = ctx->timer.begin_kernel(CAT_TRACE, CAT_LTRACE + L);
                 const bool launched = launch_trace(view, tl, s);
                 ctx->timer.end_kernel(s, id, launched);
@@ -1331,6 +1354,8 @@ int pgrt_set_config(pgrt_ctx* ctx, const pgrt_config* cfg) {
         PGRT_REQUIRE(cfg->max_batch_rays >= 0 && cfg->max_batch_rays <= (1ll << 29), PGRT_ERR_INVALID_ARGUMENT,
                      "max_batch_rays must be in [0, 2^29]");
         PGRT_REQUIRE(cfg->max_batches_in_flight >= 0, PGRT_ERR_INVALID_ARGUMENT, "max_batches_in_flight must be >= 0");
+        PGRT_REQUIRE(cfg->ray_binning == 0 || cfg->ray_binning == -1, PGRT_ERR_INVALID_ARGUMENT,
+                     "ray_binning must be 0 (default) or -1 (off)");
         PGRT_REQUIRE(cfg->rank0_share_a >= 0 && cfg->rank0_share_a <= 64 && cfg->rank0_share_b >= 0 &&
                          cfg->rank0_share_b <= 64,
                      PGRT_ERR_INVALID_ARGUMENT, "rank0_share_a / rank0_share_b must be in [0, 64]");

@@ -355,6 +355,95 @@ void launch_accumulate_frame(const float* frame, float* sum, float* mean, long l
                        reinterpret_cast<float4*>(mean), pixels, count);
 }
 
+// ------------------------------------------------------------------ bounce-level ray binning
+//
+// A level traced as wave packets runs as fast as its slowest wave, and a wave whose 64 rays leave
+// the glass in different directions walks the union of their BVH paths (r2 measurement: skipping
+// waves that spread over > 90 degrees cut a one-frame level-1 launch from 507 to 129 us).  The
+// shade that emits the level's rays writes each ray's direction octant (Queue::key); here a
+// counting sort turns the keys into the order the traversal visits the rays in (perm), bin by
+// bin.  Per block-iteration a bin's rays keep their queue order (ballot + mbcnt ranks), so a wave
+// holds same-octant rays from a few neighbouring 8x8-pixel blocks.  The order of the blocks'
+// ranges inside a bin follows the atomics (not deterministic): it changes which rays share a
+// wave, never a hit (the closest hit of a ray does not depend on the traversal order).
+constexpr int kBinGridMax = 1024;  // grid-stride kernels: bounded atomics per bin
+
+__device__ __forceinline__ void wave_bin_counts(bool active, unsigned key, unsigned& my_rank, unsigned* wcnt) {
+    my_rank = 0;
+#pragma unroll
+    for (unsigned b = 0; b < (unsigned)kBins; ++b) {
+        const unsigned long long m = __ballot(active && key == b);
+        if (active && key == b) my_rank = (unsigned)lanes_below(m);
+        if (__lane_id() == 0) wcnt[b] = (unsigned)__popcll(m);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_bin_hist(const unsigned char* __restrict__ keys, FrameCounters* fc,
+                                                     int level, int cap) {
+    __shared__ unsigned wcnt[kBlock / 64][kBins];
+    __shared__ unsigned tot[kBins];
+    const int n = min(fc_count(*fc, level), cap);
+    const int w = threadIdx.x >> 6;
+    if (threadIdx.x < kBins) tot[threadIdx.x] = 0;
+    __syncthreads();
+    for (int base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        const int i = base + threadIdx.x;
+        const bool active = i < n;
+        unsigned rank;
+        wave_bin_counts(active, active ? keys[i] : 0u, rank, wcnt[w]);
+        __syncthreads();
+        if (threadIdx.x < kBins)
+            for (int k = 0; k < kBlock / 64; ++k) tot[threadIdx.x] += wcnt[k][threadIdx.x];
+        __syncthreads();
+    }
+    if (threadIdx.x < kBins && tot[threadIdx.x]) atomicAdd(&fc->bins[level][threadIdx.x], tot[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_bin_scatter(const unsigned char* __restrict__ keys, FrameCounters* fc,
+                                                        int level, int cap, int* __restrict__ perm) {
+    __shared__ unsigned wcnt[kBlock / 64][kBins];
+    __shared__ unsigned start[kBins];  // this block-iteration's first slot per bin
+    __shared__ unsigned first[kBins];  // exclusive prefix of the bin sizes
+    const int n = min(fc_count(*fc, level), cap);
+    const int w = threadIdx.x >> 6;
+    unsigned* bins = fc->bins[level];
+    if (threadIdx.x == 0) {
+        unsigned acc = 0;
+        for (int b = 0; b < kBins; ++b) {
+            first[b] = acc;
+            acc += bins[b];
+        }
+    }
+    for (int base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        const int i = base + threadIdx.x;
+        const bool active = i < n;
+        const unsigned key = active ? keys[i] : 0u;
+        unsigned rank;
+        wave_bin_counts(active, key, rank, wcnt[w]);
+        __syncthreads();
+        if (threadIdx.x < kBins) {
+            unsigned c = 0;
+            for (int k = 0; k < kBlock / 64; ++k) c += wcnt[k][threadIdx.x];
+            start[threadIdx.x] = first[threadIdx.x] + (c ? atomicAdd(&bins[kBins + threadIdx.x], c) : 0u);
+        }
+        __syncthreads();
+        if (active) {
+            unsigned pos = start[key] + rank;
+            for (int k = 0; k < w; ++k) pos += wcnt[k][key];
+            perm[pos] = i;
+        }
+        __syncthreads();
+    }
+}
+
+void launch_bin_rays(const unsigned char* keys, FrameCounters* fc, int level, int cap, int* perm, int expect,
+                     hipStream_t stream) {
+    if (cap <= 0) return;
+    const int grid = std::min(kBinGridMax, grid_for(cap, expect));
+    hipLaunchKernelGGL(k_bin_hist, dim3(grid), dim3(kBlock), 0, stream, keys, fc, level, cap);
+    hipLaunchKernelGGL(k_bin_scatter, dim3(grid), dim3(kBlock), 0, stream, keys, fc, level, cap, perm);
+}
+
 // ------------------------------------------------------------------ counter export
 
 // last launch of a slot's frame: the frame counters go to pinned host memory and the device

@@ -249,11 +249,13 @@ __device__ __forceinline__ void shade_emit(const SceneView& s, const DevMaterial
             next.ro[sl.refl] = make_float4(r.hitp.x, r.hitp.y, r.hitp.z, 0.01f);
             next.rd[sl.refl] = make_float4(r.refl_dir.x, r.refl_dir.y, r.refl_dir.z, 3.402823466e+38f);
             next.time[sl.refl] = r.n1;
+            if (next.key) next.key[sl.refl] = (unsigned char)dir_octant(r.refl_dir.x, r.refl_dir.y, r.refl_dir.z);
             link.x = sl.refl;
             if (r.nchild == 2) {
                 next.ro[sl.refr] = make_float4(r.hitp.x, r.hitp.y, r.hitp.z, 0.01f);
                 next.rd[sl.refr] = make_float4(r.refr_dir.x, r.refr_dir.y, r.refr_dir.z, 3.402823466e+38f);
                 next.time[sl.refr] = r.n2;
+                if (next.key) next.key[sl.refr] = (unsigned char)dir_octant(r.refr_dir.x, r.refr_dir.y, r.refr_dir.z);
                 link.y = sl.refr;
             }
         }

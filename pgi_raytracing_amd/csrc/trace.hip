@@ -119,7 +119,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
                                                        const int* __restrict__ count_dev, int count_terms,
                                                        int count_host, int cap, int* __restrict__ gstack,
                                                        unsigned long long* __restrict__ counters, int rpw,
-                                                       float4 const_org, unsigned char* __restrict__ lit) {
+                                                       float4 const_org, unsigned char* __restrict__ lit,
+                                                       const int* __restrict__ perm) {
     extern __shared__ int lstack[];  // [entries][kTraceBlock]
     const int tid = threadIdx.x;
     const int lane = __lane_id();
@@ -152,8 +153,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
     int msp = 0;
     for (;;) {
         stride_i += wstride;
-        const int i = stride_i;
-        if (i >= n) break;
+        if (stride_i >= n) break;
+        const int i = perm ? perm[stride_i] : stride_i;  // binned level: the ray of this slot
         const float4 o4 = ro ? ro[i] : const_org;
         const float4 d4 = rd[i];
         const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
@@ -536,7 +537,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8g(SceneView s, const floa
                                                          const float4* __restrict__ rd, float4* __restrict__ hits,
                                                          const int* __restrict__ count_dev, int count_terms,
                                                          int count_host, int cap,
-                                                         unsigned long long* __restrict__ counters) {
+                                                         unsigned long long* __restrict__ counters,
+                                                         const int* __restrict__ perm) {
     static_assert(G == 4 || G == 8, "lanes per ray");
     constexpr int kGroups = kTraceBlock / G;
     __shared__ uint2 gstk[kGroupStack][kGroups];
@@ -546,8 +548,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8g(SceneView s, const floa
     const int gshift = __lane_id() & ~(G - 1);
     const int n = ray_count(count_dev, count_terms, count_host, cap);
     unsigned long long nvis = 0, ntest = 0, mvis = 0, mtest = 0;
-    for (int i = blockIdx.x * kGroups + gib; i < n; i += gridDim.x * kGroups) {
-            const float4 o4 = ro[i];
+    for (int slot_i = blockIdx.x * kGroups + gib; slot_i < n; slot_i += gridDim.x * kGroups) {
+        const int i = perm ? perm[slot_i] : slot_i;  // binned level: the ray of this slot
+        const float4 o4 = ro[i];
         const float4 d4 = rd[i];
         const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
         const float dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
@@ -710,7 +713,8 @@ template <bool COUNT, bool GEN, bool SAMPLE>
 __device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __restrict__ ro,
                                           const float4* __restrict__ rd, float4* __restrict__ hits, int n,
                                           unsigned long long* __restrict__ counters, const PrimaryGen& gen,
-                                          unsigned long long* __restrict__ util, int (*wstack)[kPktStack]) {
+                                          unsigned long long* __restrict__ util, int (*wstack)[kPktStack],
+                                          const int* __restrict__ perm) {
     const int wib = threadIdx.x >> 6;
     const int lane = __lane_id();
     const cfloat_ptr nodes = (cfloat_ptr)(const void*)s.nodes;  // 16 floats per node
@@ -722,8 +726,10 @@ __device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __re
     constexpr bool sample = SAMPLE;
     unsigned useful = 0, live_steps = 0;
     for (int base = (blockIdx.x * kTraceBlock) + wib * 64; base < n; base += gridDim.x * kTraceBlock) {
-        const int i = base + lane;
-        const bool valid = i < n;
+        const int slot_i = base + lane;
+        const bool valid = slot_i < n;
+        // binned level: the ray of this slot (ro / rd / hits indexed by it); level 0: the slot
+        const int i = (!GEN && perm && valid) ? perm[slot_i] : slot_i;
         float4 o4 = make_float4(0, 0, 0, 0), d4 = make_float4(0, 0, 1, -1.0f);
         bool pv = false;
         if (valid) {
@@ -849,19 +855,20 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void k_trace_pkt(SceneView s, co
                                                            const int* __restrict__ count_dev, int count_terms,
                                                            int count_host, int cap,
                                                            unsigned long long* __restrict__ counters, PrimaryGen gen,
-                                                           unsigned long long* __restrict__ util) {
+                                                           unsigned long long* __restrict__ util,
+                                                           const int* __restrict__ perm) {
     __shared__ int wstack[kTraceBlock / 64][kPktStack];
     const int n = ray_count(count_dev, count_terms, count_host, cap);
     if constexpr (GEN) {
         if (gen.store_count && blockIdx.x == 0 && threadIdx.x == 0) *gen.store_count = n;
         // level 0 is always traced as packets: its utilisation is never sampled
-        pkt_trace<COUNT, GEN, false>(s, ro, rd, hits, n, counters, gen, util, wstack);
+        pkt_trace<COUNT, GEN, false>(s, ro, rd, hits, n, counters, gen, util, wstack, nullptr);
     } else {
         // packet utilisation sampled in every 8th block (pgrt_config.packet_levels AUTO)
         if (util != nullptr && (blockIdx.x & 7) == 0)
-            pkt_trace<COUNT, GEN, true>(s, ro, rd, hits, n, counters, gen, util, wstack);
+            pkt_trace<COUNT, GEN, true>(s, ro, rd, hits, n, counters, gen, util, wstack, perm);
         else
-            pkt_trace<COUNT, GEN, false>(s, ro, rd, hits, n, counters, gen, util, wstack);
+            pkt_trace<COUNT, GEN, false>(s, ro, rd, hits, n, counters, gen, util, wstack, perm);
     }
 }
 
@@ -896,6 +903,8 @@ bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) 
     PGRT_REQUIRE((t.ro && !t.lit) || (!s.wide && !t.packets && !t.gen && !t.allow_group), PGRT_ERR_INVALID_ARGUMENT,
                  "compact shadow queues are traced by the one-lane binary kernel only");
     const int ex = t.expect > 0 && t.expect < max_count ? t.expect : max_count;  // grid sizing only
+    PGRT_REQUIRE(!t.perm || (!s.wide && !t.lit && !t.gen), PGRT_ERR_INVALID_ARGUMENT,
+                 "binned launches are level queues over the binary or grouped 8-wide kernels");
     if (s.wide) {
         int grid = ceil_div(ex, kTraceBlock);
         if (grid > t.gstack_threads / kTraceBlock) grid = t.gstack_threads / kTraceBlock;
@@ -914,7 +923,7 @@ bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) 
         const PrimaryGen g = t.gen ? *t.gen : PrimaryGen{};
 #define PGRT_LAUNCH_P(C, G, W)                                                                                \
     PGRT_TLAUNCH((k_trace_pkt<C, G, W>), dim3(grid), dim3(kTraceBlock), 0, stream, s, t.ro, t.rd, t.hits,     \
-                 t.count_dev, t.count_terms, t.count_host, max_count, t.counters, g, t.pkt_util)
+                 t.count_dev, t.count_terms, t.count_host, max_count, t.counters, g, t.pkt_util, t.perm)
         const bool big = s.ntri > kPacketBigScene;
         if (t.count) {
             if (t.gen) PGRT_LAUNCH_P(true, true, 1); else PGRT_LAUNCH_P(true, false, 1);
@@ -932,7 +941,7 @@ bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) 
         const bool g4 = ex > kGroup8Max;
 #define PGRT_LAUNCH_G(C, G)                                                                                       \
     PGRT_TLAUNCH((k_trace8g<C, G>), dim3(std::min(16384, ceil_div(ex, kTraceBlock / G))), dim3(kTraceBlock), 0, \
-                 stream, s, t.ro, t.rd, t.hits, t.count_dev, t.count_terms, t.count_host, max_count, t.counters)
+                 stream, s, t.ro, t.rd, t.hits, t.count_dev, t.count_terms, t.count_host, max_count, t.counters, t.perm)
         if (t.count) {
             if (g4) PGRT_LAUNCH_G(true, 4); else PGRT_LAUNCH_G(true, 8);
         } else {
@@ -950,7 +959,7 @@ bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) 
     const size_t lds = (size_t)(spill ? kLdsStack : entries) * kTraceBlock * sizeof(int);
 #define PGRT_LAUNCH(C, S)                                                                                       \
     PGRT_TLAUNCH((k_trace<C, S>), dim3(grid), dim3(kTraceBlock), lds, stream, s, t.ro, t.rd, t.hits, t.count_dev, \
-                 t.count_terms, t.count_host, max_count, t.gstack, t.counters, rpw, t.const_org, t.lit)
+                 t.count_terms, t.count_host, max_count, t.gstack, t.counters, rpw, t.const_org, t.lit, t.perm)
     if (t.count) {
         if (spill) PGRT_LAUNCH(true, true); else PGRT_LAUNCH(true, false);
     } else {

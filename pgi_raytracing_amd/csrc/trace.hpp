@@ -12,6 +12,10 @@ constexpr int kLdsStack = 16;
 constexpr int kGlobalStack = 112;
 constexpr int kTile = 64;         // image tile side (multi-GPU unit, level-0 ray order)
 constexpr int kMaxLevels = 16;    // max_level + 1 <= kMaxLevels
+// bounce-level ray binning (pgrt_config.ray_binning): the rays of a level traced as wave packets
+// are visited in bins of equal direction octant (key = sign bits of the direction), so a wave's
+// 64 rays share their direction signs and, within a bin, the queue's screen-space order
+constexpr int kBins = 8;
 
 // Per-frame device counters (zeroed by one hipMemsetAsync per batch).
 struct FrameCounters {
@@ -35,6 +39,8 @@ struct FrameCounters {
     // profile == 2: per level, shaded rays that hit a triangle and, of those, the ones whose
     // Phong branch sampled a texture (the whole-frame roofline's attribute / texel bytes)
     alignas(128) unsigned long long shade[kMaxLevels][2];
+    // ray binning per level: bin sizes [0, kBins), then the scatter's cursors [kBins, 2 kBins)
+    alignas(128) unsigned bins[kMaxLevels][2 * kBins];
 };
 
 __host__ __device__ inline int fc_count(const FrameCounters& f, int L) {
@@ -77,7 +83,14 @@ struct Queue {
     float* time;     // medium IOR (RTCRay::time as used by the reference)
     float4* hit;     // t, u, v, prim bits
     int cap;
+    unsigned char* key = nullptr;  // binning key per ray (written by the shade that emits the rays), or NULL
 };
+
+// direction octant of a ray: the sign bits the packet traversal specialises its node loop on
+// (bit 0: x < 0, bit 1: y < 0, bit 2: z < 0; -0 counts as negative, as rcp(-0) < 0)
+__device__ inline unsigned dir_octant(float x, float y, float z) {
+    return (__float_as_uint(x) >> 31) | ((__float_as_uint(y) >> 31) << 1) | ((__float_as_uint(z) >> 31) << 2);
+}
 
 // Where a batch's finished pixels go (k_finish; the level-0 packet traversal for primary-ray
 // misses of a 1-spp frame).  mode 0: framebuffer (rect origin ox,oy, row pitch in pixels);
@@ -147,6 +160,8 @@ struct TraceLaunch {
     // const_org (xyz, tnear in w); lit != NULL -> write is_illuminated's byte, not the hit
     float4 const_org = make_float4(0, 0, 0, 0);
     unsigned char* lit = nullptr;
+    // binned level: launch slot i traces ray perm[i] (ro / rd / hits indexed by it), NULL = i
+    const int* perm = nullptr;
 };
 // the packet traversal needs the binary layout and a tree that fits its wave-uniform stack
 bool trace_packets_available(const SceneView& s);
@@ -186,6 +201,10 @@ void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles,
 // frame sink: sum += frame (count-th frame; count == 1 resets), mean = sum / count
 void launch_accumulate_frame(const float* frame, float* sum, float* mean, long long pixels, int count,
                              hipStream_t stream);
+// ray binning of level `level` (FrameCounters::bins): histogram of the keys, then the scatter of
+// the ray indices into perm, bin by bin (expect sizes the grids)
+void launch_bin_rays(const unsigned char* keys, FrameCounters* fc, int level, int cap, int* perm, int expect,
+                     hipStream_t stream);
 // copy `n` FrameCounters to pinned host memory and zero them on the device
 void launch_export_counters(FrameCounters* dev, FrameCounters* host, int n, hipStream_t stream);
 // Distributed frames: rank r's tile-compact buffer (frame-major, count[r] tiles per frame in its

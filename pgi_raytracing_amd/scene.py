@@ -37,6 +37,9 @@ def _jpeg_lib():
         lib.pgrt_jpeg_decode.argtypes = [C.c_char_p, C.c_int] + [C.POINTER(C.c_int)] * 4 + [C.c_void_p, C.c_size_t]
         lib.pgrt_jpeg_decode.restype = C.c_int
         lib.pgrt_jpeg_error.restype = C.c_char_p
+        lib.pgrt_png_decode.argtypes = [C.c_char_p] + [C.POINTER(C.c_int)] * 4 + [C.c_void_p, C.c_size_t]
+        lib.pgrt_png_decode.restype = C.c_int
+        lib.pgrt_png_error.restype = C.c_char_p
         _JPEG = lib
     return _JPEG
 
@@ -55,13 +58,27 @@ def decode_jpeg(path: str, accurate: bool = False):
     return w.value, h.value, b.value, p.value, buf
 
 
+def decode_png(path: str):
+    """(width, height, bpp, pitch, bytes): BGR(A), top-down, FreeImage pitch (libpgrt_image.so's
+    libpng decode, csrc/image_png.c; lossless, so FreeImage's bytes)."""
+    lib = _jpeg_lib()
+    w, h, b, p = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    args = (path.encode(), C.byref(w), C.byref(h), C.byref(b), C.byref(p))
+    if lib.pgrt_png_decode(*args, None, 0) != 0:
+        raise RuntimeError(lib.pgrt_png_error().decode())
+    buf = np.zeros(p.value * h.value, np.uint8)
+    if lib.pgrt_png_decode(*args, buf.ctypes.data, buf.size) != 0:
+        raise RuntimeError(lib.pgrt_png_error().decode())
+    return w.value, h.value, b.value, p.value, buf
+
+
 @dataclass
 class TextureData:
     """Texture::Texture (texture.cpp:5-54): raw BGR(A), top-down, FreeImage pitch.
 
     JPEG: FreeImage_Load with flags 0 = JPEG_DEFAULT (FreeImage.h:693-695), i.e. IJG libjpeg's
-    fast integer IDCT without fancy upsampling (decode_jpeg, libpgrt_image.so).  PNG: PIL
-    (lossless, so the bytes are FreeImage's)."""
+    fast integer IDCT without fancy upsampling (decode_jpeg, libpgrt_image.so).  PNG: libpng
+    (decode_png, the same library; lossless, so the bytes are FreeImage's)."""
 
     width: int
     height: int
@@ -72,21 +89,12 @@ class TextureData:
 
     @staticmethod
     def from_file(path: str) -> "TextureData":
-        if path.lower().endswith((".jpg", ".jpeg")):
-            w, h, bpp, pitch, buf = decode_jpeg(path)
-            return TextureData(w, h, pitch, bpp, buf, os.path.basename(path))
-        from PIL import Image  # host-side PNG decode only
-
-        im = Image.open(path)
-        if im.mode not in ("RGB", "RGBA"):
-            im = im.convert("RGBA" if "A" in im.mode else "RGB")
-        a = np.asarray(im, dtype=np.uint8)
-        h, w, ch = a.shape
-        bgr = a[:, :, [2, 1, 0, 3] if ch == 4 else [2, 1, 0]]
-        pitch = freeimage_pitch(w, ch)
-        buf = np.zeros((h, pitch), np.uint8)
-        buf[:, : w * ch] = bgr.reshape(h, w * ch)
-        return TextureData(w, h, pitch, ch, np.ascontiguousarray(buf.reshape(-1)), os.path.basename(path))
+        with open(path, "rb") as fh:  # FreeImage_GetFileType: the signature decides (texture.cpp:15)
+            sig = fh.read(8)
+        jpeg = sig[:3] == b"\xff\xd8\xff" or (sig[:8] != b"\x89PNG\r\n\x1a\n"
+                                               and path.lower().endswith((".jpg", ".jpeg", ".jpe")))
+        w, h, bpp, pitch, buf = decode_jpeg(path) if jpeg else decode_png(path)
+        return TextureData(w, h, pitch, bpp, buf, os.path.basename(path))
 
     @staticmethod
     def from_bgr(bgr: np.ndarray, name: str = "") -> "TextureData":

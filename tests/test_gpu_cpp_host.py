@@ -23,6 +23,12 @@ def test_tutorial_1_prints_reference_output():
 
 
 def test_raytrace_loop_frame_matches_oracle(tmp_path, avenger_obj, avenger_scene):
+    """raytrace_loop through the C++ facade alone: LoadOBJ in libpgrt, every texture decoded from
+    the reference's own .jpg files by libpgrt_image (Texture::Texture, texture.cpp:5-54) -- no
+    Python-written texture files anywhere -- and the frame equals the oracle's bit for bit."""
+    import glob
+
+    assert not glob.glob(os.path.join(ROOT, "assets", "**", "*.pgrttex"), recursive=True)
     raw = tmp_path / "frame.raw"
     W, H, S, d, dof = 160, 120, 2, 5, 1
     out = subprocess.run([EXE, "render", avenger_obj, ENV_MAP, str(raw), str(W), str(H), str(S), str(d), str(dof)],

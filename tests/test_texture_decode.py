@@ -10,12 +10,11 @@ IDCT; FreeImage itself is absent, so the IFAST bytes are pinned by the decoder s
 a FreeImage-produced fixture.
 """
 import os
-import struct
 
 import numpy as np
 import pytest
 
-from pgi_raytracing_amd.scene import TextureData, decode_jpeg
+from pgi_raytracing_amd.scene import TextureData, decode_jpeg, decode_png
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ENV = os.path.join(ROOT, "assets", "spherical_map_windows.jpg")
@@ -30,7 +29,8 @@ def test_image_library_exports_its_header():
     text = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "pgrt_image.h")).read(), flags=re.S)
     names = sorted(set(re.findall(r"\b(pgrt_[a-z0-9_]+)\s*\(", text)))
     lib = C.CDLL(os.path.join(ROOT, "pgi_raytracing_amd", "lib", "libpgrt_image.so"))
-    assert names == ["pgrt_jpeg_decode", "pgrt_jpeg_error"]
+    assert names == ["pgrt_image_decode", "pgrt_image_error", "pgrt_jpeg_decode", "pgrt_jpeg_error",
+                     "pgrt_png_decode", "pgrt_png_error"]
     assert all(hasattr(lib, n) for n in names)
 
 
@@ -57,18 +57,54 @@ def test_default_load_is_the_fast_idct():
 
 
 @pytest.mark.parametrize("path", JPEGS)
-def test_texture_and_sidecar_are_the_ifast_decode(path):
+def test_texture_is_the_ifast_decode(path):
     w, h, bpp, pitch, buf = decode_jpeg(path)
     assert pitch % 4 == 0 and pitch >= w * 3
     t = TextureData.from_file(path)
     assert (t.width, t.height, t.bpp, t.pitch) == (w, h, bpp, pitch)
     assert np.array_equal(t.data, buf)
-    side = path + ".pgrttex"
-    if not os.path.exists(side):
-        pytest.skip("sidecars are written by __graft_entry__.build()")
-    with open(side, "rb") as f:
-        assert f.read(8) == b"PGRTTEX1"
-        sw, sh, sp, sb = struct.unpack("<4i", f.read(16))
-        data = np.frombuffer(f.read(), np.uint8)
-    assert (sw, sh, sp, sb) == (w, h, pitch, bpp)
-    assert np.array_equal(data, buf)
+
+
+PNGS = [os.path.join(ROOT, "assets", "test3.png"), os.path.join(ROOT, "assets", "test4.png")]
+
+
+@pytest.mark.parametrize("path", PNGS)
+def test_png_decode_matches_independent_decoder(path):
+    """libpgrt_image's libpng decode (the C++ host's and the scene loader's) equals PIL's pixels
+    in FreeImage's raw layout: BGR (test3.png, RGB) / BGRA (test4.png, RGBA), 4-byte aligned
+    pitch, top row first."""
+    from PIL import Image
+
+    w, h, bpp, pitch, buf = decode_png(path)
+    im = Image.open(path)
+    ch = {"RGB": 3, "RGBA": 4}[im.mode]
+    assert (w, h, bpp) == (im.width, im.height, ch) and pitch == ((w * ch * 8 + 31) // 32) * 4
+    a = np.asarray(im, dtype=np.uint8)
+    got = buf.reshape(h, pitch)[:, : w * ch].reshape(h, w, ch)
+    assert np.array_equal(got, a[:, :, [2, 1, 0, 3][:ch]])
+    t = TextureData.from_file(path)
+    assert (t.width, t.height, t.bpp, t.pitch) == (w, h, bpp, pitch) and np.array_equal(t.data, buf)
+
+
+def test_image_decode_dispatches_on_the_signature(tmp_path):
+    """Texture::Texture asks FreeImage for the type by file signature first (texture.cpp:15):
+    a JPEG saved under a .png name still decodes as the JPEG_DEFAULT load."""
+    import ctypes as C
+    import shutil
+
+    lib = C.CDLL(os.path.join(ROOT, "pgi_raytracing_amd", "lib", "libpgrt_image.so"))
+    lib.pgrt_image_decode.argtypes = [C.c_char_p] + [C.POINTER(C.c_int)] * 4 + [C.c_void_p, C.c_size_t]
+    lib.pgrt_image_error.restype = C.c_char_p
+    src = JPEGS[2]
+    fake = tmp_path / "decal.png"
+    shutil.copy(src, fake)
+    w, h, b, p = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    assert lib.pgrt_image_decode(str(fake).encode(), C.byref(w), C.byref(h), C.byref(b), C.byref(p), None, 0) == 0
+    out = np.zeros(p.value * h.value, np.uint8)
+    assert lib.pgrt_image_decode(str(fake).encode(), C.byref(w), C.byref(h), C.byref(b), C.byref(p),
+                                 out.ctypes.data, out.size) == 0
+    assert np.array_equal(out, decode_jpeg(src)[4])
+    bad = tmp_path / "x.bin"
+    bad.write_bytes(b"not an image")
+    assert lib.pgrt_image_decode(str(bad).encode(), C.byref(w), C.byref(h), C.byref(b), C.byref(p), None, 0) == -1
+    assert b"unknown image format" in lib.pgrt_image_error()

@@ -27,6 +27,9 @@ def main():
         if not os.environ.get("DIAG_NOENV"):
             sc.set_environment(env)
     ctx = Context(0)
+    for kv in filter(None, os.environ.get("DIAG_CFG", "").split(",")):  # e.g. DIAG_CFG=ray_binning=-1
+        k, v = kv.split("=", 1)
+        ctx.configure(**{k: float(v) if "." in v else int(v)})
     t = time.time()
     ctx.set_scene(sc)
     info = ctx.bvh_info()
@@ -39,12 +42,20 @@ def main():
         ctx.set_camera(abi.default_camera(W, H))
     p = abi.make_params(spp_side=S, max_level=d, dof=dof,
                         jitter=abi.PGRT_JITTER_HASH if S > 1 or dof else abi.PGRT_JITTER_NONE)
-    ctx.render(p)
+    F = int(os.environ.get("DIAG_FRAMES", "1"))  # frames per call (the bench's batched frames)
+    buf = ctx.alloc(F * W * H * 16)
+
+    def render(q):
+        if F == 1:
+            return ctx.render(q)
+        return None, ctx.render_frames_device(q, F, buf)
+
+    render(p)
     p.profile = 1
     reps = int(os.environ.get("DIAG_REPS", "9"))  # medians over repeated profiled frames
     stats, lvs = [], []
     for _ in range(reps):
-        _, st = ctx.render(p)
+        _, st = render(p)
         stats.append(st.as_dict())
         lvs.append([(dd["ms_trace"], dd["ms_shade"]) for dd in ctx.frame_diag()])
     med = lambda xs: sorted(xs)[len(xs) // 2]  # noqa: E731
@@ -52,7 +63,7 @@ def main():
                       "rays": st.rays(), "trace_launches": st.trace_launches, "reps": reps}))
     lv_ms = [(med([lv[L][0] for lv in lvs]), med([lv[L][1] for lv in lvs])) for L in range(len(lvs[0]))]
     p.profile = 2
-    ctx.render(p)
+    render(p)
     for L, dd in enumerate(ctx.frame_diag()):
         if dd["rays"] == 0 and dd["shadow_rays"] == 0:
             continue
