@@ -114,6 +114,7 @@ struct FrameSlot {
     DevBuf<float> q_time[2];
     DevBuf<unsigned char> q_key;  // binning key of the next level's rays (one level at a time)
     DevBuf<int> q_perm;           // the binned level's traversal order
+    DevBuf<unsigned> q_bins;      // per-chunk bin counts / offsets of the binning sort
     DevBuf<unsigned long long> l0_hit, l0_pending;  // 1-spp level-0 wave masks (L0Final)
     int q_cap = 0;
     std::vector<std::unique_ptr<DevBuf<float4>>> n_color, n_att;
@@ -264,6 +265,11 @@ struct pgrt_ctx {
 
     // multi-GPU
     ncclComm_t comm = nullptr;
+    // control communicator (ncclCommSplit of comm) on its own stream: the per-frame overflow
+    // agreement of distributed frames, never queued behind the gathers on `stream`
+    ncclComm_t comm_ctl = nullptr;
+    hipStream_t ctl_stream = nullptr;
+    DevBuf<int> ctl_buf;
     int world = 1, rank = 0;
     // PGRT_EMULATE_RANK=r/N (measurement tool only, no communicator): distributed frames render
     // rank r's share of an N-GPU frame on this device; the gather becomes a device copy of this
@@ -277,6 +283,8 @@ struct pgrt_ctx {
     int acc_count = 0, acc_w = 0, acc_h = 0;
 
     ~pgrt_ctx() {
+        if (comm_ctl) (void)ncclCommDestroy(comm_ctl);
+        if (ctl_stream) (void)hipStreamDestroy(ctl_stream);
         if (comm) (void)ncclCommDestroy(comm);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -528,6 +536,7 @@ void ensure_frame_buffers(FrameSlot* sl, int n0, int levels, int nlight, int bat
         sl->l0_pending.alloc((size_t)n0 / 64 + 1);
         sl->q_key.alloc(n0);
         sl->q_perm.alloc(n0);
+        sl->q_bins.alloc(((size_t)n0 / 256 + 1) * kBins);
         sl->q_cap = n0;
     }
     if ((int)sl->level_cap.size() < levels) sl->level_cap.resize(levels, 0);
@@ -583,6 +592,7 @@ void grow_after_overflow(FrameSlot* sl, int levels) {
                 }
                 sl->q_key.alloc(need);
                 sl->q_perm.alloc(need);
+                sl->q_bins.alloc(((size_t)need / 256 + 1) * kBins);
                 sl->q_cap = need;
             }
         }
@@ -899,7 +909,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 tl.pkt_util = fcd->pkt[L];
                 if (binned) {
                     id = ctx->timer.begin(s, CAT_BIN);
-                    launch_bin_rays(sl->q_key.p, fcd, L, maxc, sl->q_perm.p, ex, s);
+                    launch_bin_rays(sl->q_key.p, fcd, L, maxc, sl->q_perm.p, sl->q_bins.p, ex, s);
                     ctx->timer.end(s, id);
                     debug_sync(s, "bin", L, bi);
                     tl.perm = sl->q_perm.p;
@@ -973,79 +983,85 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
     fs->stats.trace_launches = trace_launches;
 }
 
-// Wait for fs's frame, re-render it after a queue overflow (larger queues), fill fs->stats; the
-// context stream is then ordered after the frame.
-void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
+// One look at fs's completed frame (host waits for its slots): the counters to the host, the next
+// frame's grid hints.  Returns whether a queue of this rank overflowed (the frame is incomplete).
+bool read_frame_counters(pgrt_ctx* ctx, FrameSet* fs) {
+    const int K = fs->K;
+    for (int j = 0; j < K; ++j) {
+        FrameSlot* sl = fs->slots[j].get();
+        PGRT_HIP(hipEventSynchronize(sl->ev_done));
+        std::copy(sl->pinned_fc, sl->pinned_fc + sl->host_fc.size(), sl->host_fc.begin());
+    }
+    PGRT_HIP(hipGetLastError());
+    bool overflow = false;
+    ctx->last_fc.clear();
+    for (int j = 0; j < K; ++j) {
+        FrameSlot* sl = fs->slots[j].get();
+        for (auto& h : sl->host_fc) {
+            overflow |= h.overflow != 0;
+            ctx->last_fc.push_back(h);
+        }
+        int shadow_need = 0;
+        for (auto& h : sl->host_fc) {
+            int sc = 0;
+            for (int L = 0; L < kMaxLevels; ++L) sc += fc_shadow(h, L);
+            shadow_need = std::max(shadow_need, sc);
+        }
+        // grid hints for the next frame: kept while the count stays within [hint/2, hint]
+        // (a stable hint keeps the captured launch sequence valid)
+        auto hint = [](int& e, int c) {
+            if (e == 0 || c > e || 2 * c + 2048 < e) e = c + c / 4 + 1024;
+        };
+        for (int L = 0; L < kMaxLevels; ++L) {
+            int c = 0;
+            for (auto& h : sl->host_fc) c = std::max(c, fc_count(h, L));
+            hint(sl->expect_count[L], c);
+        }
+        hint(sl->expect_shadow_total, shadow_need);
+    }
+    return overflow;
+}
+
+// Re-render fs after a queue overflow: this rank's queues grow when it overflowed (grow), the
+// timings of the failed attempt are dropped.
+void rerender_frame(pgrt_ctx* ctx, FrameSet* fs, bool grow, int& retries) {
+    const int levels = fs->params.max_level + 1;
+    if (grow)
+        for (int j = 0; j < fs->K; ++j) grow_after_overflow(fs->slots[j].get(), levels);
+    double ms[CAT_N] = {0};
+    ctx->timer.collect(ms);
+    ++retries;
+    PGRT_REQUIRE(retries < 8, PGRT_ERR_OUT_OF_MEMORY, "ray queues kept overflowing");
+    enqueue_frame(ctx, fs);
+}
+
+// fs->stats of a complete frame (counters read by read_frame_counters); the context stream is
+// then ordered after the frame.
+void frame_stats(pgrt_ctx* ctx, FrameSet* fs, int retries) {
     const pgrt_render_params* p = &fs->params;
     const int levels = p->max_level + 1;
     const int spp = p->spp_side * p->spp_side;
     double ms[CAT_N] = {0};
     uint64_t rays_shadow = 0, rays_reflect = 0, rays_refract = 0, trav_nodes = 0, trav_tests = 0, trav_wide = 0;
     uint64_t shade_hits = 0, shade_textured = 0;
-    int retries = 0;
-    for (;;) {
-        const int K = fs->K;
-        for (int j = 0; j < K; ++j) {
-            FrameSlot* sl = fs->slots[j].get();
-            PGRT_HIP(hipEventSynchronize(sl->ev_done));
-            std::copy(sl->pinned_fc, sl->pinned_fc + sl->host_fc.size(), sl->host_fc.begin());
-        }
-        PGRT_HIP(hipGetLastError());
-        bool overflow = false;
-        ctx->last_fc.clear();
-        for (int j = 0; j < K; ++j) {
-            FrameSlot* sl = fs->slots[j].get();
-            for (auto& h : sl->host_fc) {
-                overflow |= h.overflow != 0;
-                ctx->last_fc.push_back(h);
-            }
-            int shadow_need = 0;
-            for (auto& h : sl->host_fc) {
-                int sc = 0;
-                for (int L = 0; L < kMaxLevels; ++L) sc += fc_shadow(h, L);
-                shadow_need = std::max(shadow_need, sc);
-            }
-            // grid hints for the next frame: kept while the count stays within [hint/2, hint]
-            // (a stable hint keeps the captured launch sequence valid)
-            auto hint = [](int& e, int c) {
-                if (e == 0 || c > e || 2 * c + 2048 < e) e = c + c / 4 + 1024;
-            };
-            for (int L = 0; L < kMaxLevels; ++L) {
-                int c = 0;
-                for (auto& h : sl->host_fc) c = std::max(c, fc_count(h, L));
-                hint(sl->expect_count[L], c);
-            }
-            hint(sl->expect_shadow_total, shadow_need);
-        }
-        if (overflow) {
-            for (int j = 0; j < K; ++j) grow_after_overflow(fs->slots[j].get(), levels);
-            ctx->timer.collect(ms);
-            std::fill(ms, ms + CAT_N, 0.0);
-            ++retries;
-            PGRT_REQUIRE(retries < 8, PGRT_ERR_OUT_OF_MEMORY, "ray queues kept overflowing");
-            enqueue_frame(ctx, fs);
-            continue;
-        }
-        update_packet_choice(ctx, ctx->last_fc, levels);
-        for (auto& h : ctx->last_fc) {
-            for (int L = 0; L < levels; ++L) {
-                rays_shadow += (uint64_t)fc_shadow(h, L);
-                if (L >= 1) {
-                    rays_refract += (uint64_t)h.refract[L];
-                    rays_reflect += (uint64_t)(fc_count(h, L) - h.refract[L]);
-                }
-            }
-            for (int L = 0; L < kMaxLevels; ++L) {
-                shade_hits += h.shade[L][0];
-                shade_textured += h.shade[L][1];
-            }
-            for (int k = 0; k < 2 * kMaxLevels; ++k) {
-                trav_wide += h.trav[k][14];
-                trav_nodes += h.trav[k][0];
-                trav_tests += h.trav[k][1];
+    update_packet_choice(ctx, ctx->last_fc, levels);
+    for (auto& h : ctx->last_fc) {
+        for (int L = 0; L < levels; ++L) {
+            rays_shadow += (uint64_t)fc_shadow(h, L);
+            if (L >= 1) {
+                rays_refract += (uint64_t)h.refract[L];
+                rays_reflect += (uint64_t)(fc_count(h, L) - h.refract[L]);
             }
         }
-        break;
+        for (int L = 0; L < kMaxLevels; ++L) {
+            shade_hits += h.shade[L][0];
+            shade_textured += h.shade[L][1];
+        }
+        for (int k = 0; k < 2 * kMaxLevels; ++k) {
+            trav_wide += h.trav[k][14];
+            trav_nodes += h.trav[k][0];
+            trav_tests += h.trav[k][1];
+        }
     }
     for (int j = 0; j < fs->K; ++j) PGRT_HIP(hipStreamWaitEvent(ctx->stream, fs->slots[j]->ev_done, 0));
     ctx->timer.collect(ms);
@@ -1077,6 +1093,40 @@ void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
     st->overflow_retries = retries;
 }
 
+// Multi-process distributed frames: did ANY rank's queues overflow?  Every rank asks for every
+// frame in the same order (frames complete in submission order), over the control communicator
+// on its own stream -- not behind the gathers queued on the context stream, so the host waits for
+// the other ranks' answers only, never for later frames.
+bool any_rank_overflowed(pgrt_ctx* ctx, bool mine) {
+    if (!ctx->comm_ctl) return mine;
+    ctx->ctl_buf.alloc(1);
+    int v = mine ? 1 : 0;
+    PGRT_HIP(hipMemcpyAsync(ctx->ctl_buf.p, &v, sizeof(int), hipMemcpyHostToDevice, ctx->ctl_stream));
+    const ncclResult_t r = ncclAllReduce(ctx->ctl_buf.p, ctx->ctl_buf.p, 1, ncclInt32, ncclMax, ctx->comm_ctl,
+                                         ctx->ctl_stream);
+    if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string("ncclAllReduce (overflow flag): ") + ncclGetErrorString(r));
+    PGRT_HIP(hipMemcpyAsync(&v, ctx->ctl_buf.p, sizeof(int), hipMemcpyDeviceToHost, ctx->ctl_stream));
+    PGRT_HIP(hipStreamSynchronize(ctx->ctl_stream));
+    return v != 0;
+}
+
+void gather_frame(pgrt_ctx* ctx, FrameSet* fs);
+
+// Wait for fs's frame, re-render it after a queue overflow (larger queues), fill fs->stats.  A
+// distributed frame's gather was queued with the frame (device-ordered, start_frame): when any
+// rank overflowed, every rank re-renders and re-gathers it, so the collectives stay matched.
+void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
+    int retries = 0;
+    for (;;) {
+        const bool mine = read_frame_counters(ctx, fs);
+        const bool any = fs->distributed ? any_rank_overflowed(ctx, mine) : mine;
+        if (!any) break;
+        rerender_frame(ctx, fs, mine, retries);
+        if (fs->distributed) gather_frame(ctx, fs);
+    }
+    frame_stats(ctx, fs, retries);
+}
+
 // this rank's tile count and every rank's list layout for a distributed frame of W x H
 UnpackSrc unpack_layout(const TileDeal& d, int W, int H) {
     const int total = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
@@ -1091,18 +1141,24 @@ UnpackSrc unpack_layout(const TileDeal& d, int W, int H) {
     return u;
 }
 
-// distributed frame: every rank's tile-compact RGB buffer to rank 0 (grouped ncclSend / ncclRecv
-// with each rank's exact tile count -- no padding crosses xGMI; rank 0's own tiles stay in
-// place) and the unpack kernel there, on the context stream (after the frame's slots)
-void gather_frame(pgrt_ctx* ctx, FrameSet* fs) {
-    const int W = fs->cam_w, H = fs->cam_h;
+// Distributed frame: every rank's tile-compact RGB buffer to rank 0 (grouped ncclSend / ncclRecv
+// with each rank's exact tile count -- no padding crosses xGMI; rank 0's own tiles stay in place)
+// and the unpack kernel there, on the context stream.  Queued when the frame is submitted: the
+// context stream waits for the frame's slots on the DEVICE (hipStreamWaitEvent), so no rank's
+// send, and neither rank 0's receive nor its unpack, waits for the host to see the frame done.
+// Three parts, so a single-process multi-device context can put every rank's sends / receives
+// in ONE ncclGroupStart / ncclGroupEnd (gather_begin, gather_post in a group, gather_end).
+void gather_begin(pgrt_ctx* ctx, FrameSet* fs, UnpackSrc& u) {
+    u = unpack_layout(fs->deal, fs->cam_w, fs->cam_h);
+    for (int j = 0; j < fs->K; ++j) PGRT_HIP(hipStreamWaitEvent(ctx->stream, fs->slots[j]->ev_done, 0));
+    PGRT_HIP(hipEventRecord(fs->ev_g0, ctx->stream));
+}
+
+void gather_post(pgrt_ctx* ctx, FrameSet* fs, UnpackSrc& u) {
     const TileDeal& d = fs->deal;
     const int F = fs->nframes;
     const size_t tile_floats = (size_t)kTile * kTile * 3;  // RGB tiles (out_mode 2)
-    UnpackSrc u = unpack_layout(d, W, H);
     const int me = ctx->rank;
-    bool unpack = me == 0;
-    PGRT_HIP(hipEventRecord(fs->ev_g0, ctx->stream));
     if (ctx->emulated) {
         // one GPU measures rank `me`: its tiles are copied to their place in a full-size buffer
         // (the other ranks' blocks stay unwritten), rank 0 also unpacks the whole frame
@@ -1110,38 +1166,55 @@ void gather_frame(pgrt_ctx* ctx, FrameSet* fs) {
         PGRT_HIP(hipMemcpyAsync(ctx->gathered.p + (size_t)F * u.prefix[me] * tile_floats, fs->tilebuf.p,
                                 sizeof(float) * F * u.count[me] * tile_floats, hipMemcpyDeviceToDevice, ctx->stream));
         for (int r = 0; r < d.world; ++r) u.src[r] = ctx->gathered.p + (size_t)F * u.prefix[r] * tile_floats;
-    } else if (d.world == 1) {
-        u.src[0] = fs->tilebuf.p;
-    } else {
-        PGRT_REQUIRE(ctx->comm, PGRT_ERR_RCCL, "pgrt_comm_init has not been called");
-        const size_t others = (size_t)F * (u.prefix[d.world] - u.count[0]) * tile_floats;
-        if (me == 0) ctx->gathered.alloc(std::max<size_t>(1, others));
-        // one group for all of the call's frames
-        auto ok = [](ncclResult_t r, const char* what) {
-            if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(r));
-        };
-        ok(ncclGroupStart(), "ncclGroupStart");
-        if (me == 0) {
-            for (int r = 1; r < d.world; ++r) {
-                float* dst = ctx->gathered.p + (size_t)F * (u.prefix[r] - u.count[0]) * tile_floats;
-                u.src[r] = dst;
-                if (u.count[r] > 0)
-                    ok(ncclRecv(dst, (size_t)F * u.count[r] * tile_floats, ncclFloat, r, ctx->comm, ctx->stream),
-                       "ncclRecv");
-            }
-            u.src[0] = fs->tilebuf.p;
-        } else if (u.count[me] > 0) {
-            ok(ncclSend(fs->tilebuf.p, (size_t)F * u.count[me] * tile_floats, ncclFloat, 0, ctx->comm, ctx->stream),
-               "ncclSend");
-        }
-        ok(ncclGroupEnd(), "ncclGroupEnd");
+        return;
     }
+    if (d.world == 1) {
+        u.src[0] = fs->tilebuf.p;
+        return;
+    }
+    PGRT_REQUIRE(ctx->comm, PGRT_ERR_RCCL, "pgrt_comm_init has not been called");
+    auto ok = [](ncclResult_t r, const char* what) {
+        if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(r));
+    };
+    if (me == 0) {
+        const size_t others = (size_t)F * (u.prefix[d.world] - u.count[0]) * tile_floats;
+        ctx->gathered.alloc(std::max<size_t>(1, others));
+        for (int r = 1; r < d.world; ++r) {
+            float* dst = ctx->gathered.p + (size_t)F * (u.prefix[r] - u.count[0]) * tile_floats;
+            u.src[r] = dst;
+            if (u.count[r] > 0)
+                ok(ncclRecv(dst, (size_t)F * u.count[r] * tile_floats, ncclFloat, r, ctx->comm, ctx->stream),
+                   "ncclRecv");
+        }
+        u.src[0] = fs->tilebuf.p;
+    } else if (u.count[me] > 0) {
+        ok(ncclSend(fs->tilebuf.p, (size_t)F * u.count[me] * tile_floats, ncclFloat, 0, ctx->comm, ctx->stream),
+           "ncclSend");
+    }
+}
+
+void gather_end(pgrt_ctx* ctx, FrameSet* fs, const UnpackSrc& u) {
     PGRT_HIP(hipEventRecord(fs->ev_g1, ctx->stream));
-    if (unpack)  // every frame of the call in one launch (grid.y = frame)
-        launch_unpack_tiles(u, fs->dist_fb, W, H, d, 3, ctx->stream, 0, F);
+    if (ctx->rank == 0)  // every frame of the call in one launch (grid.y = frame)
+        launch_unpack_tiles(u, fs->dist_fb, fs->cam_w, fs->cam_h, fs->deal, 3, ctx->stream, 0, fs->nframes);
     PGRT_HIP(hipEventRecord(fs->ev_g2, ctx->stream));
+    // the set's next frame overwrites its tile buffer only after the gather has read it
+    PGRT_HIP(hipEventRecord(fs->ev_ready, ctx->stream));
     fs->gather_timed = true;
     PGRT_HIP(hipGetLastError());
+}
+
+void gather_frame(pgrt_ctx* ctx, FrameSet* fs) {
+    UnpackSrc u;
+    gather_begin(ctx, fs, u);
+    auto ok = [](ncclResult_t r, const char* what) {
+        if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(r));
+    };
+    const bool group = !ctx->emulated && fs->deal.world > 1;
+    if (group) ok(ncclGroupStart(), "ncclGroupStart");  // one group for all of the call's frames
+    gather_post(ctx, fs, u);
+    if (group) ok(ncclGroupEnd(), "ncclGroupEnd");
+    gather_end(ctx, fs, u);
 }
 
 // device ms of a completed frame's gather (ncclGather incl. the wait for peers) + unpack
@@ -1157,9 +1230,7 @@ void gather_times(FrameSet* fs, pgrt_stats* st) {
 // complete a pending frame: collect, gather (distributed), release the set's buffers
 void finish_frame(pgrt_ctx* ctx, FrameSet* fs) {
     fs->pending = false;
-    fs->gather_timed = false;
-    collect_frame(ctx, fs);
-    if (fs->distributed) gather_frame(ctx, fs);
+    collect_frame(ctx, fs);  // a distributed frame's gather was queued at submission
     PGRT_HIP(hipEventRecord(fs->ev_ready, ctx->stream));
     fs->has_result = true;
     fs->stats.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - fs->t0).count();
@@ -1193,7 +1264,7 @@ void check_frame(const pgrt_ctx* ctx, const pgrt_render_params* p) {
 // the tiles land in fs->tilebuf and finish_frame gathers them into fb (rank 0).
 void start_frame(pgrt_ctx* ctx, FrameSet* fs, const pgrt_render_params* p, std::vector<int4> tiles, float* out,
                  int out_mode, int ox, int oy, int pitch, bool distributed, float* fb, int nframes = 1,
-                 long long frame_stride = 0, TileDeal deal = TileDeal{1, 1, 1}) {
+                 long long frame_stride = 0, TileDeal deal = TileDeal{1, 1, 1}, bool defer_gather = false) {
     check_frame(ctx, p);
     PGRT_REQUIRE(nframes >= 1 && nframes <= kMaxFramesPerCall, PGRT_ERR_INVALID_ARGUMENT,
                  "frames per call must be in [1, 64]");
@@ -1227,8 +1298,12 @@ void start_frame(pgrt_ctx* ctx, FrameSet* fs, const pgrt_render_params* p, std::
     fs->pitch = pitch;
     fs->has_result = false;
     fs->ticket = ctx->next_ticket++;
+    fs->gather_timed = false;
     enqueue_frame(ctx, fs);
     fs->pending = true;
+    // the gather follows the frame on the device (a multi-device context groups every rank's
+    // gather itself: defer_gather)
+    if (distributed && !defer_gather) gather_frame(ctx, fs);
 }
 
 // Synchronous render of `tiles` (pending asynchronous frames complete first).
@@ -1676,6 +1751,11 @@ int pgrt_comm_unique_id(char id[128]) {
 int pgrt_comm_init(pgrt_ctx* ctx, int world, int rank, const char id[128]) {
     if (!ctx || !id || world <= 0 || world > kMaxRanks || rank < 0 || rank >= world) return PGRT_ERR_INVALID_ARGUMENT;
     return guarded(ctx, [&] {
+        drain_frames(ctx);
+        if (ctx->comm_ctl) {
+            (void)ncclCommDestroy(ctx->comm_ctl);
+            ctx->comm_ctl = nullptr;
+        }
         if (ctx->comm) {
             (void)ncclCommDestroy(ctx->comm);
             ctx->comm = nullptr;
@@ -1687,6 +1767,9 @@ int pgrt_comm_init(pgrt_ctx* ctx, int world, int rank, const char id[128]) {
         std::memcpy(u.internal, id, 128);
         ncclResult_t r = ncclCommInitRank(&ctx->comm, world, u, rank);
         if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+        r = ncclCommSplit(ctx->comm, 0, rank, &ctx->comm_ctl, nullptr);
+        if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string("ncclCommSplit: ") + ncclGetErrorString(r));
+        if (!ctx->ctl_stream) PGRT_HIP(hipStreamCreateWithFlags(&ctx->ctl_stream, hipStreamNonBlocking));
     });
 }
 
@@ -1717,15 +1800,12 @@ int pgrt_render_distributed_device(pgrt_ctx* ctx, const pgrt_render_params* p, v
         start_frame(ctx, fs, p, rank_tiles(ctx->cam.width, ctx->cam.height, ctx->rank, deal), nullptr, 1, 0, 0, 0,
                     true, static_cast<float*>(rgba_device), 1, 0, deal);
         fs->pending = false;
-        collect_frame(ctx, fs);
-        auto tg = std::chrono::steady_clock::now();
-        gather_frame(ctx, fs);
+        collect_frame(ctx, fs);  // the gather is queued behind the frame (start_frame)
         PGRT_HIP(hipEventRecord(fs->ev_ready, ctx->stream));
         PGRT_HIP(hipStreamSynchronize(ctx->stream));
         fs->has_result = true;
-        auto t1 = std::chrono::steady_clock::now();
-        fs->stats.ms_gather = std::chrono::duration<double, std::milli>(t1 - tg).count();
-        fs->stats.ms_total = std::chrono::duration<double, std::milli>(t1 - fs->t0).count();
+        gather_times(fs, &fs->stats);
+        fs->stats.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - fs->t0).count();
         if (st) *st = fs->stats;
     });
 }

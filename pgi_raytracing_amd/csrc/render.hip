@@ -360,14 +360,14 @@ void launch_accumulate_frame(const float* frame, float* sum, float* mean, long l
 // A level traced as wave packets runs as fast as its slowest wave, and a wave whose 64 rays leave
 // the glass in different directions walks the union of their BVH paths (r2 measurement: skipping
 // waves that spread over > 90 degrees cut a one-frame level-1 launch from 507 to 129 us).  The
-// shade that emits the level's rays writes each ray's direction octant (Queue::key); here a
-// counting sort turns the keys into the order the traversal visits the rays in (perm), bin by
-// bin.  Per block-iteration a bin's rays keep their queue order (ballot + mbcnt ranks), so a wave
-// holds same-octant rays from a few neighbouring 8x8-pixel blocks.  The order of the blocks'
-// ranges inside a bin follows the atomics (not deterministic): it changes which rays share a
-// wave, never a hit (the closest hit of a ray does not depend on the traversal order).
-constexpr int kBinGridMax = 1024;  // grid-stride kernels: bounded atomics per bin
-
+// shade that emits the level's rays writes each ray's direction octant (Queue::key); a STABLE
+// counting sort turns the keys into the order the traversal visits the rays in (perm): bin by
+// bin, and inside a bin in queue order -- which is screen order (the shade appends children in
+// pixel-block order) -- so a wave holds same-octant rays (pairwise <= 90 degrees apart) from
+// neighbouring pixels.  Three passes over chunks of kBlock queue slots: per-chunk bin counts, one
+// block scanning them into per-chunk bin offsets, the scatter.  Deterministic.  (An unstable
+// version that reserved each chunk's range with atomics lost the screen order inside a bin and
+// was slower than no binning, r3b.)
 __device__ __forceinline__ void wave_bin_counts(bool active, unsigned key, unsigned& my_rank, unsigned* wcnt) {
     my_rank = 0;
 #pragma unroll
@@ -378,57 +378,92 @@ __device__ __forceinline__ void wave_bin_counts(bool active, unsigned key, unsig
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_bin_hist(const unsigned char* __restrict__ keys, FrameCounters* fc,
-                                                     int level, int cap) {
+__global__ __launch_bounds__(kBlock) void k_bin_count(const unsigned char* __restrict__ keys, const FrameCounters* fc,
+                                                      int level, int cap, unsigned* __restrict__ chunk_cnt) {
     __shared__ unsigned wcnt[kBlock / 64][kBins];
-    __shared__ unsigned tot[kBins];
     const int n = min(fc_count(*fc, level), cap);
     const int w = threadIdx.x >> 6;
-    if (threadIdx.x < kBins) tot[threadIdx.x] = 0;
-    __syncthreads();
-    for (int base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-        const int i = base + threadIdx.x;
+    for (int c = blockIdx.x; c * kBlock < n; c += gridDim.x) {
+        const int i = c * kBlock + threadIdx.x;
         const bool active = i < n;
         unsigned rank;
         wave_bin_counts(active, active ? keys[i] : 0u, rank, wcnt[w]);
         __syncthreads();
-        if (threadIdx.x < kBins)
-            for (int k = 0; k < kBlock / 64; ++k) tot[threadIdx.x] += wcnt[k][threadIdx.x];
+        if (threadIdx.x < kBins) {
+            unsigned t = 0;
+            for (int k = 0; k < kBlock / 64; ++k) t += wcnt[k][threadIdx.x];
+            chunk_cnt[(size_t)c * kBins + threadIdx.x] = t;
+        }
         __syncthreads();
     }
-    if (threadIdx.x < kBins && tot[threadIdx.x]) atomicAdd(&fc->bins[level][threadIdx.x], tot[threadIdx.x]);
 }
 
-__global__ __launch_bounds__(kBlock) void k_bin_scatter(const unsigned char* __restrict__ keys, FrameCounters* fc,
-                                                        int level, int cap, int* __restrict__ perm) {
-    __shared__ unsigned wcnt[kBlock / 64][kBins];
-    __shared__ unsigned start[kBins];  // this block-iteration's first slot per bin
-    __shared__ unsigned first[kBins];  // exclusive prefix of the bin sizes
+// one block: per-chunk counts -> per-chunk first slot of each bin (bins in order, chunks in order
+// inside a bin); the bin sizes go to FrameCounters::bins (statistics)
+constexpr int kBinScanBlock = 1024;
+__global__ __launch_bounds__(kBinScanBlock) void k_bin_scan(FrameCounters* fc, int level, int cap,
+                                                            unsigned* __restrict__ chunk_cnt) {
+    __shared__ unsigned part[kBinScanBlock][kBins + 1];  // +1: no bank conflicts on the column walk
+    __shared__ unsigned bin_first[kBins];
     const int n = min(fc_count(*fc, level), cap);
-    const int w = threadIdx.x >> 6;
-    unsigned* bins = fc->bins[level];
+    const int nchunks = (n + kBlock - 1) / kBlock;
+    const int per = (nchunks + kBinScanBlock - 1) / kBinScanBlock;  // chunks per thread, contiguous
+    const int c0 = threadIdx.x * per, c1 = min(nchunks, c0 + per);
+    unsigned t[kBins];
+#pragma unroll
+    for (int b = 0; b < kBins; ++b) t[b] = 0;
+    for (int c = c0; c < c1; ++c)
+#pragma unroll
+        for (int b = 0; b < kBins; ++b) t[b] += chunk_cnt[(size_t)c * kBins + b];
+#pragma unroll
+    for (int b = 0; b < kBins; ++b) part[threadIdx.x][b] = t[b];
+    __syncthreads();
+    if (threadIdx.x < kBins) {  // exclusive scan of bin b over the threads (column walk)
+        const int b = threadIdx.x;
+        unsigned acc = 0;
+        for (int k = 0; k < kBinScanBlock; ++k) {
+            const unsigned v = part[k][b];
+            part[k][b] = acc;
+            acc += v;
+        }
+        fc->bins[level][b] = acc;  // bin size
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
         unsigned acc = 0;
         for (int b = 0; b < kBins; ++b) {
-            first[b] = acc;
-            acc += bins[b];
+            bin_first[b] = acc;
+            acc += fc->bins[level][b];
         }
     }
-    for (int base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-        const int i = base + threadIdx.x;
+    __syncthreads();
+    unsigned o[kBins];
+#pragma unroll
+    for (int b = 0; b < kBins; ++b) o[b] = bin_first[b] + part[threadIdx.x][b];
+    for (int c = c0; c < c1; ++c)
+#pragma unroll
+        for (int b = 0; b < kBins; ++b) {
+            const unsigned v = chunk_cnt[(size_t)c * kBins + b];
+            chunk_cnt[(size_t)c * kBins + b] = o[b];  // in place: counts -> first slots
+            o[b] += v;
+        }
+}
+
+__global__ __launch_bounds__(kBlock) void k_bin_scatter(const unsigned char* __restrict__ keys, const FrameCounters* fc,
+                                                        int level, int cap, const unsigned* __restrict__ chunk_first,
+                                                        int* __restrict__ perm) {
+    __shared__ unsigned wcnt[kBlock / 64][kBins];
+    const int n = min(fc_count(*fc, level), cap);
+    const int w = threadIdx.x >> 6;
+    for (int c = blockIdx.x; c * kBlock < n; c += gridDim.x) {
+        const int i = c * kBlock + threadIdx.x;
         const bool active = i < n;
         const unsigned key = active ? keys[i] : 0u;
         unsigned rank;
         wave_bin_counts(active, key, rank, wcnt[w]);
         __syncthreads();
-        if (threadIdx.x < kBins) {
-            unsigned c = 0;
-            for (int k = 0; k < kBlock / 64; ++k) c += wcnt[k][threadIdx.x];
-            start[threadIdx.x] = first[threadIdx.x] + (c ? atomicAdd(&bins[kBins + threadIdx.x], c) : 0u);
-        }
-        __syncthreads();
         if (active) {
-            unsigned pos = start[key] + rank;
+            unsigned pos = chunk_first[(size_t)c * kBins + key] + rank;
             for (int k = 0; k < w; ++k) pos += wcnt[k][key];
             perm[pos] = i;
         }
@@ -436,12 +471,13 @@ __global__ __launch_bounds__(kBlock) void k_bin_scatter(const unsigned char* __r
     }
 }
 
-void launch_bin_rays(const unsigned char* keys, FrameCounters* fc, int level, int cap, int* perm, int expect,
-                     hipStream_t stream) {
+void launch_bin_rays(const unsigned char* keys, FrameCounters* fc, int level, int cap, int* perm, unsigned* chunk_buf,
+                     int expect, hipStream_t stream) {
     if (cap <= 0) return;
-    const int grid = std::min(kBinGridMax, grid_for(cap, expect));
-    hipLaunchKernelGGL(k_bin_hist, dim3(grid), dim3(kBlock), 0, stream, keys, fc, level, cap);
-    hipLaunchKernelGGL(k_bin_scatter, dim3(grid), dim3(kBlock), 0, stream, keys, fc, level, cap, perm);
+    const int grid = grid_for(cap, expect);
+    hipLaunchKernelGGL(k_bin_count, dim3(grid), dim3(kBlock), 0, stream, keys, fc, level, cap, chunk_buf);
+    hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(kBinScanBlock), 0, stream, fc, level, cap, chunk_buf);
+    hipLaunchKernelGGL(k_bin_scatter, dim3(grid), dim3(kBlock), 0, stream, keys, fc, level, cap, chunk_buf, perm);
 }
 
 // ------------------------------------------------------------------ counter export

@@ -39,8 +39,8 @@ struct FrameCounters {
     // profile == 2: per level, shaded rays that hit a triangle and, of those, the ones whose
     // Phong branch sampled a texture (the whole-frame roofline's attribute / texel bytes)
     alignas(128) unsigned long long shade[kMaxLevels][2];
-    // ray binning per level: bin sizes [0, kBins), then the scatter's cursors [kBins, 2 kBins)
-    alignas(128) unsigned bins[kMaxLevels][2 * kBins];
+    // ray binning per level: bin sizes (statistics)
+    alignas(128) unsigned bins[kMaxLevels][kBins];
 };
 
 __host__ __device__ inline int fc_count(const FrameCounters& f, int L) {
@@ -201,10 +201,10 @@ void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles,
 // frame sink: sum += frame (count-th frame; count == 1 resets), mean = sum / count
 void launch_accumulate_frame(const float* frame, float* sum, float* mean, long long pixels, int count,
                              hipStream_t stream);
-// ray binning of level `level` (FrameCounters::bins): histogram of the keys, then the scatter of
-// the ray indices into perm, bin by bin (expect sizes the grids)
-void launch_bin_rays(const unsigned char* keys, FrameCounters* fc, int level, int cap, int* perm, int expect,
-                     hipStream_t stream);
+// stable ray binning of level `level`: per-chunk bin counts (chunk_buf: kBins words per 256 queue
+// slots), their scan, the scatter of the ray indices into perm, bin by bin (expect sizes the grids)
+void launch_bin_rays(const unsigned char* keys, FrameCounters* fc, int level, int cap, int* perm, unsigned* chunk_buf,
+                     int expect, hipStream_t stream);
 // copy `n` FrameCounters to pinned host memory and zero them on the device
 void launch_export_counters(FrameCounters* dev, FrameCounters* host, int n, hipStream_t stream);
 // Distributed frames: rank r's tile-compact buffer (frame-major, count[r] tiles per frame in its
