@@ -191,9 +191,10 @@ typedef struct pgrt_config {
     int rank0_share_a, rank0_share_b; /* distributed frames: rank 0 renders a tiles for every b of
                                          another rank (1..64 each; 0 = the default deal of
                                          pgrt_tile_share; pgrt_tune_distribution sets them) */
-    int ray_binning;      /* 0 = default: the rays of every bounce level traced as wave packets are
-                             visited in direction-octant bins (a counting sort by the octant the
-                             shade records, keeping screen order inside a bin); -1 = off */
+    int ray_binning;      /* 1: the rays of every bounce level traced as wave packets are visited
+                             in direction-octant bins (a counting sort by the octant the shade
+                             records, keeping screen order inside a bin); 0 / -1 = off (default:
+                             no gain on C2, profiles/r3/ab_r3c_binning.txt) */
     int reserved[2];
 } pgrt_config;
 

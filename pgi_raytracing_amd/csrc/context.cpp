@@ -651,7 +651,7 @@ bool packet_level(const pgrt_ctx* ctx, int L) {
 
 // is level L >= 1 binned by direction octant before its packet traversal (pgrt_config.ray_binning)
 bool binned_level(const pgrt_ctx* ctx, const SceneView& view, int L) {
-    return L >= 1 && ctx->cfg.ray_binning == 0 && packet_level(ctx, L) && trace_packets_available(view);
+    return L >= 1 && ctx->cfg.ray_binning == 1 && packet_level(ctx, L) && trace_packets_available(view);
 }
 
 // PGRT_PACKETS_AUTO: a level stays on wave packets while its rays use at least this fraction of
@@ -1429,8 +1429,8 @@ int pgrt_set_config(pgrt_ctx* ctx, const pgrt_config* cfg) {
         PGRT_REQUIRE(cfg->max_batch_rays >= 0 && cfg->max_batch_rays <= (1ll << 29), PGRT_ERR_INVALID_ARGUMENT,
                      "max_batch_rays must be in [0, 2^29]");
         PGRT_REQUIRE(cfg->max_batches_in_flight >= 0, PGRT_ERR_INVALID_ARGUMENT, "max_batches_in_flight must be >= 0");
-        PGRT_REQUIRE(cfg->ray_binning == 0 || cfg->ray_binning == -1, PGRT_ERR_INVALID_ARGUMENT,
-                     "ray_binning must be 0 (default) or -1 (off)");
+        PGRT_REQUIRE(cfg->ray_binning >= -1 && cfg->ray_binning <= 1, PGRT_ERR_INVALID_ARGUMENT,
+                     "ray_binning must be 0 / -1 (off, the default) or 1 (on)");
         PGRT_REQUIRE(cfg->rank0_share_a >= 0 && cfg->rank0_share_a <= 64 && cfg->rank0_share_b >= 0 &&
                          cfg->rank0_share_b <= 64,
                      PGRT_ERR_INVALID_ARGUMENT, "rank0_share_a / rank0_share_b must be in [0, 64]");

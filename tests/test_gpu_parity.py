@@ -263,13 +263,15 @@ def test_bvh_layouts_bit_exact(gpu_ctx, avenger_scene, builder, width, split, gr
         gpu_ctx.set_scene(avenger_scene)
 
 
-@pytest.mark.parametrize("packets", [abi.PGRT_PACKETS_OFF, 1, abi.PGRT_PACKETS_AUTO, 16])
-def test_packet_levels_bit_exact(gpu_ctx, avenger_scene, packets):
+@pytest.mark.parametrize("packets,binning", [(abi.PGRT_PACKETS_OFF, 0), (1, 0), (abi.PGRT_PACKETS_AUTO, 0), (16, 0),
+                                             (abi.PGRT_PACKETS_AUTO, 1), (16, 1)])
+def test_packet_levels_bit_exact(gpu_ctx, avenger_scene, packets, binning):
     """Every packet-traversal depth (none: k_raygen + one lane per ray; level 0 only, which
-    generates its rays in the traversal; the default; every level) renders the oracle's frame
-    bit for bit, frames in flight and batched frames included."""
+    generates its rays in the traversal; the default; every level), with and without the
+    direction-octant binning of the packet-traced bounce levels (ray_binning 1), renders the
+    oracle's frame bit for bit, frames in flight and batched frames included."""
     gpu_ctx.set_scene(avenger_scene)
-    old = gpu_ctx.configure(packet_levels=packets)
+    old = gpu_ctx.configure(packet_levels=packets, ray_binning=binning)
     try:
         W, H = 96, 64
         cam = abi.default_camera(W, H)
