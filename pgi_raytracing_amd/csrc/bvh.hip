@@ -146,14 +146,12 @@ __global__ __launch_bounds__(kB) void k_gather_tris(const float* __restrict__ po
 __device__ __forceinline__ void write_slot(BvhNode* nd, int slot, const float* lo, const float* hi) {
     if (slot == 0) {
         nd->a = make_float4(lo[0], hi[0], lo[1], hi[1]);
-        float* c = reinterpret_cast<float*>(&nd->c);
-        c[0] = lo[2];
-        c[1] = hi[2];
+        nd->c.x = lo[2];
+        nd->c.y = hi[2];
     } else {
         nd->b = make_float4(lo[0], hi[0], lo[1], hi[1]);
-        float* c = reinterpret_cast<float*>(&nd->c);
-        c[2] = lo[2];
-        c[3] = hi[2];
+        nd->c.z = lo[2];
+        nd->c.w = hi[2];
     }
 }
 

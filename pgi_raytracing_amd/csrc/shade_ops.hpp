@@ -66,44 +66,76 @@ __device__ __forceinline__ V3 tex_pixel(const DevTexture& t, const unsigned char
     return v3(lut[p[0]], lut[p[1]], lut[p[2]]);
 }
 
-// Two horizontally adjacent texels whose bytes start at offset off (both in bounds): the bytes
-// off .. off + 7 from three aligned dwords (v_alignbyte_b32 funnel shifts), the same values as
-// two tex_pixel calls.  Reads up to 12 bytes past off & ~3: set_scene pads the texel pool for it.
-__device__ __forceinline__ void tex_row_pair(const DevTexture& t, const unsigned char* pool, const float* lut,
-                                             long long off, V3& a, V3& b) {
-    const unsigned char* p = pool + t.offset + off;
-    const unsigned k = (unsigned)((uintptr_t)p & 3u);
-    const unsigned* w = reinterpret_cast<const unsigned*>((uintptr_t)p & ~(uintptr_t)3);
-    const unsigned w0 = w[0], w1 = w[1], w2 = w[2];
-    const unsigned lo = __builtin_amdgcn_alignbyte(w1, w0, k);  // bytes off .. off + 3
-    const unsigned hi = __builtin_amdgcn_alignbyte(w2, w1, k);  // bytes off + 4 .. off + 7
+// Texture::get_texel (APP/texture.cpp:77-130): bilinear with the reference's edge quirks, in two
+// halves so a kernel can issue a texel fetch, do other work (another ray's loads) and consume it
+// later: tex_fetch computes the taps and issues the loads of the usual case, tex_finish waits for
+// them and interpolates.  tex_texel == tex_finish(tex_fetch(...)).
+struct TexTap {
+    float x, y;
+    int x1, x2, y1, y2;
+    int mode;             // 0: black (edge quirk / non-finite); 1: row windows loaded; 2: edge taps
+    unsigned w1[3], w2[3];  // the two rows' aligned 12-byte windows (mode 1)
+    unsigned k1, k2;        // byte shift of each window
+};
+__device__ __forceinline__ TexTap tex_fetch(const DevTexture& t, const unsigned char* pool, float u, float v) {
+    TexTap q;
+    q.x = u * (float)t.width;
+    q.y = v * (float)t.height;
+    q.mode = 0;
+    q.x1 = q.x2 = q.y1 = q.y2 = 0;
+    q.k1 = q.k2 = 0;
+    if (!(fabsf(q.x) < 16777216.0f) || !(fabsf(q.y) < 16777216.0f)) return q;
+    const int tmp_x1 = (int)floorf(q.x), tmp_x2 = (int)ceilf(q.x);
+    const int tmp_y1 = (int)floorf(q.y), tmp_y2 = (int)ceilf(q.y);
+    q.x1 = (tmp_x1 < 1) ? tmp_x1 + 1 : tmp_x1;
+    q.x2 = (tmp_x2 == t.width) ? 0 : tmp_x2;
+    q.y1 = (tmp_y1 < 1) ? tmp_y1 + 1 : tmp_y1;
+    q.y2 = (tmp_y2 == t.height) ? tmp_y1 : tmp_y2;
+    if (q.x1 == q.x2 || q.y1 == q.y2) return q;
+    const long long o1 = (long long)q.y1 * t.pitch + (long long)q.x1 * t.bpp;
+    const long long o2 = (long long)q.y2 * t.pitch + (long long)q.x1 * t.bpp;
+    if (q.x2 == q.x1 + 1 && t.bpp <= 4 && o1 >= 0 && o2 >= 0 && o1 + t.bpp + 2 < t.size && o2 + t.bpp + 2 < t.size) {
+        // the usual case: both taps of a row are neighbours inside the texture -> one aligned
+        // 12-byte window per row (the texel pool is padded for it) instead of 6 byte loads
+        const unsigned char* p1 = pool + t.offset + o1;
+        const unsigned char* p2 = pool + t.offset + o2;
+        q.k1 = (unsigned)((uintptr_t)p1 & 3u);
+        q.k2 = (unsigned)((uintptr_t)p2 & 3u);
+        const unsigned* a = reinterpret_cast<const unsigned*>((uintptr_t)p1 & ~(uintptr_t)3);
+        const unsigned* b = reinterpret_cast<const unsigned*>((uintptr_t)p2 & ~(uintptr_t)3);
+        q.w1[0] = a[0];
+        q.w1[1] = a[1];
+        q.w1[2] = a[2];
+        q.w2[0] = b[0];
+        q.w2[1] = b[1];
+        q.w2[2] = b[2];
+        q.mode = 1;
+    } else {
+        q.mode = 2;
+    }
+    return q;
+}
+// the two horizontally adjacent texels of a row window: bytes off .. off + 7 out of three aligned
+// dwords by v_alignbyte_b32 funnel shifts (set_scene pads the texel pool for the 12-byte read)
+__device__ __forceinline__ void tex_window_pair(int bpp, const float* lut, const unsigned* w, unsigned k, V3& a,
+                                                V3& b) {
+    const unsigned lo = __builtin_amdgcn_alignbyte(w[1], w[0], k);  // bytes off .. off + 3
+    const unsigned hi = __builtin_amdgcn_alignbyte(w[2], w[1], k);  // bytes off + 4 .. off + 7
     a = v3(lut[lo & 0xffu], lut[(lo >> 8) & 0xffu], lut[(lo >> 16) & 0xffu]);
-    if (t.bpp == 3)
+    if (bpp == 3)
         b = v3(lut[lo >> 24], lut[hi & 0xffu], lut[(hi >> 8) & 0xffu]);
     else
         b = v3(lut[hi & 0xffu], lut[(hi >> 8) & 0xffu], lut[(hi >> 16) & 0xffu]);
 }
-
-// Texture::get_texel (APP/texture.cpp:77-130): bilinear with the reference's edge quirks.
-__device__ inline V3 tex_texel(const DevTexture& t, const unsigned char* pool, const float* lut, float u, float v) {
-    const float x = u * (float)t.width;
-    const float y = v * (float)t.height;
-    if (!(fabsf(x) < 16777216.0f) || !(fabsf(y) < 16777216.0f)) return v3(0, 0, 0);
-    const int tmp_x1 = (int)floorf(x), tmp_x2 = (int)ceilf(x);
-    const int tmp_y1 = (int)floorf(y), tmp_y2 = (int)ceilf(y);
-    const int x1 = (tmp_x1 < 1) ? tmp_x1 + 1 : tmp_x1;
-    const int x2 = (tmp_x2 == t.width) ? 0 : tmp_x2;
-    const int y1 = (tmp_y1 < 1) ? tmp_y1 + 1 : tmp_y1;
-    const int y2 = (tmp_y2 == t.height) ? tmp_y1 : tmp_y2;
-    if (x1 == x2 || y1 == y2) return v3(0, 0, 0);
+__device__ __forceinline__ V3 tex_finish(const TexTap& q, const DevTexture& t, const unsigned char* pool,
+                                         const float* lut) {
+    if (q.mode == 0) return v3(0, 0, 0);
+    const float x = q.x, y = q.y;
+    const int x1 = q.x1, x2 = q.x2, y1 = q.y1, y2 = q.y2;
     V3 x1y1, x2y1, x1y2, x2y2;
-    const long long o1 = (long long)y1 * t.pitch + (long long)x1 * t.bpp;
-    const long long o2 = (long long)y2 * t.pitch + (long long)x1 * t.bpp;
-    if (x2 == x1 + 1 && t.bpp <= 4 && o1 >= 0 && o2 >= 0 && o1 + t.bpp + 2 < t.size && o2 + t.bpp + 2 < t.size) {
-        // the usual case: both taps of a row are neighbours inside the texture -> one aligned
-        // 12-byte window per row (the texel pool is padded for it) instead of 6 byte loads
-        tex_row_pair(t, pool, lut, o1, x1y1, x2y1);
-        tex_row_pair(t, pool, lut, o2, x1y2, x2y2);
+    if (q.mode == 1) {
+        tex_window_pair(t.bpp, lut, q.w1, q.k1, x1y1, x2y1);
+        tex_window_pair(t.bpp, lut, q.w2, q.k2, x1y2, x2y2);
     } else {
         x1y1 = tex_pixel(t, pool, lut, x1, y1);
         x2y1 = tex_pixel(t, pool, lut, x2, y1);
@@ -121,6 +153,9 @@ __device__ inline V3 tex_texel(const DevTexture& t, const unsigned char* pool, c
     const float wy2 = dy == 1.0f ? (float)y2 - y : ((float)y2 - y) / dy;
     const float wy1 = dy == 1.0f ? y - (float)y1 : (y - (float)y1) / dy;
     return v3(f1.x * wy2 + f2.x * wy1, f1.y * wy2 + f2.y * wy1, f1.z * wy2 + f2.z * wy1);
+}
+__device__ inline V3 tex_texel(const DevTexture& t, const unsigned char* pool, const float* lut, float u, float v) {
+    return tex_finish(tex_fetch(t, pool, u, v), t, pool, lut);
 }
 
 // ---- env-map angles, fast and still bit-identical to pg_atan2f / pg_asinf ----
@@ -182,14 +217,26 @@ __device__ inline float asinf_env(float x) {  // == pg_asinf(x)
     return f == f ? f : pg_asinf(x);
 }
 
-// SphericalMap::get_texel (APP/SphericalMap.cpp:17-29): returns RGBA with a = 1.
-__device__ inline float4 env_texel(const SceneView& s, const float* lut, V3 d) {
-    if (s.env < 0) return make_float4(0, 0, 0, 1);
+// SphericalMap::get_texel (APP/SphericalMap.cpp:17-29): returns RGBA with a = 1.  env_fetch /
+// env_finish split it like tex_fetch / tex_finish (env_texel == env_finish(env_fetch(...))).
+__device__ __forceinline__ TexTap env_fetch(const SceneView& s, V3 d) {
+    if (s.env < 0) {
+        TexTap q;
+        q.mode = 0;
+        return q;
+    }
     const V3 vec = normalize(v3(d.x, d.z, d.y));
     const float u = (float)(0.5 + (double)atan2f_env(vec.x, vec.z) / (2 * 3.14159265358979323846));
     const float v = (float)(0.5 - (double)asinf_env(vec.y) / 3.14159265358979323846);
-    const V3 c = tex_texel(s.tex[s.env], s.texels, lut, u, v);
+    return tex_fetch(s.tex[s.env], s.texels, u, v);
+}
+__device__ __forceinline__ float4 env_finish(const SceneView& s, const float* lut, const TexTap& q) {
+    if (s.env < 0) return make_float4(0, 0, 0, 1);
+    const V3 c = tex_finish(q, s.tex[s.env], s.texels, lut);
     return make_float4(c.z, c.y, c.x, 1.0f);
+}
+__device__ inline float4 env_texel(const SceneView& s, const float* lut, V3 d) {
+    return env_finish(s, lut, env_fetch(s, d));
 }
 
 // utils.cpp:204-241

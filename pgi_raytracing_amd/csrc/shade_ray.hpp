@@ -13,11 +13,8 @@
 
 namespace pgrt {
 
-// child order in the next level's queue: 2 = per block (256 parents), its reflections then its
-// refractions; 1 = the same per wave; 0 = interleaved
-#ifndef PGRT_CHILD_SPLIT
-#define PGRT_CHILD_SPLIT 2
-#endif
+// child order in the next level's queue: per block (256 parents), its reflections then its
+// refractions (r2k A/B: per wave, or interleaved, was slower)
 
 // shading tables in LDS when they fit (the hit -> attributes -> material -> texture chain has one
 // global round trip fewer per hop)
@@ -51,29 +48,35 @@ struct ShadeOut {
     float m_d_r, m_d_g, m_d_b;
 };
 
-// the hit triangle's 16 shading floats (n0 n1 n2 uv0 uv1 uv2 material), 4 x 16 B
+// the hit triangle's 16 shading floats (n0 n1 n2 uv0 uv1 uv2 material), fetched as 4 x 16 B and
+// kept as plain floats (reading a float4 array through a float pointer is type punning: with
+// TBAA the optimiser may order those float reads before the float4 stores that fill the array)
 struct HitAttr {
-    float4 q[4];
+    float f[16];
 };
 __device__ __forceinline__ HitAttr load_attr(const SceneView& s, float4 h) {
     HitAttr a;
     const int prim = __float_as_int(h.w);
+    float4 q0 = make_float4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0;
     if (prim >= 0) {
         const float4* p = reinterpret_cast<const float4*>(s.attr + 16 * (size_t)prim);
-        a.q[0] = p[0];
-        a.q[1] = p[1];
-        a.q[2] = p[2];
-        a.q[3] = p[3];
-    } else {
-        a.q[0] = a.q[1] = a.q[2] = a.q[3] = make_float4(0, 0, 0, 0);
+        q0 = p[0];
+        q1 = p[1];
+        q2 = p[2];
+        q3 = p[3];
+    }
+    const float4 q[4] = {q0, q1, q2, q3};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        a.f[4 * k] = q[k].x;
+        a.f[4 * k + 1] = q[k].y;
+        a.f[4 * k + 2] = q[k].z;
+        a.f[4 * k + 3] = q[k].w;
     }
     return a;
 }
 
-// Phase 1 for one ray (o4 = org|tnear, d4 = dir|tfar, rtime = medium IOR, h = t|u|v|prim).
-__device__ __forceinline__ void shade_eval(const SceneView& s, const DevMaterial* mats, const float* lut,
-                                           int level, int max_level, bool active, float4 o4, float4 d4,
-                                           float rtime, float4 h, ShadeOut& r) {
+__device__ __forceinline__ void shade_init(ShadeOut& r) {
     r.kind = 0;
     r.color = make_float4(0, 0, 0, 1);
     r.nshadow = 0;
@@ -83,6 +86,101 @@ __device__ __forceinline__ void shade_eval(const SceneView& s, const DevMaterial
     r.att = make_float4(0, 0, 0, 0);
     r.m_d_r = r.m_d_g = r.m_d_b = 0;
     r.mid = 0;
+}
+
+// Phase 1, hit part: the ray (r.org, r.dirraw set; d = normalize(r.dirraw)) hit triangle h.w,
+// whose shading attributes are ha (raytracer.cpp:246-386 up to the emitted rays).
+__device__ __forceinline__ void shade_hit(const SceneView& s, const DevMaterial* mats, const float* lut, int level,
+                                          int max_level, V3 d, float rtime, float4 h, const HitAttr& ha,
+                                          ShadeOut& r) {
+    // every ShadeOut field is written whole, once, at the end of its branch: partial stores of a
+    // member in some branches only (r.att.w, r.color) let the optimiser merge them into one store
+    // through a phi of addresses, which kept ShadeOut in scratch memory (measured: wrong pixels)
+    const float t = h.x;
+    const float* a = ha.f;
+    const float u = h.y, v = h.z;
+    V3 nn = v3(interp1(a[0], a[3], a[6], u, v), interp1(a[1], a[4], a[7], u, v), interp1(a[2], a[5], a[8], u, v));
+    const int mid = __float_as_int(a[15]);
+    const DevMaterial& m = mats[mid];
+    nn = normalize(nn);
+    const V3 hitp = r.org + scale(t, r.dirraw);
+    float n1, n2;
+    if (rtime == PGRT_IOR_AIR) {
+        n1 = PGRT_IOR_AIR;
+        n2 = m.ior;
+    } else {
+        n1 = m.ior;
+        n2 = PGRT_IOR_AIR;
+    }
+    if (dot(nn, d) > 0) nn = -nn;
+    r.mid = mid;
+    r.hitp = hitp;
+    r.n1 = n1;
+    r.n2 = n2;
+    r.nrm = nn;
+    if (level >= max_level) return;  // r.color (0, 0, 0, 1): raytracer.cpp:282-283
+    if (m.type == PGRT_MATERIAL_DIELECTRIC) {
+        V3 refl, refr;
+        {  // get_reflection_ray (raytracer.cpp:209-235)
+            const V3 dd = normalize(d), rn = normalize(nn);
+            refl = dd - scale(2, scale(dot(dd, rn), rn));
+        }
+        const float ax = pg_expf(-(1 - m.kd[0]) * t);  // raytracer.cpp:303-305
+        const float ay = pg_expf(-(1 - m.kd[1]) * t);
+        const float az = pg_expf(-(1 - m.kd[2]) * t);
+        {  // get_refraction_ray (raytracer.cpp:178-207)
+            const V3 dd = normalize(d), rn = normalize(nn);
+            const float n1_n2 = n1 / n2;
+            const float d_n = dot(dd, rn);
+            const V3 sd = v3(dd.x * n1_n2, dd.y * n1_n2, dd.z * n1_n2);
+            const float kk = n1_n2 * d_n + sqrtf(1 - ((n1_n2 * n1_n2) * (1 - (d_n * d_n))));
+            refr = sd - scale(kk, rn);
+        }
+        int nchild = 1;
+        float R = 0.0f;
+        if (refr.x == refr.x) {  // no total internal reflection
+            nchild = 2;
+            const float cos1 = fabsf(dot(nn, -d));
+            const float alpha = (n1 - n2) / (n1 + n2);
+            R = (float)((double)(alpha * alpha + (1 - (alpha * alpha))) * pg_pow_d((double)(1 - cos1), 5.0));
+        }
+        r.kind = 1;
+        r.nchild = nchild;
+        r.refl_dir = refl;
+        r.refr_dir = refr;
+        r.att = make_float4(ax, ay, az, R);
+    } else {
+        float mr, mg, mb;
+        if (m.tex < 0) {
+            mr = m.kd[2];
+            mg = m.kd[1];
+            mb = m.kd[0];
+        } else {
+            const float tu = interp1(a[9], a[11], a[13], u, v);
+            const float tv = interp1(a[10], a[12], a[14], u, v);
+            const V3 tx = tex_texel(s.tex[m.tex], s.texels, lut, tu, 1.0f - tv);
+            mr = tx.x;
+            mg = tx.y;
+            mb = tx.z;
+        }
+        int nshadow = 0;
+        for (int li = 0; li < s.nlight; ++li) {
+            const DevLight& L = s.lights[li];
+            if (!(dot(nn, v3(L.pos[0], L.pos[1], L.pos[2])) < 0)) ++nshadow;
+        }
+        r.kind = 2;
+        r.m_d_r = mr;
+        r.m_d_g = mg;
+        r.m_d_b = mb;
+        r.nshadow = nshadow;
+    }
+}
+
+// Phase 1 for one ray (o4 = org|tnear, d4 = dir|tfar, rtime = medium IOR, h = t|u|v|prim).
+__device__ __forceinline__ void shade_eval(const SceneView& s, const DevMaterial* mats, const float* lut,
+                                           int level, int max_level, bool active, float4 o4, float4 d4,
+                                           float rtime, float4 h, ShadeOut& r) {
+    shade_init(r);
     if (!active) return;
     r.org = v3(o4.x, o4.y, o4.z);
     r.dirraw = v3(d4.x, d4.y, d4.z);
@@ -96,77 +194,14 @@ __device__ __forceinline__ void shade_eval(const SceneView& s, const DevMaterial
         r.color = env_texel(s, lut, d);  // miss (raytracer.cpp:390-393)
         return;
     }
-    const float t = h.x;
-    const HitAttr ha = load_attr(s, h);
-    const float* a = reinterpret_cast<const float*>(ha.q);
-    const float u = h.y, v = h.z;
-    V3 nn = v3(interp1(a[0], a[3], a[6], u, v), interp1(a[1], a[4], a[7], u, v), interp1(a[2], a[5], a[8], u, v));
-    r.mid = __float_as_int(a[15]);
-    const DevMaterial& m = mats[r.mid];
-    nn = normalize(nn);
-    r.hitp = r.org + scale(t, r.dirraw);
-    if (rtime == PGRT_IOR_AIR) {
-        r.n1 = PGRT_IOR_AIR;
-        r.n2 = m.ior;
-    } else {
-        r.n1 = m.ior;
-        r.n2 = PGRT_IOR_AIR;
-    }
-    if (dot(nn, d) > 0) nn = -nn;
-    r.nrm = nn;
-    if (level >= max_level) {
-        r.color = make_float4(0, 0, 0, 1);  // raytracer.cpp:282-283
-    } else if (m.type == PGRT_MATERIAL_DIELECTRIC) {
-        r.kind = 1;
-        {  // get_reflection_ray (raytracer.cpp:209-235)
-            const V3 dd = normalize(d), rn = normalize(nn);
-            r.refl_dir = dd - scale(2, scale(dot(dd, rn), rn));
-        }
-        r.att.x = pg_expf(-(1 - m.kd[0]) * t);  // raytracer.cpp:303-305
-        r.att.y = pg_expf(-(1 - m.kd[1]) * t);
-        r.att.z = pg_expf(-(1 - m.kd[2]) * t);
-        {  // get_refraction_ray (raytracer.cpp:178-207)
-            const V3 dd = normalize(d), rn = normalize(nn);
-            const float n1_n2 = r.n1 / r.n2;
-            const float d_n = dot(dd, rn);
-            const V3 sd = v3(dd.x * n1_n2, dd.y * n1_n2, dd.z * n1_n2);
-            const float kk = n1_n2 * d_n + sqrtf(1 - ((n1_n2 * n1_n2) * (1 - (d_n * d_n))));
-            r.refr_dir = sd - scale(kk, rn);
-        }
-        r.nchild = 1;
-        if (r.refr_dir.x == r.refr_dir.x) {  // no total internal reflection
-            r.nchild = 2;
-            const float cos1 = fabsf(dot(nn, -d));
-            const float alpha = (r.n1 - r.n2) / (r.n1 + r.n2);
-            r.att.w = (float)((double)(alpha * alpha + (1 - (alpha * alpha))) * pg_pow_d((double)(1 - cos1), 5.0));
-        }
-    } else {
-        r.kind = 2;
-        if (m.tex < 0) {
-            r.m_d_r = m.kd[2];
-            r.m_d_g = m.kd[1];
-            r.m_d_b = m.kd[0];
-        } else {
-            const float tu = interp1(a[9], a[11], a[13], u, v);
-            const float tv = interp1(a[10], a[12], a[14], u, v);
-            const V3 tx = tex_texel(s.tex[m.tex], s.texels, lut, tu, 1.0f - tv);
-            r.m_d_r = tx.x;
-            r.m_d_g = tx.y;
-            r.m_d_b = tx.z;
-        }
-        for (int li = 0; li < s.nlight; ++li) {
-            const DevLight& L = s.lights[li];
-            if (!(dot(nn, v3(L.pos[0], L.pos[1], L.pos[2])) < 0)) ++r.nshadow;
-        }
-        r.color = make_float4(0, 0, 0, 1);
-    }
+    shade_hit(s, mats, lut, level, max_level, d, rtime, h, load_attr(s, h), r);
 }
 
 // LDS of the block-level allocation (BLOCK threads)
 template <int BLOCK>
 struct ShadeAllocLds {
     unsigned long long wtot[2][BLOCK / 64];
-    int wrefl[2][BLOCK / 64];  // reflection children per wave (PGRT_CHILD_SPLIT 2)
+    int wrefl[2][BLOCK / 64];  // reflection children per wave
     unsigned long long bbase;
 };
 
@@ -175,72 +210,101 @@ struct ShadeSlots {
 };
 
 // Phase 2: every thread of the block calls it in the same iteration (uniform control flow; it
-// has two barriers).  it_par alternates per iteration.
+// has two barriers).  it_par alternates per iteration.  shade_alloc_begin claims the block's
+// slots (thread 0's atomic is in flight when it returns), shade_alloc_end hands them out: work
+// placed between the two overlaps the atomic's round trip.
+struct ShadeAllocPending {
+    int spre;
+    unsigned long long mrefl, mrefr;
+    unsigned long long base;  // thread 0: the atomic's result
+};
 template <int BLOCK>
-__device__ __forceinline__ ShadeSlots shade_alloc(ShadeAllocLds<BLOCK>& lds, int& it_par, FrameCounters* fc, int level,
-                                                  int sq_base, int sbits, const ShadeOut& r) {
-    int cpre, ctot, spre, stot;
+__device__ __forceinline__ ShadeAllocPending shade_alloc_begin(ShadeAllocLds<BLOCK>& lds, int it_par, FrameCounters* fc,
+                                                               int level, int sbits, const ShadeOut& r) {
+    ShadeAllocPending pa;
+    int cpre, ctot, stot;
     wave_prefix_small(r.nchild, 2, cpre, ctot);
-    wave_prefix_small(r.nshadow, sbits, spre, stot);
+    wave_prefix_small(r.nshadow, sbits, pa.spre, stot);
+    (void)cpre;
     const int rtot = (int)__popcll(__ballot(r.nchild == 2));
     const unsigned long long wtot = ((unsigned long long)(unsigned)stot << 32) | (unsigned)ctot;
     const int w = threadIdx.x >> 6;
-    const unsigned long long mrefl = __ballot(r.nchild >= 1), mrefr = __ballot(r.nchild == 2);
+    pa.mrefl = __ballot(r.nchild >= 1);
+    pa.mrefr = __ballot(r.nchild == 2);
     if (__lane_id() == 0) {
         lds.wtot[it_par][w] = wtot;
-#if PGRT_CHILD_SPLIT == 2
-        lds.wrefl[it_par][w] = (int)__popcll(mrefl);
-#endif
+        lds.wrefl[it_par][w] = (int)__popcll(pa.mrefl);
         if (rtot && level + 1 < kMaxLevels) atomicAdd(&fc->refract[level + 1], rtot);  // statistics
     }
     __syncthreads();
+    pa.base = 0;
     if (threadIdx.x == 0) {
         unsigned long long btot = 0;
         for (int k = 0; k < BLOCK / 64; ++k) btot += lds.wtot[it_par][k];
-        lds.bbase = btot ? atomicAdd(&fc->alloc[level], btot) : 0ull;
+        pa.base = btot ? atomicAdd(&fc->alloc[level], btot) : 0ull;
     }
+    return pa;
+}
+template <int BLOCK>
+__device__ __forceinline__ ShadeSlots shade_alloc_end(ShadeAllocLds<BLOCK>& lds, int& it_par, int sq_base,
+                                                      const ShadeAllocPending& pa) {
+    if (threadIdx.x == 0) lds.bbase = pa.base;
     __syncthreads();
+    const int w = threadIdx.x >> 6;
     unsigned long long old = lds.bbase;
     for (int k = 0; k < w; ++k) old += lds.wtot[it_par][k];
-#if PGRT_CHILD_SPLIT == 2
     int refl_below = 0, refl_block = 0;  // reflections of the block's waves below this one / all
     for (int k = 0; k < BLOCK / 64; ++k) {
         const int c = lds.wrefl[it_par][k];
         refl_block += c;
         if (k < w) refl_below += c;
     }
-#endif
     it_par ^= 1;
     const int cb = __builtin_amdgcn_readfirstlane((int)(unsigned)(old & 0xffffffffull));
     const int sb = __builtin_amdgcn_readfirstlane((int)(unsigned)(old >> 32));
     ShadeSlots o;
-#if PGRT_CHILD_SPLIT == 2
     // the BLOCK's reflection rays first, then its refraction rays, each group in pixel order: a
     // reflection leaves the surface and a refraction enters it, so a next-level wave that mixes
     // the two spans > 90 degrees and its packet traversal visits the union of both paths
     const int bb = __builtin_amdgcn_readfirstlane((int)(unsigned)(lds.bbase & 0xffffffffull));
     const int rb = __builtin_amdgcn_readfirstlane(refl_below), rk = __builtin_amdgcn_readfirstlane(refl_block);
-    o.refl = bb + rb + lanes_below(mrefl);
-    o.refr = bb + rk + (cb - bb - rb) + lanes_below(mrefr);
-    (void)cpre;
-#elif PGRT_CHILD_SPLIT
-    // the wave's reflection rays first, then its refraction rays, each group in pixel order:
-    // the next level's waves are coherent bundles instead of alternating reflect / refract
-    o.refl = cb + lanes_below(mrefl);
-    o.refr = cb + (int)__popcll(mrefl) + lanes_below(mrefr);
-    (void)cpre;
-#else
-    o.refl = cb + cpre;
-    o.refr = o.refl + 1;
-#endif
-    o.shadow = sq_base + sb + spre;
+    o.refl = bb + rb + lanes_below(pa.mrefl);
+    o.refr = bb + rk + (cb - bb - rb) + lanes_below(pa.mrefr);
+    o.shadow = sq_base + sb + pa.spre;
     return o;
+}
+template <int BLOCK>
+__device__ __forceinline__ ShadeSlots shade_alloc(ShadeAllocLds<BLOCK>& lds, int& it_par, FrameCounters* fc, int level,
+                                                  int sq_base, int sbits, const ShadeOut& r) {
+    return shade_alloc_end(lds, it_par, sq_base, shade_alloc_begin(lds, it_par, fc, level, sbits, r));
+}
+
+// Phong term of a lit hit for one light (raytracer.cpp:355-382): (blue, green, red, 0)
+__device__ __forceinline__ float4 phong_term(const DevMaterial& m, const DevLight& L, const ShadeOut& r) {
+    const V3 nrm = r.nrm, hitp = r.hitp, org = r.org, dirraw = r.dirraw;
+    const V3 lp = v3(L.pos[0], L.pos[1], L.pos[2]);
+    const V3 lv = normalize(v3(lp.x - hitp.x, lp.y - hitp.y, lp.z - hitp.z));
+    const V3 cv = normalize(v3(org.x - dirraw.x, org.y - dirraw.y, org.z - dirraw.z));
+    const float gam = m.ns;
+    const float i_d_r = L.kd[2], i_d_g = L.kd[1], i_d_b = L.kd[0];
+    const float i_s_r = L.ks[2], i_s_g = L.ks[1], i_s_b = L.ks[0];
+    const float m_s_r = m.ks[2], m_s_g = m.ks[1], m_s_b = m.ks[0];
+    const float nl = dot(nrm, lv);
+    V3 l_r = scale(2 * nl, nrm) - lv;
+    l_r = normalize(l_r);
+    const float spec = pg_powf(dot(cv, l_r), gam);
+    const float tb = i_d_b * r.m_d_b * dot(nrm, lv) + i_s_b * m_s_b * spec;
+    const float tg = i_d_g * r.m_d_g * dot(nrm, lv) + i_s_g * m_s_g * spec;
+    const float tr = i_d_r * r.m_d_r * dot(nrm, lv) + i_s_r * m_s_r * spec;
+    return make_float4(tb, tg, tr, 0.0f);
 }
 
 // Phase 3 for an active ray i.
+// use_pre0: light 0's Phong term is pre0 (computed earlier by the caller), not computed here
 __device__ __forceinline__ void shade_emit(const SceneView& s, const DevMaterial* mats, int level, int i,
                                            const ShadeOut& r, const ShadeSlots& sl, Queue next, LevelNodes nodes,
-                                           ShadowQueue sq, FrameCounters* fc) {
+                                           ShadowQueue sq, FrameCounters* fc, bool use_pre0 = false,
+                                           float4 pre0 = make_float4(0, 0, 0, 0)) {
     int4 link = make_int4(-1, -1, -1, 0);
     if (r.kind == 1) {
         if ((r.nchild == 2 ? max(sl.refl, sl.refr) : sl.refl) >= next.cap || level + 1 >= kMaxLevels) {
@@ -265,7 +329,7 @@ __device__ __forceinline__ void shade_emit(const SceneView& s, const DevMaterial
             atomicOr(&fc->overflow, 1);
         } else {
             const DevMaterial& m = mats[r.mid];
-            const V3 nrm = r.nrm, hitp = r.hitp, org = r.org, dirraw = r.dirraw;
+            const V3 nrm = r.nrm, hitp = r.hitp;
             int k = sl.shadow;
             for (int li = 0; li < s.nlight; ++li) {
                 const DevLight& L = s.lights[li];
@@ -275,20 +339,7 @@ __device__ __forceinline__ void shade_emit(const SceneView& s, const DevMaterial
                 if (sq.ro) sq.ro[k] = make_float4(lp.x, lp.y, lp.z, 0.01f);
                 sq.rd[k] = make_float4(hitp.x, hitp.y, hitp.z, length(v3(lp.x - hitp.x, lp.y - hitp.y, lp.z - hitp.z)));
                 // Phong term for this light (raytracer.cpp:355-382)
-                const V3 lv = normalize(v3(lp.x - hitp.x, lp.y - hitp.y, lp.z - hitp.z));
-                const V3 cv = normalize(v3(org.x - dirraw.x, org.y - dirraw.y, org.z - dirraw.z));
-                const float gam = m.ns;
-                const float i_d_r = L.kd[2], i_d_g = L.kd[1], i_d_b = L.kd[0];
-                const float i_s_r = L.ks[2], i_s_g = L.ks[1], i_s_b = L.ks[0];
-                const float m_s_r = m.ks[2], m_s_g = m.ks[1], m_s_b = m.ks[0];
-                const float nl = dot(nrm, lv);
-                V3 l_r = scale(2 * nl, nrm) - lv;
-                l_r = normalize(l_r);
-                const float spec = pg_powf(dot(cv, l_r), gam);
-                const float tb = i_d_b * r.m_d_b * dot(nrm, lv) + i_s_b * m_s_b * spec;
-                const float tg = i_d_g * r.m_d_g * dot(nrm, lv) + i_s_g * m_s_g * spec;
-                const float tr = i_d_r * r.m_d_r * dot(nrm, lv) + i_s_r * m_s_r * spec;
-                sq.contrib[k] = make_float4(tb, tg, tr, 0.0f);
+                sq.contrib[k] = (use_pre0 && li == 0) ? pre0 : phong_term(m, L, r);
                 ++k;
             }
             link.z = sl.shadow;

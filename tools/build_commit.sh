@@ -1,11 +1,11 @@
 #!/bin/bash
-# Build libpgrt.so from the csrc/ and include/ of a git revision into build/<name>/ (same-session
-# A/B against the working tree: PGRT_LIB=build/<name>/libpgrt.so, tools/ab_libs.sh).
+# Build libpgrt.so from the csrc/ and include/ of a git revision into ablib/<name>/ (objects under /tmp/pgrt_variants) (same-session
+# A/B against the working tree: PGRT_LIB=ablib/<name>/libpgrt.so, tools/ab_libs.sh).
 # usage: tools/build_commit.sh <rev> <name>
 set -e
 cd "$(dirname "$0")/.."
 REV=$1; NAME=$2
-OUT=build/$NAME
+OUT=/tmp/pgrt_variants/$NAME
 rm -rf "$OUT"; mkdir -p "$OUT/csrc" "$OUT/include"
 for f in $(git ls-tree --name-only "$REV" pgi_raytracing_amd/csrc/); do git show "$REV:$f" > "$OUT/csrc/$(basename $f)"; done
 for f in $(git ls-tree --name-only "$REV" include/); do git show "$REV:$f" > "$OUT/include/$(basename $f)"; done
@@ -20,4 +20,5 @@ for src in "$OUT"/csrc/*.hip "$OUT"/csrc/*.cpp; do
 done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$OUT/libpgrt.so" $OBJS -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
-echo "$OUT/libpgrt.so"
+mkdir -p ablib/$NAME && cp "$OUT/libpgrt.so" ablib/$NAME/
+echo "ablib/$NAME/libpgrt.so"

@@ -1,12 +1,12 @@
 #!/bin/bash
-# Build libpgrt.so from the working tree's csrc/ + include/ into build/<name>/, optionally with one
+# Build libpgrt.so from the working tree's csrc/ + include/ into ablib/<name>/ (objects under /tmp/pgrt_variants), optionally with one
 # source file patched by a sed expression and/or extra compiler flags (EXTRA_FLAGS="-DFOO=1"), for
-# same-session A/B (load it with PGRT_LIB=build/<name>/libpgrt.so, tools/ab_matrix.sh).
+# same-session A/B (load it with PGRT_LIB=ablib/<name>/libpgrt.so, tools/ab_matrix.sh).
 # usage: [EXTRA_FLAGS=...] tools/build_variant.sh <name> [<file in csrc/> <sed-expr>]
 set -e
 cd "$(dirname "$0")/.."
 NAME=$1; SRC=${2:-}; EXPR=${3:-}
-OUT=build/$NAME
+OUT=/tmp/pgrt_variants/$NAME
 rm -rf "$OUT"; mkdir -p "$OUT/csrc" "$OUT/include"
 cp pgi_raytracing_amd/csrc/* "$OUT/csrc/"
 cp include/* "$OUT/include/"
@@ -25,4 +25,5 @@ for src in "$OUT"/csrc/*.hip "$OUT"/csrc/*.cpp; do
 done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$OUT/libpgrt.so" $OBJS -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
-echo "$OUT/libpgrt.so"
+mkdir -p ablib/$NAME && cp "$OUT/libpgrt.so" ablib/$NAME/
+echo "ablib/$NAME/libpgrt.so"
