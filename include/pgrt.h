@@ -195,7 +195,10 @@ typedef struct pgrt_config {
                              in direction-octant bins (a counting sort by the octant the shade
                              records, keeping screen order inside a bin); 0 / -1 = off (default:
                              no gain on C2, profiles/r3/ab_r3c_binning.txt) */
-    int reserved[2];
+    int packet_budget;    /* bounce levels traced as wave packets: a wave still traversing after this
+                             many node / triangle steps hands its rays (with their closest hits so
+                             far) to the 8-lanes-per-ray kernel; 0 = default, -1 = no budget */
+    int reserved[1];
 } pgrt_config;
 
 /* ---- context ---- */

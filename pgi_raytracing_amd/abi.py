@@ -127,7 +127,8 @@ class Config(C.Structure):
         ("rank0_share_a", C.c_int),
         ("rank0_share_b", C.c_int),
         ("ray_binning", C.c_int),
-        ("reserved", C.c_int * 2),
+        ("packet_budget", C.c_int),
+        ("reserved", C.c_int * 1),
     ]
 
 

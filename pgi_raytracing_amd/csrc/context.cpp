@@ -115,6 +115,7 @@ struct FrameSlot {
     DevBuf<unsigned char> q_key;  // binning key of the next level's rays (one level at a time)
     DevBuf<int> q_perm;           // the binned level's traversal order
     DevBuf<unsigned> q_bins;      // per-chunk bin counts / offsets of the binning sort
+    DevBuf<int> q_defer;          // rays a budgeted packet launch handed to the 8-lane kernel
     DevBuf<unsigned long long> l0_hit, l0_pending;  // 1-spp level-0 wave masks (L0Final)
     int q_cap = 0;
     std::vector<std::unique_ptr<DevBuf<float4>>> n_color, n_att;
@@ -148,6 +149,7 @@ struct FrameSlot {
     DevBuf<int> gstack;
     std::vector<int4> tiles_dev;  // host copy of the device tile list
     int expect_count[kMaxLevels] = {0};  // grid hints from the previous frame (0 = unknown)
+    int expect_defer[kMaxLevels] = {0};
     int expect_shadow_total = 0;
     FrameSlot() {
         PGRT_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -537,6 +539,7 @@ void ensure_frame_buffers(FrameSlot* sl, int n0, int levels, int nlight, int bat
         sl->q_key.alloc(n0);
         sl->q_perm.alloc(n0);
         sl->q_bins.alloc(((size_t)n0 / 256 + 1) * kBins);
+        sl->q_defer.alloc(n0);
         sl->q_cap = n0;
     }
     if ((int)sl->level_cap.size() < levels) sl->level_cap.resize(levels, 0);
@@ -593,6 +596,7 @@ void grow_after_overflow(FrameSlot* sl, int levels) {
                 sl->q_key.alloc(need);
                 sl->q_perm.alloc(need);
                 sl->q_bins.alloc(((size_t)need / 256 + 1) * kBins);
+                sl->q_defer.alloc(need);
                 sl->q_cap = need;
             }
         }
@@ -694,6 +698,12 @@ int group_max(const pgrt_ctx* ctx) {
     return ctx->frames_in_flight > 1 ? kDefaultGroupMaxInFlight : kDefaultGroupMax;
 }
 
+// step budget of the bounce levels' packet launches (pgrt_config.packet_budget)
+int packet_budget(const pgrt_ctx* ctx) {
+    const int b = ctx->cfg.packet_budget;
+    return b < 0 ? 0 : (b == 0 ? kDefaultPacketBudget : b);
+}
+
 // One sample batch of a PGRT_MODE_PATH frame (path.hip): raygen, then per bounce L the closest
 // hits of the path queue, the bounce's shading, its shadow rays and their resolve; the finish
 // sums each pixel's path accumulators (a resolved level 0) and writes the output like a Whitted
@@ -730,6 +740,10 @@ void enqueue_path_batch(pgrt_ctx* ctx, FrameSlot* sl, const SceneView& view, con
         tl.count = p->profile >= 2;
         tl.packets = packet_level(ctx, L);
         tl.pkt_util = fcd->pkt[L];
+        tl.budget = packet_budget(ctx);
+        tl.defer_list = sl->q_defer.p;
+        tl.defer_count = &fcd->defer[L];
+        tl.defer_expect = sl->expect_defer[L];
         id = ctx->timer.begin_kernel(CAT_TRACE, CAT_LTRACE + L);
         const bool launched = launch_trace(view, tl, s);
         ctx->timer.end_kernel(s, id, launched);
@@ -907,6 +921,10 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 tl.packets = packet_level(ctx, L);  // coherent 8x8-pixel waves -> packet traversal
                 tl.gen = L == 0 && fuse ? &gen : nullptr;
                 tl.pkt_util = fcd->pkt[L];
+                tl.budget = packet_budget(ctx);
+                tl.defer_list = sl->q_defer.p;
+                tl.defer_count = &fcd->defer[L];
+                tl.defer_expect = sl->expect_defer[L];
                 if (binned) {
                     id = ctx->timer.begin(s, CAT_BIN);
                     launch_bin_rays(sl->q_key.p, fcd, L, maxc, sl->q_perm.p, sl->q_bins.p, ex, s);
@@ -1013,9 +1031,13 @@ bool read_frame_counters(pgrt_ctx* ctx, FrameSet* fs) {
             if (e == 0 || c > e || 2 * c + 2048 < e) e = c + c / 4 + 1024;
         };
         for (int L = 0; L < kMaxLevels; ++L) {
-            int c = 0;
-            for (auto& h : sl->host_fc) c = std::max(c, fc_count(h, L));
+            int c = 0, dc = 0;
+            for (auto& h : sl->host_fc) {
+                c = std::max(c, fc_count(h, L));
+                dc = std::max(dc, h.defer[L]);
+            }
             hint(sl->expect_count[L], c);
+            hint(sl->expect_defer[L], dc);
         }
         hint(sl->expect_shadow_total, shadow_need);
     }
@@ -1431,6 +1453,8 @@ int pgrt_set_config(pgrt_ctx* ctx, const pgrt_config* cfg) {
         PGRT_REQUIRE(cfg->max_batches_in_flight >= 0, PGRT_ERR_INVALID_ARGUMENT, "max_batches_in_flight must be >= 0");
         PGRT_REQUIRE(cfg->ray_binning >= -1 && cfg->ray_binning <= 1, PGRT_ERR_INVALID_ARGUMENT,
                      "ray_binning must be 0 / -1 (off, the default) or 1 (on)");
+        PGRT_REQUIRE(cfg->packet_budget >= -1, PGRT_ERR_INVALID_ARGUMENT,
+                     "packet_budget must be -1 (off), 0 (default) or a step count");
         PGRT_REQUIRE(cfg->rank0_share_a >= 0 && cfg->rank0_share_a <= 64 && cfg->rank0_share_b >= 0 &&
                          cfg->rank0_share_b <= 64,
                      PGRT_ERR_INVALID_ARGUMENT, "rank0_share_a / rank0_share_b must be in [0, 64]");

@@ -532,7 +532,9 @@ __device__ __forceinline__ SlotTest test_slot(unsigned slot, const uint4& m, con
     return r;
 }
 
-template <bool COUNT, int G>
+// RESUME: the rays are a budgeted packet launch's deferred rays (perm = the defer list): each
+// starts from the closest hit the packet found so far (hits[i]), which bounds its traversal
+template <bool COUNT, int G, bool RESUME = false>
 __global__ __launch_bounds__(kTraceBlock) void k_trace8g(SceneView s, const float4* __restrict__ ro,
                                                          const float4* __restrict__ rd, float4* __restrict__ hits,
                                                          const int* __restrict__ count_dev, int count_terms,
@@ -563,6 +565,13 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8g(SceneView s, const floa
         const unsigned oct = (dx > 0.0f ? 1u : 0u) | (dy > 0.0f ? 2u : 0u) | (dz > 0.0f ? 4u : 0u);
         float best_t = tfar, best_u = 0.0f, best_v = 0.0f;
         int best_prim = -1;
+        if constexpr (RESUME) {  // the packet's closest hit so far (its t is <= tfar)
+            const float4 h = hits[i];
+            best_t = h.x;
+            best_u = h.y;
+            best_v = h.z;
+            best_prim = __float_as_int(h.w);
+        }
         unsigned rvis = 0, rtest = 0;
         int sp = 0;
         unsigned gbase = 0, gbits = (1u << (24 + oct)) | 1u;  // the root: slot 0 of a virtual parent
@@ -661,11 +670,17 @@ constexpr int kPktStack = 64;  // wave-uniform stack entries (>= BVH depth + 2)
 // The packet's internal-node loop: from `node` down to the next leaf (returned) or kSentinel.
 // SGN 0-7: every live ray's direction has sign bits SGN (1 = x < 0, 2 = y, 4 = z), so each
 // axis's near / far plane is a fixed operand (box_hit_nf); SGN 8: mixed signs (box_hit).
-template <int SGN, bool COUNT, bool SAMPLE>
+// BUDGET: stop with kDefer once `steps` (wave-uniform, counted across calls) exceeds `budget`
+constexpr int kDefer = 0x7ffffffe;  // pkt_nodes result: the wave ran out of steps (not a node index)
+template <int SGN, bool COUNT, bool SAMPLE, bool BUDGET>
 __device__ __forceinline__ int pkt_nodes(const cfloat_ptr nodes, int node, int& sp, int* wstk, float bt, float idx,
                                          float idy, float idz, float oix, float oiy, float oiz, bool live,
-                                         unsigned& rvis, unsigned& useful, unsigned& live_steps) {
+                                         unsigned& rvis, unsigned& useful, unsigned& live_steps, int& steps,
+                                         int budget) {
     while ((unsigned)node < (unsigned)kSentinel) {
+        if constexpr (BUDGET) {
+            if (++steps > budget) return kDefer;
+        }
         const cfloat_ptr nd = nodes + 16 * node;
         const float4 a = cload4(nd), b = cload4(nd + 4), c = cload4(nd + 8);
         const int4 d = make_int4(__float_as_int(nd[12]), __float_as_int(nd[13]), __float_as_int(nd[14]),
@@ -709,12 +724,16 @@ __device__ __forceinline__ int pkt_nodes(const cfloat_ptr nodes, int node, int& 
 
 // SAMPLE: this block measures packet utilisation (a block-uniform choice; the loop without the
 // counters is a separate copy, so unsampled blocks pay nothing for them)
-template <bool COUNT, bool GEN, bool SAMPLE>
+// BUDGET (bounce levels): a wave that has taken `budget` node / triangle steps stops; its live
+// rays keep the closest hit found so far and go to defer_list (k_trace8g<RESUME> finishes them)
+template <bool COUNT, bool GEN, bool SAMPLE, bool BUDGET>
 __device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __restrict__ ro,
                                           const float4* __restrict__ rd, float4* __restrict__ hits, int n,
                                           unsigned long long* __restrict__ counters, const PrimaryGen& gen,
                                           unsigned long long* __restrict__ util, int (*wstack)[kPktStack],
-                                          const int* __restrict__ perm) {
+                                          const int* __restrict__ perm, int budget, int* __restrict__ defer_list,
+                                          int* __restrict__ defer_count) {
+    static_assert(!(GEN && BUDGET), "level 0 has no step budget");
     const int wib = threadIdx.x >> 6;
     const int lane = __lane_id();
     const cfloat_ptr nodes = (cfloat_ptr)(const void*)s.nodes;  // 16 floats per node
@@ -773,6 +792,7 @@ __device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __re
         const int sgn = __builtin_amdgcn_readfirstlane(
             uni ? (negx != 0ull ? 1 : 0) | (negy != 0ull ? 2 : 0) | (negz != 0ull ? 4 : 0) : 8);
         unsigned rvis = 0, rtest = 0;
+        int steps = 0;
         node = __builtin_amdgcn_readfirstlane(node);  // wave-uniform by construction
         for (;;) {
             // internal nodes (0 <= node < kSentinel) in a loop of their own: the leaf code, which
@@ -781,8 +801,8 @@ __device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __re
             // every step)
             const float bt = __builtin_canonicalizef(best_t);
 #define PGRT_PKT_NODES(S)                                                                                      \
-    node = pkt_nodes<S, COUNT, SAMPLE>(nodes, node, sp, wstack[wib], bt, idx, idy, idz, oix, oiy, oiz, live, rvis, \
-                                       useful, live_steps)
+    node = pkt_nodes<S, COUNT, SAMPLE, BUDGET>(nodes, node, sp, wstack[wib], bt, idx, idy, idz, oix, oiy, oiz, live, \
+                                               rvis, useful, live_steps, steps, budget)
             switch (sgn) {
                 case 0: PGRT_PKT_NODES(0); break;
                 case 1: PGRT_PKT_NODES(1); break;
@@ -795,9 +815,10 @@ __device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __re
                 default: PGRT_PKT_NODES(8); break;
             }
 #undef PGRT_PKT_NODES
-            if (node == kSentinel) break;
+            if (node == kSentinel || (BUDGET && node == kDefer)) break;
             // leaf: its triangles against every lane's ray
             const int first = leaf_first(node), end = first + leaf_count(node);
+            if constexpr (BUDGET) steps += end - first;
             for (int k = first; k < end; ++k) {
                 const cfloat_ptr q = tris + 12 * k;
                 const float4 q0 = cload4(q), q1 = cload4(q + 4), q2 = cload4(q + 8);
@@ -823,6 +844,17 @@ __device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __re
             }
         }
         if (valid) hits[i] = make_float4(live ? best_t : tfar, best_u, best_v, __int_as_float(best_prim));
+        if constexpr (BUDGET) {
+            if (node == kDefer) {  // out of steps: the live rays to the 8-lanes-per-ray kernel
+                const unsigned long long dm = __ballot(live);
+                int b = 0;
+                if (lane == 0) b = atomicAdd(defer_count, (int)__popcll(dm));
+                b = __builtin_amdgcn_readfirstlane(b);
+                if (live)
+                    defer_list[b + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(dm >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((unsigned)dm, 0u))] = i;
+            }
+        }
         if (COUNT && lane == 0) {
             nvis += rvis;
             ntest += rtest;
@@ -849,26 +881,30 @@ __device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __re
 // kernel (GEN) uses 67 VGPRs -> 7 waves; big scenes (BVH + triangles far beyond the L2, fetches
 // that wait on the MALL / HBM) take the 8-wave build (59 VGPRs, more SGPR spills): C5 19.6 ->
 // 19.1 ms/frame, while the avenger proxy's issue-bound level 0 runs better at 7 (r2j A/B)
-template <bool COUNT, bool GEN, int MINW>
+template <bool COUNT, bool GEN, int MINW, bool BUDGET = false>
 __global__ __launch_bounds__(kTraceBlock, MINW) void k_trace_pkt(SceneView s, const float4* __restrict__ ro,
                                                            const float4* __restrict__ rd, float4* __restrict__ hits,
                                                            const int* __restrict__ count_dev, int count_terms,
                                                            int count_host, int cap,
                                                            unsigned long long* __restrict__ counters, PrimaryGen gen,
                                                            unsigned long long* __restrict__ util,
-                                                           const int* __restrict__ perm) {
+                                                           const int* __restrict__ perm, int budget,
+                                                           int* __restrict__ defer_list, int* __restrict__ defer_count) {
     __shared__ int wstack[kTraceBlock / 64][kPktStack];
     const int n = ray_count(count_dev, count_terms, count_host, cap);
     if constexpr (GEN) {
         if (gen.store_count && blockIdx.x == 0 && threadIdx.x == 0) *gen.store_count = n;
         // level 0 is always traced as packets: its utilisation is never sampled
-        pkt_trace<COUNT, GEN, false>(s, ro, rd, hits, n, counters, gen, util, wstack, nullptr);
+        pkt_trace<COUNT, GEN, false, false>(s, ro, rd, hits, n, counters, gen, util, wstack, nullptr, 0, nullptr,
+                                            nullptr);
     } else {
         // packet utilisation sampled in every 8th block (pgrt_config.packet_levels AUTO)
         if (util != nullptr && (blockIdx.x & 7) == 0)
-            pkt_trace<COUNT, GEN, true>(s, ro, rd, hits, n, counters, gen, util, wstack, perm);
+            pkt_trace<COUNT, GEN, true, BUDGET>(s, ro, rd, hits, n, counters, gen, util, wstack, perm, budget,
+                                                defer_list, defer_count);
         else
-            pkt_trace<COUNT, GEN, false>(s, ro, rd, hits, n, counters, gen, util, wstack, perm);
+            pkt_trace<COUNT, GEN, false, BUDGET>(s, ro, rd, hits, n, counters, gen, util, wstack, perm, budget,
+                                                 defer_list, defer_count);
     }
 }
 
@@ -921,18 +957,38 @@ bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) 
         int grid = ceil_div(ex, kTraceBlock);
         if (grid > 16384) grid = 16384;
         const PrimaryGen g = t.gen ? *t.gen : PrimaryGen{};
-#define PGRT_LAUNCH_P(C, G, W)                                                                                \
-    PGRT_TLAUNCH((k_trace_pkt<C, G, W>), dim3(grid), dim3(kTraceBlock), 0, stream, s, t.ro, t.rd, t.hits,     \
-                 t.count_dev, t.count_terms, t.count_host, max_count, t.counters, g, t.pkt_util, t.perm)
+        // a step budget on a bounce level: the waves out of steps hand their rays to k_trace8g
+        const bool budget = !t.gen && t.budget > 0 && t.defer_list && t.defer_count && s.depth8 + 1 <= kGroupStack;
+        hipEvent_t ev_stop = budget ? nullptr : t_ev_stop;  // profile timing spans both launches
+#define PGRT_LAUNCH_P(C, G, W, B)                                                                              \
+    hipExtLaunchKernelGGL((k_trace_pkt<C, G, W, B>), dim3(grid), dim3(kTraceBlock), 0, stream, t_ev_start, ev_stop, \
+                          0, s, t.ro, t.rd, t.hits, t.count_dev, t.count_terms, t.count_host, max_count, t.counters, \
+                          g, t.pkt_util, t.perm, t.budget, t.defer_list, t.defer_count)
         const bool big = s.ntri > kPacketBigScene;
         if (t.count) {
-            if (t.gen) PGRT_LAUNCH_P(true, true, 1); else PGRT_LAUNCH_P(true, false, 1);
+            if (t.gen) PGRT_LAUNCH_P(true, true, 1, false);
+            else if (budget) PGRT_LAUNCH_P(true, false, 1, true);
+            else PGRT_LAUNCH_P(true, false, 1, false);
         } else if (t.gen) {
-            if (big) PGRT_LAUNCH_P(false, true, 8); else PGRT_LAUNCH_P(false, true, 1);
+            if (big) PGRT_LAUNCH_P(false, true, 8, false); else PGRT_LAUNCH_P(false, true, 1, false);
+        } else if (budget) {
+            PGRT_LAUNCH_P(false, false, 1, true);
         } else {
-            PGRT_LAUNCH_P(false, false, 1);
+            PGRT_LAUNCH_P(false, false, 1, false);
         }
 #undef PGRT_LAUNCH_P
+        if (budget) {  // the deferred rays: 8 lanes per ray, from the packet's closest hits
+            const int dex = std::max(t.defer_expect, 1024);
+            const int g8 = std::min(16384, ceil_div(dex, kTraceBlock / 8));
+            if (t.count)
+                hipExtLaunchKernelGGL((k_trace8g<true, 8, true>), dim3(g8), dim3(kTraceBlock), 0, stream, nullptr,
+                                      t_ev_stop, 0, s, t.ro, t.rd, t.hits, t.defer_count, 1, 0, max_count, t.counters,
+                                      t.defer_list);
+            else
+                hipExtLaunchKernelGGL((k_trace8g<false, 8, true>), dim3(g8), dim3(kTraceBlock), 0, stream, nullptr,
+                                      t_ev_stop, 0, s, t.ro, t.rd, t.hits, t.defer_count, 1, 0, max_count, t.counters,
+                                      t.defer_list);
+        }
         return true;
     }
     if (t.allow_group && ex <= s.group_max && s.depth8 + 1 <= kGroupStack) {

@@ -41,6 +41,9 @@ struct FrameCounters {
     alignas(128) unsigned long long shade[kMaxLevels][2];
     // ray binning per level: bin sizes (statistics)
     alignas(128) unsigned bins[kMaxLevels][kBins];
+    // packet launches with a step budget (pgrt_config.packet_budget): rays of the waves that ran
+    // out of steps, finished by the 8-lanes-per-ray kernel (count; the list is FrameSlot::q_defer)
+    alignas(128) int defer[kMaxLevels];
 };
 
 __host__ __device__ inline int fc_count(const FrameCounters& f, int L) {
@@ -162,6 +165,14 @@ struct TraceLaunch {
     unsigned char* lit = nullptr;
     // binned level: launch slot i traces ray perm[i] (ro / rd / hits indexed by it), NULL = i
     const int* perm = nullptr;
+    // bounce-level packets (packets && !gen): a wave still traversing after `budget` node /
+    // triangle steps stores its rays' closest hits so far and appends the rays to defer_list
+    // (count in *defer_count); a second launch finishes them 8 lanes per ray over the 8-wide BVH,
+    // starting from those hits.  budget 0: no budget.  defer_expect sizes its grid.
+    int budget = 0;
+    int* defer_list = nullptr;
+    int* defer_count = nullptr;
+    int defer_expect = 0;
 };
 // the packet traversal needs the binary layout and a tree that fits its wave-uniform stack
 bool trace_packets_available(const SceneView& s);
@@ -230,6 +241,9 @@ constexpr int kDefaultGroupMax = 400000;   // pgrt_config.group_max default: que
 constexpr int kDefaultGroupMaxInFlight = 100000;  // with frames in flight the concurrent frames hide
                                                   // the latency floors: level 2 (~150k rays) runs
                                                   // faster one lane per ray (r1 scan: 0.392 -> 0.366)
+// pgrt_config.packet_budget default: node / triangle steps a bounce-level packet wave takes before
+// its rays go to the 8-lanes-per-ray kernel (calibrated on C2)
+constexpr int kDefaultPacketBudget = 256;
 struct BuildOut {
     int builder;   // in: kBuilder*
     int leaf_max;  // in: triangles per binary leaf (<= kLeafMaxTris)

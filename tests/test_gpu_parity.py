@@ -300,6 +300,32 @@ def test_packet_levels_bit_exact(gpu_ctx, avenger_scene, packets, binning):
         gpu_ctx.set_config(old)
 
 
+@pytest.mark.parametrize("budget", [1, 24, 200])
+def test_packet_budget_deferral_bit_exact(gpu_ctx, avenger_scene, budget):
+    """Bounce-level packets with a step budget: waves out of steps store their rays' closest hits so
+    far and hand the rays to the 8-lanes-per-ray kernel, which resumes from those hits.  A tiny
+    budget defers nearly every wave (every ray resumed), a middling one a mix; packets on every
+    level, DoF samples and the all-glass geosphere included, oracle bit for bit."""
+    gpu_ctx.set_scene(avenger_scene)
+    old = gpu_ctx.configure(packet_levels=16, packet_budget=budget)
+    try:
+        W, H = 96, 64
+        cam = abi.default_camera(W, H)
+        gpu_ctx.set_camera(cam)
+        for p in (abi.make_params(spp_side=1, max_level=5),
+                  abi.make_params(spp_side=2, max_level=7, dof=1, jitter=abi.PGRT_JITTER_HASH, frame=5)):
+            img, _ = gpu_ctx.render(p)
+            ref, _ = _oracle(avenger_scene).render(cam, p)
+            _, exact = assert_frames_match(img, ref)
+            assert exact == 1.0
+        rays = _random_rays(avenger_scene, 4000, 3)
+        hg = gpu_ctx.intersect(rays)
+        ho = _oracle(avenger_scene).intersect(rays)
+        assert (hg.view(np.int32) == ho.view(np.int32)).all()
+    finally:
+        gpu_ctx.set_config(old)
+
+
 @pytest.mark.parametrize("octant", range(8))
 def test_packet_sign_octants_bit_exact(gpu_ctx, avenger_scene, octant):
     """The packet kernel runs one of 8 node loops per direction-sign combination (near / far
