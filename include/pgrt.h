@@ -198,7 +198,10 @@ typedef struct pgrt_config {
     int packet_budget;    /* bounce levels traced as wave packets: a wave still traversing after this
                              many node / triangle steps hands its rays (with their closest hits so
                              far) to the 8-lanes-per-ray kernel; 0 = default, -1 = no budget */
-    int reserved[1];
+    int tail_level;       /* k >= 1: Whitted levels >= k run as ONE persistent launch that hands each
+                             ray's children to the next level as soon as they exist (device-side
+                             level iteration); 0 / -1 = one launch per level (the default: the
+                             persistent tail measured slower on C2, profiles/r3/ab_r3h_tail.txt) */
 } pgrt_config;
 
 /* ---- context ---- */

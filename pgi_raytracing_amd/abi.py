@@ -128,7 +128,7 @@ class Config(C.Structure):
         ("rank0_share_b", C.c_int),
         ("ray_binning", C.c_int),
         ("packet_budget", C.c_int),
-        ("reserved", C.c_int * 1),
+        ("tail_level", C.c_int),
     ]
 
 

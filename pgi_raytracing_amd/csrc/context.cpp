@@ -26,6 +26,7 @@ namespace {
 
 constexpr long long kMaxBatchRays = 16ll << 20;  // level-0 rays per sample batch (pgrt_config default)
 constexpr int kTraceGridThreads = 2048 * 256;    // persistent trace grid (global overflow stacks)
+constexpr int kTailGridMax = 1024;                // persistent tail: 4 resident blocks x 256 CUs
 constexpr int kMaxFramesInFlight = 16;
 constexpr int kMaxFramesPerCall = 64;
 
@@ -116,6 +117,10 @@ struct FrameSlot {
     DevBuf<int> q_perm;           // the binned level's traversal order
     DevBuf<unsigned> q_bins;      // per-chunk bin counts / offsets of the binning sort
     DevBuf<int> q_defer;          // rays a budgeted packet launch handed to the 8-lane kernel
+    // persistent tail (tail.hip): hand-off granules of tail levels > first (5 words per slot) and
+    // the batch epoch their flag words carry (counts up, never 0)
+    std::unique_ptr<DevBuf<unsigned long long>> t_gran[kMaxLevels];
+    unsigned tail_epoch = 0;
     DevBuf<unsigned long long> l0_hit, l0_pending;  // 1-spp level-0 wave masks (L0Final)
     int q_cap = 0;
     std::vector<std::unique_ptr<DevBuf<float4>>> n_color, n_att;
@@ -698,6 +703,14 @@ int group_max(const pgrt_ctx* ctx) {
     return ctx->frames_in_flight > 1 ? kDefaultGroupMaxInFlight : kDefaultGroupMax;
 }
 
+// first level of the persistent tail (pgrt_config.tail_level >= 1), -1 = no tail (the default:
+// measured slower than one launch per level on C2)
+int tail_first(const pgrt_ctx* ctx, const SceneView& view, const pgrt_render_params* p) {
+    const int k = ctx->cfg.tail_level;
+    if (k <= 0 || p->mode != PGRT_MODE_WHITTED || !tail_available(view)) return -1;
+    return k <= p->max_level ? k : -1;
+}
+
 // step budget of the bounce levels' packet launches (pgrt_config.packet_budget)
 int packet_budget(const pgrt_ctx* ctx) {
     const int b = ctx->cfg.packet_budget;
@@ -893,9 +906,44 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             if (!fuse) launch_raygen(ctx->cam, fp, sl->tiles.p, q[0], n0, fcd, s);
             debug_sync(s, "raygen", 0, bi);
             ctx->timer.end(s, id);
+            const int tail = tail_first(ctx, view, p);
             for (int L = 0; L < levels; ++L) {
                 Queue qc = q[L & 1], qn = q[(L + 1) & 1];
                 const int maxc = L == 0 ? n0 : std::min(sl->q_cap, sl->level_cap[L]);
+                if (L == tail) {  // levels tail .. max_level: one persistent launch
+                    TailLaunch tt{};
+                    tt.first = L;
+                    tt.levels = levels;
+                    qc.cap = maxc;
+                    tt.q_first = qc;
+                    long long ex_total = 0;
+                    for (int l = L; l < levels; ++l) {
+                        tt.cap[l] = l == L ? maxc : std::min(sl->q_cap, sl->level_cap[l]);
+                        tt.nodes[l] = LevelNodes{sl->n_color[l]->p, sl->n_link[l]->p, sl->n_att[l]->p};
+                        ex_total += sl->expect_count[l] > 0 ? sl->expect_count[l] : tt.cap[l];
+                        if (l > L) {
+                            if (!sl->t_gran[l]) sl->t_gran[l].reset(new DevBuf<unsigned long long>());
+                            DevBuf<unsigned long long>& g = *sl->t_gran[l];
+                            if (g.n < (size_t)tt.cap[l] * 5) {
+                                // fresh memory: no flag word may hold a live epoch by chance
+                                g.alloc((size_t)tt.cap[l] * 5);
+                                PGRT_HIP(hipMemsetAsync(g.p, 0, g.bytes(), s));
+                            }
+                            tt.gran[l] = g.p;
+                        }
+                    }
+                    tt.sq = sq;
+                    tt.fc = fcd;
+                    if (++sl->tail_epoch == 0) ++sl->tail_epoch;
+                    tt.epoch = sl->tail_epoch;
+                    tt.grid = (int)std::max<long long>(64, std::min<long long>(kTailGridMax, (ex_total + 255) / 256));
+                    int id = ctx->timer.begin(s, CAT_TRACE, CAT_LTRACE + L);
+                    launch_tail(view, fp, tt, s);
+                    ctx->timer.end(s, id);
+                    debug_sync(s, "tail", L, bi);
+                    ++trace_launches;
+                    break;
+                }
                 qc.cap = maxc;
                 qn.cap = std::min(sl->q_cap, L + 1 < levels ? sl->level_cap[L + 1] : sl->q_cap);
                 // the next level's rays get their binning key from this level's shade when the
@@ -1017,6 +1065,8 @@ bool read_frame_counters(pgrt_ctx* ctx, FrameSet* fs) {
         FrameSlot* sl = fs->slots[j].get();
         for (auto& h : sl->host_fc) {
             overflow |= h.overflow != 0;
+            PGRT_REQUIRE(h.tail_err == 0, PGRT_ERR_HIP,
+                         "persistent tail: a bounded wait ran out (tail_err " + std::to_string(h.tail_err) + ")");
             ctx->last_fc.push_back(h);
         }
         int shadow_need = 0;
@@ -1455,6 +1505,8 @@ int pgrt_set_config(pgrt_ctx* ctx, const pgrt_config* cfg) {
                      "ray_binning must be 0 / -1 (off, the default) or 1 (on)");
         PGRT_REQUIRE(cfg->packet_budget >= -1, PGRT_ERR_INVALID_ARGUMENT,
                      "packet_budget must be -1 (off), 0 (default) or a step count");
+        PGRT_REQUIRE(cfg->tail_level >= -1 && cfg->tail_level < kMaxLevels, PGRT_ERR_INVALID_ARGUMENT,
+                     "tail_level must be 0 / -1 (off, the default) or a level in [1, 15]");
         PGRT_REQUIRE(cfg->rank0_share_a >= 0 && cfg->rank0_share_a <= 64 && cfg->rank0_share_b >= 0 &&
                          cfg->rank0_share_b <= 64,
                      PGRT_ERR_INVALID_ARGUMENT, "rank0_share_a / rank0_share_b must be in [0, 64]");

@@ -218,9 +218,14 @@ struct ShadeAllocPending {
     unsigned long long mrefl, mrefr;
     unsigned long long base;  // thread 0: the atomic's result
 };
+// child_ctr / shadow_ctr: where the block's children (low word) and shadow rays (high word) are
+// counted -- both fc->alloc[level] (one packed atomic) unless the persistent tail counts every
+// tail level's shadow rays on its first level's word (tail.hip)
 template <int BLOCK>
 __device__ __forceinline__ ShadeAllocPending shade_alloc_begin(ShadeAllocLds<BLOCK>& lds, int it_par, FrameCounters* fc,
-                                                               int level, int sbits, const ShadeOut& r) {
+                                                               int level, int sbits, const ShadeOut& r,
+                                                               unsigned long long* child_ctr = nullptr,
+                                                               unsigned long long* shadow_ctr = nullptr) {
     ShadeAllocPending pa;
     int cpre, ctot, stot;
     wave_prefix_small(r.nchild, 2, cpre, ctot);
@@ -241,7 +246,15 @@ __device__ __forceinline__ ShadeAllocPending shade_alloc_begin(ShadeAllocLds<BLO
     if (threadIdx.x == 0) {
         unsigned long long btot = 0;
         for (int k = 0; k < BLOCK / 64; ++k) btot += lds.wtot[it_par][k];
-        pa.base = btot ? atomicAdd(&fc->alloc[level], btot) : 0ull;
+        if (!child_ctr || child_ctr == shadow_ctr) {
+            unsigned long long* ctr = child_ctr ? child_ctr : &fc->alloc[level];
+            pa.base = btot ? atomicAdd(ctr, btot) : 0ull;
+        } else {  // separate words: children on the low word of one, shadow rays on the high word of the other
+            const unsigned long long ct = btot & 0xffffffffull, st = btot & ~0xffffffffull;
+            const unsigned long long cb = ct ? atomicAdd(child_ctr, ct) : 0ull;
+            const unsigned long long sb = st ? atomicAdd(shadow_ctr, st) : 0ull;
+            pa.base = (sb & ~0xffffffffull) | (cb & 0xffffffffull);
+        }
     }
     return pa;
 }
@@ -299,30 +312,43 @@ __device__ __forceinline__ float4 phong_term(const DevMaterial& m, const DevLigh
     return make_float4(tb, tg, tr, 0.0f);
 }
 
-// Phase 3 for an active ray i.
-// use_pre0: light 0's Phong term is pre0 (computed earlier by the caller), not computed here
-__device__ __forceinline__ void shade_emit(const SceneView& s, const DevMaterial* mats, int level, int i,
-                                           const ShadeOut& r, const ShadeSlots& sl, Queue next, LevelNodes nodes,
-                                           ShadowQueue sq, FrameCounters* fc, bool use_pre0 = false,
-                                           float4 pre0 = make_float4(0, 0, 0, 0)) {
+// the children of a dielectric hit (raytracer.cpp:306-316): reflection (medium n1), refraction
+// (medium n2); origin the hit point, tnear 0.01, tfar FLT_MAX
+__device__ __forceinline__ float4 child_org(const ShadeOut& r) { return make_float4(r.hitp.x, r.hitp.y, r.hitp.z, 0.01f); }
+__device__ __forceinline__ float4 child_dir(V3 d) { return make_float4(d.x, d.y, d.z, 3.402823466e+38f); }
+
+// Phase 3a: a dielectric hit's children into the next level's queue; returns the node link
+// (refl, refr or -1); -1, -1 when a queue was full (overflow: the frame is re-rendered)
+__device__ __forceinline__ int4 emit_children(int level, const ShadeOut& r, const ShadeSlots& sl, Queue next,
+                                              FrameCounters* fc) {
     int4 link = make_int4(-1, -1, -1, 0);
+    if ((r.nchild == 2 ? max(sl.refl, sl.refr) : sl.refl) >= next.cap || level + 1 >= kMaxLevels) {
+        atomicOr(&fc->overflow, 1);
+        return link;
+    }
+    next.ro[sl.refl] = child_org(r);
+    next.rd[sl.refl] = child_dir(r.refl_dir);
+    next.time[sl.refl] = r.n1;
+    if (next.key) next.key[sl.refl] = (unsigned char)dir_octant(r.refl_dir.x, r.refl_dir.y, r.refl_dir.z);
+    link.x = sl.refl;
+    if (r.nchild == 2) {
+        next.ro[sl.refr] = child_org(r);
+        next.rd[sl.refr] = child_dir(r.refr_dir);
+        next.time[sl.refr] = r.n2;
+        if (next.key) next.key[sl.refr] = (unsigned char)dir_octant(r.refr_dir.x, r.refr_dir.y, r.refr_dir.z);
+        link.y = sl.refr;
+    }
+    return link;
+}
+
+// Phase 3b for an active ray i: the node record (attenuation of a dielectric; an opaque hit's
+// shadow rays with their Phong terms; a final colour).  link: emit_children's result for a
+// dielectric.  use_pre0: light 0's Phong term is pre0 (computed earlier by the caller).
+__device__ __forceinline__ void emit_node(const SceneView& s, const DevMaterial* mats, int i, const ShadeOut& r,
+                                          const ShadeSlots& sl, int4 link, LevelNodes nodes, ShadowQueue sq,
+                                          FrameCounters* fc, bool use_pre0 = false,
+                                          float4 pre0 = make_float4(0, 0, 0, 0)) {
     if (r.kind == 1) {
-        if ((r.nchild == 2 ? max(sl.refl, sl.refr) : sl.refl) >= next.cap || level + 1 >= kMaxLevels) {
-            atomicOr(&fc->overflow, 1);
-        } else {
-            next.ro[sl.refl] = make_float4(r.hitp.x, r.hitp.y, r.hitp.z, 0.01f);
-            next.rd[sl.refl] = make_float4(r.refl_dir.x, r.refl_dir.y, r.refl_dir.z, 3.402823466e+38f);
-            next.time[sl.refl] = r.n1;
-            if (next.key) next.key[sl.refl] = (unsigned char)dir_octant(r.refl_dir.x, r.refl_dir.y, r.refl_dir.z);
-            link.x = sl.refl;
-            if (r.nchild == 2) {
-                next.ro[sl.refr] = make_float4(r.hitp.x, r.hitp.y, r.hitp.z, 0.01f);
-                next.rd[sl.refr] = make_float4(r.refr_dir.x, r.refr_dir.y, r.refr_dir.z, 3.402823466e+38f);
-                next.time[sl.refr] = r.n2;
-                if (next.key) next.key[sl.refr] = (unsigned char)dir_octant(r.refr_dir.x, r.refr_dir.y, r.refr_dir.z);
-                link.y = sl.refr;
-            }
-        }
         nodes.att[i] = r.att;
     } else if (r.kind == 2 && r.nshadow > 0) {
         if (sl.shadow + r.nshadow > sq.cap) {
@@ -348,6 +374,15 @@ __device__ __forceinline__ void shade_emit(const SceneView& s, const DevMaterial
     }
     nodes.link[i] = link;
     if (link.x < 0 && link.z < 0) nodes.color[i] = r.color;  // else derived by k_finish
+}
+
+// Phase 3 for an active ray i.
+__device__ __forceinline__ void shade_emit(const SceneView& s, const DevMaterial* mats, int level, int i,
+                                           const ShadeOut& r, const ShadeSlots& sl, Queue next, LevelNodes nodes,
+                                           ShadowQueue sq, FrameCounters* fc, bool use_pre0 = false,
+                                           float4 pre0 = make_float4(0, 0, 0, 0)) {
+    const int4 link = r.kind == 1 ? emit_children(level, r, sl, next, fc) : make_int4(-1, -1, -1, 0);
+    emit_node(s, mats, i, r, sl, link, nodes, sq, fc, use_pre0, pre0);
 }
 
 }  // namespace pgrt

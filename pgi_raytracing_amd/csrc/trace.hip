@@ -21,79 +21,12 @@
 #include <hip/hip_ext.h>
 
 #include "trace.hpp"
+#include "traverse.hpp"
 #include "camera_ops.hpp"
 
 namespace pgrt {
 
 constexpr int kTraceBlock = 256;
-constexpr int kSentinel = 0x7fffffff;  // bottom of every stack: "traversal finished"
-
-__device__ __forceinline__ bool box_hit(float lox, float hix, float loy, float hiy, float loz,
-                                        float hiz, float idx, float idy, float idz, float oix,
-                                        float oiy, float oiz, float tmax, float& tent) {
-    const float tx0 = fmaf(lox, idx, -oix), tx1 = fmaf(hix, idx, -oix);
-    const float ty0 = fmaf(loy, idy, -oiy), ty1 = fmaf(hiy, idy, -oiy);
-    const float tz0 = fmaf(loz, idz, -oiz), tz1 = fmaf(hiz, idz, -oiz);
-    const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-    const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
-    tent = t0;
-    return t0 <= t1 * 1.000001f;  // conservative: rounding never culls a box a hit lies in
-}
-// the same test with each axis's near and far planes already chosen from the sign of the ray's
-// inverse direction: fma is monotonic, so the near plane's t IS the fminf above (and the far's
-// the fmaxf) -- identical t0 / t1 without the 6 min / max that order them
-__device__ __forceinline__ bool box_hit_nf(float nx, float fx, float ny, float fy, float nz, float fz, float idx,
-                                           float idy, float idz, float oix, float oiy, float oiz, float tmax,
-                                           float& tent) {
-    const float txn = fmaf(nx, idx, -oix), txf = fmaf(fx, idx, -oix);
-    const float tyn = fmaf(ny, idy, -oiy), tyf = fmaf(fy, idy, -oiy);
-    const float tzn = fmaf(nz, idz, -oiz), tzf = fmaf(fz, idz, -oiz);
-    const float t0 = fmaxf(fmaxf(txn, tyn), fmaxf(tzn, 0.0f));
-    const float t1 = fminf(fminf(txf, tyf), fminf(tzf, tmax));
-    tent = t0;
-    return t0 <= t1 * 1.000001f;
-}
-
-// Moeller-Trumbore as Embree's closest-hit path evaluates it (see oracle/oracle.c): e1 = v0 - v1,
-// e2 = v2 - v0 (precomputed), Ng = e2 x e1, scaled edge tests, IEEE divisions.  Closest hit in
-// (tnear, tfar]; ties in t go to the smaller original triangle index.
-// ng: the triangle's Ng = e2 x e1 (tri_normal, precomputed per reference with the same float ops)
-__device__ __forceinline__ void tri_test_ng(float4 q0, float4 q1, float4 q2, float4 ng, float ox, float oy, float oz,
-                                            float dx, float dy, float dz, float tnear, float tfar, float& best_t,
-                                            float& best_u, float& best_v, int& best_prim) {
-    const float e1x = q1.x, e1y = q1.y, e1z = q1.z;
-    const float e2x = q2.x, e2y = q2.y, e2z = q2.z;
-    const float ngx = ng.x, ngy = ng.y, ngz = ng.z;
-    const float cx = q0.x - ox, cy = q0.y - oy, cz = q0.z - oz;
-    const float rx = cy * dz - cz * dy;
-    const float ry = cz * dx - cx * dz;
-    const float rz = cx * dy - cy * dx;
-    const float den = ngx * dx + ngy * dy + ngz * dz;
-    const float absden = fabsf(den);
-    const float U = xorsign(rx * e2x + ry * e2y + rz * e2z, den);
-    const float V = xorsign(rx * e1x + ry * e1y + rz * e1z, den);
-    if (den != 0.0f && U >= 0.0f && V >= 0.0f && U + V <= absden) {
-        const float T = xorsign(ngx * cx + ngy * cy + ngz * cz, den);
-        const float t = T / absden;
-        if (t > tnear && t <= tfar) {
-            const int prim = __float_as_int(q0.w);
-            if (best_prim < 0 || t < best_t || (t == best_t && prim < best_prim)) {
-                best_t = t;
-                best_u = U / absden;
-                best_v = V / absden;
-                best_prim = prim;
-            }
-        }
-    }
-}
-
-__device__ __forceinline__ void tri_test(float4 q0, float4 q1, float4 q2, float ox, float oy, float oz, float dx,
-                                         float dy, float dz, float tnear, float tfar, float& best_t, float& best_u,
-                                         float& best_v, int& best_prim) {
-    tri_test_ng(q0, q1, q2, tri_normal(q1, q2), ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v,
-                best_prim);
-}
-
 __device__ __forceinline__ int ray_count(const int* count_dev, int count_terms, int count_host, int cap) {
     if (!count_dev) return count_host;
     int n = 0;

@@ -44,6 +44,13 @@ struct FrameCounters {
     // packet launches with a step budget (pgrt_config.packet_budget): rays of the waves that ran
     // out of steps, finished by the 8-lanes-per-ray kernel (count; the list is FrameSlot::q_defer)
     alignas(128) int defer[kMaxLevels];
+    // persistent tail (tail.hip): per tail level the next unclaimed queue slot; rays shaded so far;
+    // set when a bounded wait ran out (a fault report, never a normal outcome)
+    alignas(128) int tail_head[kMaxLevels];
+    alignas(128) int tail_done_level[kMaxLevels];  // rays of each tail level shaded so far
+    alignas(128) int tail_done;
+    alignas(128) int tail_alive;  // blocks of the tail launch still running
+    int tail_err;
 };
 
 __host__ __device__ inline int fc_count(const FrameCounters& f, int L) {
@@ -216,6 +223,27 @@ void launch_accumulate_frame(const float* frame, float* sum, float* mean, long l
 // slots), their scan, the scatter of the ray indices into perm, bin by bin (expect sizes the grids)
 void launch_bin_rays(const unsigned char* keys, FrameCounters* fc, int level, int cap, int* perm, unsigned* chunk_buf,
                      int expect, hipStream_t stream);
+// The deep Whitted levels first .. levels-1 as ONE persistent launch (tail.hip): blocks claim 256
+// rays of the shallowest level with unclaimed rays, trace them one lane per ray, shade them and
+// hand their children to the next level through write-through 40-B granules whose last word
+// carries `epoch` (the slot's ready flag), so a ray is traced as soon as its parent is shaded and a
+// level never waits for the slowest ray of the one before it.  Level `first` is the queue the
+// shade of level first-1 wrote (count fc_count(first), capacity first_cap); children of level L go
+// to gran[L+1] (5 words per slot, capacity cap[L+1]); node records and shadow rays as in k_shade,
+// every tail level's shadow rays counted on the high word of fc->alloc[first].
+struct TailLaunch {
+    int first, levels;
+    Queue q_first;
+    unsigned long long* gran[kMaxLevels];
+    int cap[kMaxLevels];
+    LevelNodes nodes[kMaxLevels];
+    ShadowQueue sq;
+    FrameCounters* fc;
+    unsigned epoch;
+    int grid;
+};
+bool tail_available(const SceneView& s);
+void launch_tail(const SceneView& s, const FrameParams& fp, const TailLaunch& t, hipStream_t stream);
 // copy `n` FrameCounters to pinned host memory and zero them on the device
 void launch_export_counters(FrameCounters* dev, FrameCounters* host, int n, hipStream_t stream);
 // Distributed frames: rank r's tile-compact buffer (frame-major, count[r] tiles per frame in its

@@ -326,6 +326,54 @@ def test_packet_budget_deferral_bit_exact(gpu_ctx, avenger_scene, budget):
         gpu_ctx.set_config(old)
 
 
+@pytest.mark.parametrize("tail,packets", [(1, 1), (2, abi.PGRT_PACKETS_AUTO), (3, 16), (5, 1), (0, abi.PGRT_PACKETS_AUTO)])
+def test_persistent_tail_bit_exact(gpu_ctx, avenger_scene, geosphere_scene, tail, packets):
+    """The deep levels as one persistent launch (tail.hip: children handed to the next level through
+    write-through granules, levels overlapping): every start level, with packets before it or not,
+    renders the oracle's frames bit for bit -- the avenger at d = 7 (pinhole and DoF samples), the
+    all-glass geosphere at d = 8 (total internal reflection, long glass chains), batched frames in
+    flight -- and counts the same rays per kind."""
+    old = gpu_ctx.configure(tail_level=tail, packet_levels=packets)
+    try:
+        for scene, cfgs in ((avenger_scene, (dict(spp_side=1, max_level=7),
+                                             dict(spp_side=2, max_level=7, dof=1, jitter=abi.PGRT_JITTER_HASH,
+                                                  frame=2))),
+                             (geosphere_scene, (dict(spp_side=2, max_level=8, jitter=abi.PGRT_JITTER_HASH),))):
+            gpu_ctx.set_scene(scene)
+            W, H = 96, 64
+            cam = (abi.default_camera(W, H) if scene is avenger_scene else
+                   abi.make_camera(W, H, abi.deg2rad(90.0), (2.0, 0.0, 0.0), (0.0, 0.0, 0.0)))  # tutorials.cpp:194
+            gpu_ctx.set_camera(cam)
+            for c in cfgs:
+                p = abi.make_params(**c)
+                img, st = gpu_ctx.render(p)
+                ref, sto = _oracle(scene).render(cam, p)
+                _, exact = assert_frames_match(img, ref)
+                assert exact == 1.0
+                assert (st.rays_primary, st.rays_shadow, st.rays_reflect, st.rays_refract) == \
+                    (sto.rays_primary, sto.rays_shadow, sto.rays_reflect, sto.rays_refract)
+        gpu_ctx.set_scene(avenger_scene)
+        cam = abi.default_camera(96, 64)
+        gpu_ctx.set_camera(cam)
+        buf = gpu_ctx.alloc(3 * 96 * 64 * 16)
+        try:
+            gpu_ctx.set_frames_in_flight(2)
+            p = abi.make_params(spp_side=1, max_level=6, jitter=abi.PGRT_JITTER_HASH, frame=11)
+            gpu_ctx.render_wait(gpu_ctx.render_frames_device_async(p, 3, buf))
+            out = gpu_ctx.to_host(buf, (3, 64, 96, 4))
+            for f in range(3):
+                ref, _ = _oracle(avenger_scene).render(
+                    cam, abi.make_params(spp_side=1, max_level=6, jitter=abi.PGRT_JITTER_HASH, frame=11 + f))
+                _, exact = assert_frames_match(out[f], ref)
+                assert exact == 1.0, f"batched frame {f}"
+        finally:
+            gpu_ctx.set_frames_in_flight(1)
+            gpu_ctx.free(buf)
+    finally:
+        gpu_ctx.set_config(old)
+        gpu_ctx.set_scene(avenger_scene)
+
+
 @pytest.mark.parametrize("octant", range(8))
 def test_packet_sign_octants_bit_exact(gpu_ctx, avenger_scene, octant):
     """The packet kernel runs one of 8 node loops per direction-sign combination (near / far
