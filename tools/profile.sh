@@ -29,4 +29,4 @@ run pmc_fetch 300 --kernel-trace --pmc FETCH_SIZE
 run pmc_write 300 --kernel-trace --pmc WRITE_SIZE
 run pmc_l2 300 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum
 run pmc_valu 300 --kernel-trace --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE
-python3 tools/traffic.py "$OUT" "$OUT/traffic_${CFG}.json" "$TAG" "$CFG $(grep -o '"workload": "[^"]*"' "$OUT/trace.log" | head -1)"
+python3 tools/traffic.py "$OUT" "$OUT/traffic_${CFG}.json" "$TAG" "$(grep -o '"workload": "[^"]*"' "$OUT/trace.log" | head -1 | sed 's/"workload": "//; s/"$//')"

@@ -40,16 +40,25 @@ def main():
     def trace_ids(names):  # the uninstrumented closest-hit launches (COUNT=false variants)
         return [d for d, n in names.items() if "k_trace" in n and "<true" not in n]
 
+    # a budgeted bounce-level packet launch is followed by k_trace8g<..., RESUME = true> over its
+    # deferred rays: bench.py times the pair as ONE closest-hit launch (launch_trace), so their
+    # bytes are summed and the pair counted once
+    def is_resume(n):
+        return "k_trace8g" in n and ", true>" in n.split("(")[0]
+
     fids, wids = trace_ids(fn), trace_ids(wn)
-    f_kb = sum(fetch[d] for d in fids) / max(1, len(fids))
-    w_kb = sum(write[d] for d in wids) / max(1, len(wids))
+    f_n = max(1, sum(1 for d in fids if not is_resume(fn[d])))
+    w_n = max(1, sum(1 for d in wids if not is_resume(wn[d])))
+    f_kb = sum(fetch[d] for d in fids) / f_n
+    w_kb = sum(write[d] for d in wids) / w_n
     res = {
         "workload": workload,
         "kernel": "closest-hit launches (k_trace, k_trace8g), every level + shadow queue",
         "source": f"{root}: rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE, separate passes",
         "correction": "gfx950: FETCH_SIZE x2 (MI355X_MICROARCH.md HBM section); WRITE_SIZE as reported; KB=1024 B",
-        "launches_fetch_pass": len(fids),
-        "launches_write_pass": len(wids),
+        "launches_fetch_pass": f_n,
+        "launches_write_pass": w_n,
+        "resume_launches_fetch_pass": len(fids) - f_n,
         "fetch_kb_per_launch": round(f_kb, 1),
         "write_kb_per_launch": round(w_kb, 1),
         "bytes_per_launch": int(round((2 * f_kb + w_kb) * 1024)),
