@@ -208,6 +208,22 @@ typedef struct pgrt_config {
 const char* pgrt_version(void);
 int pgrt_device_count(int* count);
 int pgrt_create(int hip_device, pgrt_ctx** out);
+/* Single-process multi-device context (SURVEY §8b `pgrt_create(const int* hip_device_ids, int
+ * n_devices, ...)`; the reference is one process with one Producer thread,
+ * simpleguidx11.cpp:86-128): rank r renders its image tiles (the deal of pgrt_tile_count_ex
+ * with the context's share) on hip_device_ids[r], and every frame is gathered into rank 0's
+ * output over RCCL communicators the context creates itself (ncclCommInitAll; one host thread
+ * posts every rank's sends / receives in one ncclGroupStart / ncclGroupEnd).  Ranks listed on
+ * the same device exchange their tiles by device copies instead (RCCL takes one rank per device).
+ * n_devices in [1, 16].  Every pgrt_* call on the returned context applies to all ranks:
+ * set_scene (the same deterministic build on each device), set_camera, set_config,
+ * set_frames_in_flight, synchronize, destroy; pgrt_render / pgrt_render_device /
+ * pgrt_render_frames_device, their _async forms and the pgrt_render_distributed* calls render
+ * whole frames (no render rect) into a buffer on hip_device_ids[0]; stats count the rays of
+ * every rank, device times are the slowest rank's.  The batch queries (pgrt_intersect_closest,
+ * pgrt_occluded), pgrt_render_accumulate and pgrt_render_tiles_device run on rank 0's device;
+ * host-output frames (pgrt_render_frames_host_async) and pgrt_comm_init are not available. */
+int pgrt_create_devices(const int* hip_device_ids, int n_devices, pgrt_ctx** out);
 void pgrt_destroy(pgrt_ctx* ctx);
 const char* pgrt_last_error(const pgrt_ctx* ctx);
 /* The BVH fields take effect at the next pgrt_set_scene, the others at the next frame

@@ -284,12 +284,26 @@ struct pgrt_ctx {
     // rank's compute and rank 0's unpack at N GPUs without the xGMI transfer
     bool emulated = false;
     DevBuf<float> tilebuf, gathered, fb_dev;
+    // single-process multi-device context (pgrt_create_devices): this context is
+    // rank 0 and owns one member context per further device (rank r = members[r - 1]); every
+    // frame renders each rank's tiles on its device and gathers them here.  Communicators from
+    // ncclCommInitAll over distinct devices; ranks that share a device (peer_copy) exchange
+    // their tiles by device copies instead (RCCL takes one rank per device)
+    bool group = false;
+    bool peer_copy = false;
+    std::vector<pgrt_ctx*> members;
 
     // frame sink (progressive accumulation)
     DevBuf<float> acc_frame, acc_sum, acc_mean;
     int acc_count = 0, acc_w = 0, acc_h = 0;
 
     ~pgrt_ctx() {
+        for (pgrt_ctx* m : members) {
+            (void)hipSetDevice(m->device);
+            if (m->stream) (void)hipStreamSynchronize(m->stream);
+            delete m;
+        }
+        (void)hipSetDevice(device);
         if (comm_ctl) (void)ncclCommDestroy(comm_ctl);
         if (ctl_stream) (void)hipStreamDestroy(ctl_stream);
         if (comm) (void)ncclCommDestroy(comm);
@@ -1308,9 +1322,15 @@ void finish_frame(pgrt_ctx* ctx, FrameSet* fs) {
     fs->stats.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - fs->t0).count();
 }
 
+void group_finish_through(pgrt_ctx* head, unsigned long long last);
+
 // finish every pending frame with ticket <= last, oldest first (distributed frames gather in
-// submission order on every rank)
+// submission order on every rank; a multi-device context finishes every rank's frame together)
 void finish_through(pgrt_ctx* ctx, unsigned long long last) {
+    if (ctx->group) {
+        group_finish_through(ctx, last);
+        return;
+    }
     for (;;) {
         FrameSet* oldest = nullptr;
         for (auto& s : ctx->sets)
@@ -1430,6 +1450,183 @@ std::vector<int4> rank_tiles(int W, int H, int rank, const TileDeal& d) {
     return mine;
 }
 
+// ---- single-process multi-device context (pgrt_create_devices) --------------------------
+// One host thread drives every rank: each rank's frame is enqueued on its own device, the
+// gathers of all ranks go into ONE ncclGroupStart / ncclGroupEnd (the form RCCL requires when
+// one thread owns several communicators), and the queue-overflow agreement is a host OR over
+// the ranks' counters (no control collective).  Every rank uses frame set (ticket mod frames in
+// flight), so the ranks' sets stay in lockstep.
+
+std::vector<pgrt_ctx*> group_ranks(pgrt_ctx* head) {
+    std::vector<pgrt_ctx*> r{head};
+    r.insert(r.end(), head->members.begin(), head->members.end());
+    return r;
+}
+
+void on_device(const pgrt_ctx* c) { PGRT_HIP(hipSetDevice(c->device)); }
+
+// every rank's gather of the frames on set si: grouped ncclSend / ncclRecv, or (ranks sharing a
+// device) device copies into rank 0's gather buffer on rank 0's stream
+void group_gather(const std::vector<pgrt_ctx*>& R, int si) {
+    const size_t n = R.size();
+    std::vector<UnpackSrc> u(n);
+    for (size_t i = 0; i < n; ++i) {
+        on_device(R[i]);
+        gather_begin(R[i], frame_set(R[i], si), u[i]);
+    }
+    pgrt_ctx* head = R[0];
+    FrameSet* h = frame_set(head, si);
+    if (head->peer_copy && n > 1) {
+        on_device(head);
+        const TileDeal& d = h->deal;
+        const size_t tile_floats = (size_t)kTile * kTile * 3;
+        const size_t F = (size_t)h->nframes;
+        UnpackSrc& u0 = u[0];
+        head->gathered.alloc(std::max<size_t>(1, F * (u0.prefix[d.world] - u0.count[0]) * tile_floats));
+        u0.src[0] = h->tilebuf.p;
+        for (size_t r = 1; r < n; ++r) {
+            FrameSet* m = frame_set(R[r], (int)si);
+            float* dst = head->gathered.p + F * (u0.prefix[r] - u0.count[0]) * tile_floats;
+            u0.src[r] = dst;
+            // rank r's frame is complete when its gather_begin event is (it follows the slots)
+            PGRT_HIP(hipStreamWaitEvent(head->stream, m->ev_g0, 0));
+            if (u0.count[r] > 0)
+                PGRT_HIP(hipMemcpyPeerAsync(dst, head->device, m->tilebuf.p, R[r]->device,
+                                            sizeof(float) * F * u0.count[r] * tile_floats, head->stream));
+        }
+        gather_end(head, h, u0);
+        for (size_t r = 1; r < n; ++r) {
+            on_device(R[r]);
+            // a member's next frame on this set overwrites its tile buffer after rank 0 copied it
+            PGRT_HIP(hipStreamWaitEvent(R[r]->stream, h->ev_g1, 0));
+            gather_end(R[r], frame_set(R[r], (int)si), u[r]);
+        }
+        return;
+    }
+    auto ok = [](ncclResult_t r, const char* what) {
+        if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(r));
+    };
+    if (n > 1) ok(ncclGroupStart(), "ncclGroupStart");
+    for (size_t i = 0; i < n; ++i) {
+        on_device(R[i]);
+        gather_post(R[i], frame_set(R[i], (int)si), u[i]);
+    }
+    if (n > 1) ok(ncclGroupEnd(), "ncclGroupEnd");
+    for (size_t i = 0; i < n; ++i) {
+        on_device(R[i]);
+        gather_end(R[i], frame_set(R[i], (int)si), u[i]);
+    }
+}
+
+// complete the frame on set si of every rank: counters, re-render + re-gather on any rank's
+// overflow, stats; rank 0's stats describe the whole frame (counts summed over the ranks,
+// device times of the slowest rank)
+void group_finish_set(pgrt_ctx* head, int si) {
+    const std::vector<pgrt_ctx*> R = group_ranks(head);
+    std::vector<char> mine(R.size());
+    int retries = 0;
+    for (pgrt_ctx* m : R) frame_set(m, si)->pending = false;
+    for (;;) {
+        bool any = false;
+        for (size_t i = 0; i < R.size(); ++i) {
+            on_device(R[i]);
+            mine[i] = read_frame_counters(R[i], frame_set(R[i], si));
+            any |= mine[i] != 0;
+        }
+        if (!any) break;
+        const int tries = retries;
+        for (size_t i = 0; i < R.size(); ++i) {
+            on_device(R[i]);
+            int t = tries;
+            rerender_frame(R[i], frame_set(R[i], si), mine[i] != 0, t);
+            retries = t;
+        }
+        group_gather(R, si);
+    }
+    pgrt_stats sum{};
+    for (size_t i = 0; i < R.size(); ++i) {
+        on_device(R[i]);
+        FrameSet* fs = frame_set(R[i], si);
+        frame_stats(R[i], fs, retries);
+        PGRT_HIP(hipEventRecord(fs->ev_ready, R[i]->stream));
+        fs->has_result = true;
+        const pgrt_stats& s = fs->stats;
+        sum.rays_primary += s.rays_primary;
+        sum.rays_shadow += s.rays_shadow;
+        sum.rays_reflect += s.rays_reflect;
+        sum.rays_refract += s.rays_refract;
+        sum.node_visits += s.node_visits;
+        sum.tri_tests += s.tri_tests;
+        sum.wide_node_visits += s.wide_node_visits;
+        sum.shade_hits += s.shade_hits;
+        sum.shade_textured_hits += s.shade_textured_hits;
+        sum.ms_raygen = std::max(sum.ms_raygen, s.ms_raygen);
+        sum.ms_trace = std::max(sum.ms_trace, s.ms_trace);
+        sum.ms_shade = std::max(sum.ms_shade, s.ms_shade);
+        sum.ms_shadow = std::max(sum.ms_shadow, s.ms_shadow);
+        sum.ms_combine = std::max(sum.ms_combine, s.ms_combine);
+        sum.trace_launches = std::max(sum.trace_launches, s.trace_launches);
+        sum.levels = std::max(sum.levels, s.levels);
+    }
+    on_device(head);
+    FrameSet* h = frame_set(head, si);
+    sum.overflow_retries = retries;
+    h->stats = sum;
+    h->stats.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h->t0).count();
+}
+
+void group_finish_through(pgrt_ctx* head, unsigned long long last) {
+    for (;;) {
+        int oldest = -1;
+        for (int i = 0; i < (int)head->sets.size(); ++i) {
+            const FrameSet* s = head->sets[i].get();
+            if (s->pending && s->ticket <= last && (oldest < 0 || s->ticket < head->sets[oldest]->ticket)) oldest = i;
+        }
+        if (oldest < 0) break;
+        group_finish_set(head, oldest);
+    }
+    on_device(head);
+}
+
+// enqueue nframes distributed frames on every rank (rank 0's output: fb, frame-major W x H
+// RGBA) and their grouped gather; returns the ticket
+unsigned long long group_submit(pgrt_ctx* head, const pgrt_render_params* p, int nframes, float* fb) {
+    PGRT_REQUIRE(fb, PGRT_ERR_INVALID_ARGUMENT, "a multi-device context needs an output buffer");
+    PGRT_REQUIRE(p->rect_w <= 0 || (p->rect_x == 0 && p->rect_y == 0 && p->rect_w == head->cam.width &&
+                                     p->rect_h == head->cam.height),
+                 PGRT_ERR_INVALID_ARGUMENT, "a multi-device context renders whole frames (no render rect)");
+    const std::vector<pgrt_ctx*> R = group_ranks(head);
+    const int si = (int)(head->next_ticket % (unsigned long long)head->frames_in_flight);
+    FrameSet* h = frame_set(head, si);
+    if (h->pending) group_finish_through(head, h->ticket);  // the set's previous frame first
+    const TileDeal deal = ctx_deal(head, (int)R.size());
+    const unsigned long long ticket = head->next_ticket;
+    for (pgrt_ctx* m : R) {
+        on_device(m);
+        FrameSet* fs = frame_set(m, si);
+        fs->host_dst = nullptr;
+        m->next_ticket = ticket;  // every rank's frame carries rank 0's ticket
+        start_frame(m, fs, p, rank_tiles(head->cam.width, head->cam.height, m->rank, deal), nullptr, 1, 0, 0, 0,
+                    true, m == head ? fb : nullptr, nframes, 0, deal, true);
+    }
+    group_gather(R, si);
+    on_device(head);
+    return ticket;
+}
+
+// synchronous group frame(s) into fb (rank 0's device)
+void group_render(pgrt_ctx* head, const pgrt_render_params* p, int nframes, float* fb, pgrt_stats* st) {
+    group_finish_through(head, ~0ull);
+    const unsigned long long t = group_submit(head, p, nframes, fb);
+    group_finish_through(head, t);
+    FrameSet* fs = nullptr;
+    for (auto& s : head->sets)
+        if (s->ticket == t) fs = s.get();
+    PGRT_HIP(hipEventSynchronize(fs->ev_ready));
+    gather_times(fs, &fs->stats);
+    if (st) *st = fs->stats;
+}
+
 }  // namespace
 
 // =========================================================================== C ABI
@@ -1472,8 +1669,51 @@ int pgrt_create(int hip_device, pgrt_ctx** out) {
     return PGRT_OK;
 }
 
+int pgrt_create_devices(const int* hip_device_ids, int n_devices, pgrt_ctx** out) {
+    if (!out || !hip_device_ids || n_devices < 1 || n_devices > kMaxRanks) return PGRT_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    pgrt_ctx* head = nullptr;
+    int rc = pgrt_create(hip_device_ids[0], &head);
+    if (rc != PGRT_OK) return rc;
+    for (int r = 1; r < n_devices; ++r) {
+        pgrt_ctx* m = nullptr;
+        rc = pgrt_create(hip_device_ids[r], &m);
+        if (rc != PGRT_OK) {
+            delete head;
+            return rc;
+        }
+        head->members.push_back(m);
+    }
+    rc = guarded(head, [&] {
+        const std::vector<pgrt_ctx*> R = group_ranks(head);
+        bool distinct = true;
+        for (int a = 0; a < n_devices; ++a)
+            for (int b = 0; b < a; ++b) distinct &= hip_device_ids[a] != hip_device_ids[b];
+        for (int r = 0; r < n_devices; ++r) {
+            R[r]->world = n_devices;
+            R[r]->rank = r;
+            R[r]->emulated = false;
+        }
+        head->group = true;
+        head->peer_copy = !distinct;
+        if (distinct) {  // one communicator per device, all created by this thread
+            std::vector<ncclComm_t> comms(n_devices, nullptr);
+            const ncclResult_t r = ncclCommInitAll(comms.data(), n_devices, hip_device_ids);
+            if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+            for (int k = 0; k < n_devices; ++k) R[k]->comm = comms[k];
+        }
+    });
+    if (rc != PGRT_OK) {
+        delete head;
+        return rc;
+    }
+    *out = head;
+    return PGRT_OK;
+}
+
 void pgrt_destroy(pgrt_ctx* ctx) {
     if (!ctx) return;
+    if (ctx->group) (void)guarded(ctx, [&] { drain_frames(ctx); });
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     delete ctx;
@@ -1512,6 +1752,7 @@ int pgrt_set_config(pgrt_ctx* ctx, const pgrt_config* cfg) {
                      PGRT_ERR_INVALID_ARGUMENT, "rank0_share_a / rank0_share_b must be in [0, 64]");
         drain_frames(ctx);  // pending frames were enqueued with the old choices
         ctx->cfg = *cfg;
+        for (pgrt_ctx* m : ctx->members) m->cfg = *cfg;  // a multi-device context: every rank
     });
 }
 
@@ -1521,6 +1762,11 @@ int pgrt_set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* scene) {
         drain_frames(ctx);  // frames in flight read the old scene
         PGRT_HIP(hipStreamSynchronize(ctx->stream));
         set_scene(ctx, scene);
+        for (pgrt_ctx* m : ctx->members) {  // a multi-device context: the same build on every rank
+            on_device(m);
+            PGRT_HIP(hipStreamSynchronize(m->stream));
+            set_scene(m, scene);
+        }
     });
 }
 
@@ -1538,6 +1784,10 @@ int pgrt_set_camera(pgrt_ctx* ctx, const pgrt_camera* cam) {
                      PGRT_ERR_INVALID_ARGUMENT, "camera resolution must be in [1, 65536]");
         ctx->cam = make_camera(*cam);
         ctx->has_cam = true;
+        for (pgrt_ctx* m : ctx->members) {
+            m->cam = ctx->cam;
+            m->has_cam = true;
+        }
     });
 }
 
@@ -1548,7 +1798,10 @@ int pgrt_render_device(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_de
         auto t0 = std::chrono::steady_clock::now();
         int x, y, w, h;
         frame_rect(ctx, p, x, y, w, h);
-        render_tiles(ctx, p, rect_tiles(x, y, w, h), static_cast<float*>(rgba_device), 0, x, y, w, st);
+        if (ctx->group)  // every rank renders its tiles, rank 0 gathers (pgrt_create_devices)
+            group_render(ctx, p, 1, static_cast<float*>(rgba_device), st);
+        else
+            render_tiles(ctx, p, rect_tiles(x, y, w, h), static_cast<float*>(rgba_device), 0, x, y, w, st);
         if (st) st->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     });
 }
@@ -1561,8 +1814,11 @@ int pgrt_render_frames_device(pgrt_ctx* ctx, const pgrt_render_params* p, int nf
         auto t0 = std::chrono::steady_clock::now();
         int x, y, w, h;
         frame_rect(ctx, p, x, y, w, h);
-        render_tiles(ctx, p, rect_tiles(x, y, w, h), static_cast<float*>(rgba_device), 0, x, y, w, st, nframes,
-                     (long long)w * h * 4);
+        if (ctx->group)
+            group_render(ctx, p, nframes, static_cast<float*>(rgba_device), st);
+        else
+            render_tiles(ctx, p, rect_tiles(x, y, w, h), static_cast<float*>(rgba_device), 0, x, y, w, st, nframes,
+                         (long long)w * h * 4);
         if (st) st->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     });
 }
@@ -1575,7 +1831,10 @@ int pgrt_render(pgrt_ctx* ctx, const pgrt_render_params* p, float* rgba_host, pg
         int x, y, w, h;
         frame_rect(ctx, p, x, y, w, h);
         ctx->out_tmp.alloc((size_t)w * h * 4);
-        render_tiles(ctx, p, rect_tiles(x, y, w, h), ctx->out_tmp.p, 0, x, y, w, st);
+        if (ctx->group)
+            group_render(ctx, p, 1, ctx->out_tmp.p, st);
+        else
+            render_tiles(ctx, p, rect_tiles(x, y, w, h), ctx->out_tmp.p, 0, x, y, w, st);
         PGRT_HIP(hipMemcpyAsync(rgba_host, ctx->out_tmp.p, (size_t)w * h * 4 * sizeof(float), hipMemcpyDeviceToHost,
                                 ctx->stream));
         PGRT_HIP(hipStreamSynchronize(ctx->stream));
@@ -1606,7 +1865,14 @@ int pgrt_copy_to_host(pgrt_ctx* ctx, void* dst, const void* src, size_t bytes) {
 
 int pgrt_synchronize(pgrt_ctx* ctx) {
     if (!ctx) return PGRT_ERR_INVALID_ARGUMENT;
-    return guarded(ctx, [&] { PGRT_HIP(hipStreamSynchronize(ctx->stream)); });
+    return guarded(ctx, [&] {
+        for (pgrt_ctx* m : ctx->members) {
+            on_device(m);
+            PGRT_HIP(hipStreamSynchronize(m->stream));
+        }
+        on_device(ctx);
+        PGRT_HIP(hipStreamSynchronize(ctx->stream));
+    });
 }
 
 extern "C++" {
@@ -1827,6 +2093,8 @@ int pgrt_comm_unique_id(char id[128]) {
 int pgrt_comm_init(pgrt_ctx* ctx, int world, int rank, const char id[128]) {
     if (!ctx || !id || world <= 0 || world > kMaxRanks || rank < 0 || rank >= world) return PGRT_ERR_INVALID_ARGUMENT;
     return guarded(ctx, [&] {
+        PGRT_REQUIRE(!ctx->group, PGRT_ERR_INVALID_ARGUMENT,
+                     "a multi-device context (pgrt_create_devices) has its own communicators");
         drain_frames(ctx);
         if (ctx->comm_ctl) {
             (void)ncclCommDestroy(ctx->comm_ctl);
@@ -1866,6 +2134,10 @@ int pgrt_render_distributed_device(pgrt_ctx* ctx, const pgrt_render_params* p, v
     return guarded(ctx, [&] {
         PGRT_REQUIRE(ctx->has_cam, PGRT_ERR_NO_CAMERA, "pgrt_set_camera has not been called");
         PGRT_REQUIRE(ctx->rank != 0 || rgba_device, PGRT_ERR_INVALID_ARGUMENT, "rank 0 needs an output buffer");
+        if (ctx->group) {
+            group_render(ctx, p, 1, static_cast<float*>(rgba_device), st);
+            return;
+        }
         drain_frames(ctx);
         FrameSet* fs = frame_set(ctx, 0);
         // set 0 may last have served pgrt_render_frames_host_async: its host destination belongs
@@ -1906,6 +2178,12 @@ int submit_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device, 
         PGRT_REQUIRE(p->profile == 0, PGRT_ERR_INVALID_ARGUMENT, "profiled frames are synchronous (profile must be 0)");
         PGRT_REQUIRE(!distributed || ctx->rank != 0 || rgba_device, PGRT_ERR_INVALID_ARGUMENT,
                      "rank 0 needs an output buffer");
+        if (ctx->group) {  // every rank's tiles, gathered into rgba_device on rank 0
+            PGRT_REQUIRE(!rgba_host, PGRT_ERR_INVALID_ARGUMENT,
+                         "host-output frames are not available on a multi-device context");
+            *ticket = group_submit(ctx, p, nframes, static_cast<float*>(rgba_device));
+            return;
+        }
         FrameSet* fs = frame_set(ctx, (int)(ctx->next_ticket % (unsigned long long)ctx->frames_in_flight));
         if (fs->pending) finish_through(ctx, fs->ticket);  // the set's previous frame completes first
         fs->host_dst = nullptr;
@@ -2015,7 +2293,7 @@ int pgrt_tune_distribution(pgrt_ctx* ctx, const pgrt_render_params* p, int nfram
                            int* a_out, int* b_out) {
     if (!ctx || !p || nframes < 1 || nframes > kMaxFramesPerCall || calls < 1 || calls > 64)
         return PGRT_ERR_INVALID_ARGUMENT;
-    if (ctx->world <= 1 || (!ctx->comm && !ctx->emulated)) {  // one rank: nothing to balance
+    if (ctx->world <= 1 || (!ctx->comm && !ctx->emulated && !ctx->group)) {  // one rank: nothing to balance
         if (a_out) *a_out = 1;
         if (b_out) *b_out = 1;
         return PGRT_OK;
@@ -2055,7 +2333,8 @@ int pgrt_tune_distribution(pgrt_ctx* ctx, const pgrt_render_params* p, int nfram
         double v2[2] = {std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
                         rc == PGRT_OK ? 0.0 : 1.0};
         const int rrc = guarded(ctx, [&] {
-            if (!ctx->comm) return;  // emulation: this rank's time alone
+            // emulation: this rank's time alone; a multi-device context timed every rank itself
+            if (!ctx->comm || ctx->group) return;
             DevBuf<double> v;
             v.alloc(2);
             PGRT_HIP(hipMemcpyAsync(v.p, v2, sizeof(v2), hipMemcpyHostToDevice, ctx->stream));

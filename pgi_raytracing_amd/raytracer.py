@@ -41,6 +41,7 @@ def lib():
         "pgrt_version": (C.c_char_p, []),
         "pgrt_device_count": (ip, [C.POINTER(C.c_int)]),
         "pgrt_create": (ip, [ip, C.POINTER(vp)]),
+        "pgrt_create_devices": (ip, [C.POINTER(C.c_int), ip, C.POINTER(vp)]),
         "pgrt_destroy": (None, [vp]),
         "pgrt_last_error": (C.c_char_p, [vp]),
         "pgrt_get_config": (ip, [vp, C.POINTER(abi.Config)]),
@@ -122,14 +123,23 @@ def _check(ctx, rc: int):
 
 
 class Context:
-    """One libpgrt context on one HIP device (one process per GPU)."""
+    """One libpgrt context on one HIP device (one process per GPU), or with `devices` a
+    single-process multi-device context (pgrt_create_devices): rank r renders its image tiles on
+    devices[r], every frame is gathered on devices[0]."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, devices=None):
         self.L = lib()
         h = C.c_void_p()
-        rc = self.L.pgrt_create(device, C.byref(h))
-        if rc != abi.PGRT_OK:
-            raise PgrtError(rc, f"pgrt_create(device={device})")
+        if devices is not None:
+            ids = (C.c_int * len(devices))(*devices)
+            rc = self.L.pgrt_create_devices(ids, len(devices), C.byref(h))
+            if rc != abi.PGRT_OK:
+                raise PgrtError(rc, f"pgrt_create_devices({list(devices)})")
+            device = devices[0]
+        else:
+            rc = self.L.pgrt_create(device, C.byref(h))
+            if rc != abi.PGRT_OK:
+                raise PgrtError(rc, f"pgrt_create(device={device})")
         self.h = h
         self.device = device
         self.scene = None

@@ -40,6 +40,19 @@ def test_create_without_device_fails_loudly():
     h = C.c_void_p()
     assert lib().pgrt_create(0, C.byref(h)) == -8  # PGRT_ERR_NO_DEVICE, never a CPU fallback
     assert not h.value
+    ids = (C.c_int * 2)(0, 0)
+    assert lib().pgrt_create_devices(ids, 2, C.byref(h)) == -8
+    assert not h.value
+
+
+def test_create_devices_validation():
+    L = lib()
+    h = C.c_void_p()
+    ids = (C.c_int * 17)(*([0] * 17))
+    assert L.pgrt_create_devices(ids, 0, C.byref(h)) == -1
+    assert L.pgrt_create_devices(ids, 17, C.byref(h)) == -1  # at most 16 ranks
+    assert L.pgrt_create_devices(None, 1, C.byref(h)) == -1
+    assert L.pgrt_create_devices(ids, 1, None) == -1
 
 
 def test_argument_validation():

@@ -228,6 +228,57 @@ def test_distributed_world1_equals_render(gpu_ctx, avenger_scene):
         gpu_ctx.free(buf)
 
 
+@pytest.mark.parametrize("ranks", [1, 2, 3, 8])
+def test_multi_device_context_equals_render(gpu_ctx, avenger_scene, ranks):
+    """pgrt_create_devices (SURVEY 8b's single-process multi-device context).  One device: its
+    own RCCL communicator from ncclCommInitAll (the RCCL path at world 1).  Several ranks listed
+    on this one GPU (the pool has one GPU per box): every rank renders its tile deal on its own
+    streams and rank 0 gathers by device copies -- the single-thread submission, the grouped
+    gather, the lockstep frame sets and the host overflow agreement at world > 1.  Frames are
+    bit-identical to one context's render, synchronous, batched and in flight."""
+    from pgi_raytracing_amd.raytracer import Context, PgrtError
+
+    W, H = 330, 200  # 6 x 4 tiles, ragged edge tiles
+    gpu_ctx.set_scene(avenger_scene)
+    gpu_ctx.set_camera(abi.default_camera(W, H))
+    params = [abi.make_params(max_level=5, spp_side=1 + f % 2, dof=f % 2, jitter=abi.PGRT_JITTER_HASH, frame=f)
+              for f in range(4)]
+    refs = [gpu_ctx.render(p) for p in params]
+    g = Context(devices=[0] * ranks)
+    try:
+        assert g.comm_info() == (ranks, 0)
+        g.set_scene(avenger_scene)
+        g.set_camera(abi.default_camera(W, H))
+        for p, (ref, st_ref) in zip(params, refs):
+            img, st = g.render(p)
+            same = (img == ref) | (np.isnan(img) & np.isnan(ref))
+            assert same.all(), f"{(~same).sum()} pixels differ"
+            assert st.rays() == st_ref.rays() and st.rays_shadow == st_ref.rays_shadow
+        with pytest.raises(PgrtError):  # whole frames only
+            g.render(abi.make_params(max_level=5, rect=(0, 0, 64, 64)))
+        # batched frames, two calls in flight
+        F = 3
+        q = abi.make_params(max_level=5, spp_side=1, jitter=abi.PGRT_JITTER_HASH, frame=0)
+        fr = [gpu_ctx.render(abi.make_params(max_level=5, spp_side=1, jitter=abi.PGRT_JITTER_HASH, frame=f))[0]
+              for f in range(2 * F)]
+        bufs = [g.alloc(F * W * H * 16) for _ in range(2)]
+        g.set_frames_in_flight(2)
+        t0 = g.render_frames_device_async(q, F, bufs[0])
+        q.frame = F
+        t1 = g.render_frames_device_async(q, F, bufs[1])
+        for t, b, base in ((t0, bufs[0], 0), (t1, bufs[1], F)):
+            st = g.render_wait(t)
+            assert st.rays_primary == F * W * H
+            out = g.to_host(b, (F, H, W, 4))
+            for f in range(F):
+                same = (out[f] == fr[base + f]) | (np.isnan(out[f]) & np.isnan(fr[base + f]))
+                assert same.all(), f"frame {base + f}: {(~same).sum()} pixels differ"
+        for b in bufs:
+            g.free(b)
+    finally:
+        g.close()
+
+
 @pytest.mark.parametrize("builder,width,split,group", [
     (abi.PGRT_BVH_LBVH, 2, 0.0, -1), (abi.PGRT_BVH_PLOC, 8, 0.0, -1), (abi.PGRT_BVH_LBVH, 8, 0.0, -1),
     (abi.PGRT_BVH_PLOC, 2, 0.0, -1), (abi.PGRT_BVH_PLOC, 2, 1.0, -1), (abi.PGRT_BVH_PLOC, 8, 0.5, -1),
