@@ -61,6 +61,50 @@ def test_path_glass_two_outcomes(geosphere_scene):
     assert nvals.max() == 2 and (nvals == 2).sum() >= 4, nvals
 
 
+def _furnace_scene():
+    """A grey diffuse ground plane (albedo 0.5, z = 0, +z normals) under a constant
+    environment (BGR bytes 100, 150, 200 on a 1024 x 512 map, so the get_texel edge bands --
+    texture.cpp:96-103 -- cover < 0.2 % of the sky), no lights."""
+    from pgi_raytracing_amd.scene import MaterialData, TextureData
+
+    s = 1000.0
+    pos = np.array([-s, -s, 0, s, -s, 0, s, s, 0, -s, -s, 0, s, s, 0, -s, s, 0], np.float32)
+    nrm = np.tile(np.array([0, 0, 1], np.float32), 6)
+    uv = np.zeros(12, np.float32)
+    env = np.empty((512, 1024, 3), np.uint8)
+    env[...] = (100, 150, 200)
+    tex = TextureData.from_bgr(env, "constant_env")
+    mat = MaterialData("grey", diffuse=(0.5, 0.5, 0.5), specular=(0.0, 0.0, 0.0))
+    return Scene(pos, nrm, uv, np.zeros(2, np.int32), [mat], [tex], 0, [])
+
+
+def test_path_furnace_one_diffuse_bounce():
+    """Energy check that does not use the restatement's own output as the answer:
+    under a constant environment E with no lights, a path that hits the albedo-a plane bounces
+    once into the upper hemisphere, where nothing but the sky remains, so its value is a * E
+    exactly -- per sample, not only in expectation (the cosine-weighted bounce carries T * a,
+    DESIGN.md §2) -- unless the bounce lands in an edge band of the map (black).  A primary
+    miss sees E itself.  Checked per pixel at d = 1 and d = 4 (deeper levels add nothing:
+    the bounce ray escapes), 1 and 4 samples."""
+    sc = _furnace_scene()
+    orc = pyoracle.OracleScene(sc, accel=1)
+    cam = abi.make_camera(64, 48, abi.deg2rad(60.0), (0.0, -60.0, 25.0), (0.0, 40.0, 0.0))
+    for d, S in ((1, 1), (4, 2)):
+        img, st = orc.render(cam, abi.make_params(max_level=d, spp_side=S, mode=PATH,
+                                                  jitter=abi.PGRT_JITTER_HASH, seed=3))
+        rgb = img[..., :3].reshape(-1, 3).astype(np.float64)
+        e = np.array([200, 150, 100], np.float64) / 255.0  # RGB of the BGR bytes
+        sky = np.abs(rgb / e - 1.0).max(1) < 1e-5
+        ground = np.abs(rgb / (0.5 * e) - 1.0).max(1) < 1e-5
+        band = (rgb == 0).all(1)
+        assert sky.sum() > 200 and ground.sum() > 1500, (sky.sum(), ground.sum())
+        # S x S samples: a pixel mixes sky, ground and band samples only on the horizon line
+        other = ~(sky | ground | band)
+        assert other.sum() <= (64 if S > 1 else 0) and band.sum() <= 0.01 * rgb.shape[0]
+        assert (rgb <= e * (1 + 1e-5)).all()  # no pixel brighter than the sky: no energy created
+        assert st.rays_shadow == 0
+
+
 # ---------------------------------------------------------------- GPU parity
 
 PATH_CONFIGS = [
@@ -83,6 +127,21 @@ def test_path_avenger_parity(gpu_ctx, avenger_scene, cfg):
     assert exact == 1.0, f"max diff {diff}, exact fraction {exact}"
     assert (st.rays_primary, st.rays_shadow, st.rays_reflect, st.rays_refract) == \
         (sto.rays_primary, sto.rays_shadow, sto.rays_reflect, sto.rays_refract)
+
+
+@pytest.mark.gpu
+def test_path_furnace_parity(gpu_ctx):
+    """The furnace scene (test_path_furnace_one_diffuse_bounce) on the GPU: bit-exact with the
+    restatement, so the GPU frame meets the same per-pixel a * E energy check."""
+    sc = _furnace_scene()
+    gpu_ctx.set_scene(sc)
+    cam = abi.make_camera(64, 48, abi.deg2rad(60.0), (0.0, -60.0, 25.0), (0.0, 40.0, 0.0))
+    gpu_ctx.set_camera(cam)
+    p = abi.make_params(max_level=4, spp_side=2, mode=PATH, jitter=abi.PGRT_JITTER_HASH, seed=3)
+    img, _ = gpu_ctx.render(p)
+    ref, _ = pyoracle.OracleScene(sc, accel=1).render(cam, p)
+    _, exact = assert_frames_match(img, ref)
+    assert exact == 1.0
 
 
 @pytest.mark.gpu
