@@ -202,6 +202,8 @@ typedef struct pgrt_config {
                              ray's children to the next level as soon as they exist (device-side
                              level iteration); 0 / -1 = one launch per level (the default: the
                              persistent tail measured slower on C2, profiles/r3/ab_r3h_tail.txt) */
+    int packet_width;     /* bounce levels traced as wave packets: 0 / 2 = over the binary BVH (default),
+                             8 = over the quantized 8-wide BVH (one 80-B node per packet step) */
 } pgrt_config;
 
 /* ---- context ---- */

@@ -129,6 +129,7 @@ class Config(C.Structure):
         ("ray_binning", C.c_int),
         ("packet_budget", C.c_int),
         ("tail_level", C.c_int),
+        ("packet_width", C.c_int),
     ]
 
 

@@ -768,6 +768,7 @@ void enqueue_path_batch(pgrt_ctx* ctx, FrameSlot* sl, const SceneView& view, con
         tl.packets = packet_level(ctx, L);
         tl.pkt_util = fcd->pkt[L];
         tl.budget = packet_budget(ctx);
+        tl.wide_packets = L > 0 && ctx->cfg.packet_width == 8;
         tl.defer_list = sl->q_defer.p;
         tl.defer_count = &fcd->defer[L];
         tl.defer_expect = sl->expect_defer[L];
@@ -984,6 +985,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 tl.gen = L == 0 && fuse ? &gen : nullptr;
                 tl.pkt_util = fcd->pkt[L];
                 tl.budget = packet_budget(ctx);
+                tl.wide_packets = L > 0 && ctx->cfg.packet_width == 8;
                 tl.defer_list = sl->q_defer.p;
                 tl.defer_count = &fcd->defer[L];
                 tl.defer_expect = sl->expect_defer[L];
@@ -1747,6 +1749,8 @@ int pgrt_set_config(pgrt_ctx* ctx, const pgrt_config* cfg) {
                      "packet_budget must be -1 (off), 0 (default) or a step count");
         PGRT_REQUIRE(cfg->tail_level >= -1 && cfg->tail_level < kMaxLevels, PGRT_ERR_INVALID_ARGUMENT,
                      "tail_level must be 0 / -1 (off, the default) or a level in [1, 15]");
+        PGRT_REQUIRE(cfg->packet_width == 0 || cfg->packet_width == 2 || cfg->packet_width == 8,
+                     PGRT_ERR_INVALID_ARGUMENT, "packet_width must be 0, 2 or 8");
         PGRT_REQUIRE(cfg->rank0_share_a >= 0 && cfg->rank0_share_a <= 64 && cfg->rank0_share_b >= 0 &&
                          cfg->rank0_share_b <= 64,
                      PGRT_ERR_INVALID_ARGUMENT, "rank0_share_a / rank0_share_b must be in [0, 64]");

@@ -841,6 +841,183 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void k_trace_pkt(SceneView s, co
     }
 }
 
+// ---------------------------------------------------------------- wave packets, 8-wide BVH
+//
+// The bounce levels' packets are bound by their chain of dependent node fetches (one scalar-load
+// round trip per binary step, a few hundred to a thousand steps for the slowest wave), not by
+// VALU (rocprof: 4-9 % VALU busy).  Here a packet step fetches one 80-B quantized 8-wide node
+// (five scalar 16-B loads, one round trip) and every lane tests its ray against all 8 child
+// boxes: about a third of the binary steps for ~4x the VALU per step.  The wave's node groups
+// are those of k_trace8g (child base, hit bits at 24 + (slot ^ oct) | internal mask), with oct
+// the octant of the first live ray: taking the highest bit first visits the children on the
+// side the packet comes from first.  A visited node's hit leaves are tested at once (scalar
+// triangle loads, every live lane), so each lane keeps the one-lane kernels' closest hit.
+constexpr int kPkt8Stack = 32;  // node groups per wave (>= 8-wide depth + 1, like kGroupStack)
+
+template <bool COUNT, bool SAMPLE, bool BUDGET>
+__device__ __forceinline__ void pkt8_trace(const SceneView& s, const float4* __restrict__ ro,
+                                           const float4* __restrict__ rd, float4* __restrict__ hits, int n,
+                                           unsigned long long* __restrict__ counters,
+                                           unsigned long long* __restrict__ util, uint2 (*wstack)[kPkt8Stack],
+                                           const int* __restrict__ perm, int budget, int* __restrict__ defer_list,
+                                           int* __restrict__ defer_count) {
+    const int wib = threadIdx.x >> 6;
+    const int lane = __lane_id();
+    const cfloat_ptr nodes = (cfloat_ptr)(const void*)s.nodes8;  // 20 floats per node
+    const cfloat_ptr tris = (cfloat_ptr)(const void*)s.tri8;     // 12 floats per triangle
+    unsigned long long nvis = 0, ntest = 0;
+    unsigned useful = 0, live_steps = 0;
+    for (int base = (blockIdx.x * kTraceBlock) + wib * 64; base < n; base += gridDim.x * kTraceBlock) {
+        const int slot_i = base + lane;
+        const bool valid = slot_i < n;
+        const int i = (perm && valid) ? perm[slot_i] : slot_i;
+        float4 o4 = make_float4(0, 0, 0, 0), d4 = make_float4(0, 0, 1, -1.0f);
+        if (valid) {
+            o4 = ro[i];
+            d4 = rd[i];
+        }
+        const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
+        const float dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
+        const float sdx = fabsf(dx) < 1e-30f ? copysignf(1e-30f, dx) : dx;
+        const float sdy = fabsf(dy) < 1e-30f ? copysignf(1e-30f, dy) : dy;
+        const float sdz = fabsf(dz) < 1e-30f ? copysignf(1e-30f, dz) : dz;
+        const float idx = __builtin_amdgcn_rcpf(sdx), idy = __builtin_amdgcn_rcpf(sdy),
+                    idz = __builtin_amdgcn_rcpf(sdz);
+        const bool px = idx >= 0.0f, py = idy >= 0.0f, pz = idz >= 0.0f;
+        const bool live = valid && tfar >= 0.0f;
+        float best_t = live ? tfar : -1.0f;  // a dead lane's boxes all miss (t1 < 0 <= t0)
+        float best_u = 0.0f, best_v = 0.0f;
+        int best_prim = -1;
+        const unsigned long long lmask = __ballot(live);
+        const unsigned myoct = (dx > 0.0f ? 1u : 0u) | (dy > 0.0f ? 2u : 0u) | (dz > 0.0f ? 4u : 0u);
+        const int first_live = lmask ? (int)__builtin_ctzll(lmask) : 0;
+        const unsigned oct = (unsigned)__builtin_amdgcn_readfirstlane(__shfl((int)myoct, first_live, 64));
+        int sp = 0, steps = 0;
+        unsigned gbase = 0, gbits = lmask ? ((1u << (24 + oct)) | 1u) : 0u;  // root: slot 0, base 0
+        unsigned rvis = 0, rtest = 0;
+        bool deferred = false;
+        for (;;) {
+            if (gbits <= 0x00ffffffu) {
+                if (sp == 0) break;
+                --sp;
+                const uint2 g = wstack[wib][sp];
+                gbase = (unsigned)__builtin_amdgcn_readfirstlane((int)g.x);
+                gbits = (unsigned)__builtin_amdgcn_readfirstlane((int)g.y);
+            }
+            if constexpr (BUDGET) {
+                if (++steps > budget) {
+                    deferred = true;
+                    break;
+                }
+            }
+            const int pb = 31 - __clz((int)gbits);
+            gbits &= ~(1u << pb);
+            const unsigned slot = (unsigned)(pb - 24) ^ oct;
+            const int child = (int)gbase + __popc(gbits & 0xffu & ((1u << slot) - 1u));
+            if (gbits > 0x00ffffffu) {  // siblings left: save the group (the same value from every lane)
+                wstack[wib][sp] = make_uint2(gbase, gbits);
+                ++sp;
+            }
+            const cfloat_ptr nd = nodes + 20 * child;
+            const float4 p = cload4(nd);
+            const float4 mf = cload4(nd + 4), qxf = cload4(nd + 8), qyf = cload4(nd + 12), qzf = cload4(nd + 16);
+            const uint4 m = make_uint4(__float_as_uint(mf.x), __float_as_uint(mf.y), __float_as_uint(mf.z),
+                                       __float_as_uint(mf.w));
+            const uint4 qx = make_uint4(__float_as_uint(qxf.x), __float_as_uint(qxf.y), __float_as_uint(qxf.z),
+                                        __float_as_uint(qxf.w));
+            const uint4 qy = make_uint4(__float_as_uint(qyf.x), __float_as_uint(qyf.y), __float_as_uint(qyf.z),
+                                        __float_as_uint(qyf.w));
+            const uint4 qz = make_uint4(__float_as_uint(qzf.x), __float_as_uint(qzf.y), __float_as_uint(qzf.z),
+                                        __float_as_uint(qzf.w));
+            if (COUNT) ++rvis;
+            const unsigned eb = __float_as_uint(p.w);
+            const unsigned imask = eb >> 24;
+            const float ax = __uint_as_float((eb & 0xffu) << 23) * idx;
+            const float ay = __uint_as_float(((eb >> 8) & 0xffu) << 23) * idy;
+            const float az = __uint_as_float(((eb >> 16) & 0xffu) << 23) * idz;
+            const float bx = (p.x - ox) * idx, by = (p.y - oy) * idy, bz = (p.z - oz) * idz;
+            unsigned nb = 0u, tb = 0u;  // wave-uniform: hit internal children (ordered bits), hit leaves' triangles
+            bool any_hit = false;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const SlotTest st = test_slot((unsigned)k, m, qx, qy, qz, imask, ax, ay, az, bx, by, bz, px, py, pz,
+                                              best_t);
+                if (SAMPLE) any_hit |= st.hit;
+                if (__ballot(st.hit) != 0ull) {  // meta / imask are wave-uniform: so is the branch
+                    if (st.inner) nb |= 1u << (24 + ((unsigned)k ^ oct));
+                    else tb |= wide_leaf_bits(st.meta);
+                }
+            }
+            if (SAMPLE && live) {
+                ++live_steps;
+                useful += any_hit ? 1u : 0u;
+            }
+            if constexpr (BUDGET) steps += __popc(tb);
+            const unsigned tbase = m.y;
+            while (tb != 0u) {
+                const int k = (int)tbase + __ffs((int)tb) - 1;
+                tb &= tb - 1u;
+                const cfloat_ptr q = tris + 12 * k;
+                const float4 q0 = cload4(q), q1 = cload4(q + 4), q2 = cload4(q + 8);
+                if (COUNT) ++rtest;
+                if (live) tri_test(q0, q1, q2, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v, best_prim);
+            }
+            gbase = m.x;
+            gbits = nb | imask;
+        }
+        if (valid) hits[i] = make_float4(live ? best_t : tfar, best_u, best_v, __int_as_float(best_prim));
+        if constexpr (BUDGET) {
+            if (deferred) {  // out of steps: the live rays to the 8-lanes-per-ray kernel
+                const unsigned long long dm = __ballot(live);
+                int b = 0;
+                if (lane == 0) b = atomicAdd(defer_count, (int)__popcll(dm));
+                b = __builtin_amdgcn_readfirstlane(b);
+                if (live)
+                    defer_list[b + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(dm >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((unsigned)dm, 0u))] = i;
+            }
+        }
+        if (COUNT && lane == 0) {
+            nvis += rvis;
+            ntest += rtest;
+        }
+    }
+    if (SAMPLE) {
+        unsigned long long u = useful, l = live_steps;
+        for (int off = 32; off >= 1; off >>= 1) {
+            u += __shfl_xor(u, off, 64);
+            l += __shfl_xor(l, off, 64);
+        }
+        if (lane == 0 && l > 0) {
+            atomicAdd(&util[0], u);
+            atomicAdd(&util[1], l);
+        }
+    }
+    if (COUNT && lane == 0) {  // one packet step = one 80-B wide-node visit
+        atomicAdd(&counters[14], nvis);
+        atomicAdd(&counters[1], ntest);
+    }
+}
+
+template <bool COUNT, bool BUDGET>
+__global__ __launch_bounds__(kTraceBlock) void k_trace_pkt8(SceneView s, const float4* __restrict__ ro,
+                                                            const float4* __restrict__ rd, float4* __restrict__ hits,
+                                                            const int* __restrict__ count_dev, int count_terms,
+                                                            int count_host, int cap,
+                                                            unsigned long long* __restrict__ counters,
+                                                            unsigned long long* __restrict__ util,
+                                                            const int* __restrict__ perm, int budget,
+                                                            int* __restrict__ defer_list, int* __restrict__ defer_count) {
+    __shared__ uint2 wstack[kTraceBlock / 64][kPkt8Stack];
+    const int n = ray_count(count_dev, count_terms, count_host, cap);
+    if (util != nullptr && (blockIdx.x & 7) == 0)
+        pkt8_trace<COUNT, true, BUDGET>(s, ro, rd, hits, n, counters, util, wstack, perm, budget, defer_list,
+                                        defer_count);
+    else
+        pkt8_trace<COUNT, false, BUDGET>(s, ro, rd, hits, n, counters, util, wstack, perm, budget, defer_list,
+                                         defer_count);
+}
+
 // Kernel-exact launch timing (profile frames): the closest-hit launch records the caller's
 // events itself (hipExtLaunchKernel: taken by the packet processor at kernel start / end, the
 // same clock rocprofv3's kernel trace reads), instead of event records queued around it.
@@ -898,7 +1075,18 @@ bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) 
                           0, s, t.ro, t.rd, t.hits, t.count_dev, t.count_terms, t.count_host, max_count, t.counters, \
                           g, t.pkt_util, t.perm, t.budget, t.defer_list, t.defer_count)
         const bool big = s.ntri > kPacketBigScene;
-        if (t.count) {
+        if (!t.gen && t.wide_packets && s.depth8 + 1 <= kPkt8Stack) {  // bounce level over the 8-wide BVH
+#define PGRT_LAUNCH_P8(C, B)                                                                                      \
+    hipExtLaunchKernelGGL((k_trace_pkt8<C, B>), dim3(grid), dim3(kTraceBlock), 0, stream, t_ev_start, ev_stop, 0, s, \
+                          t.ro, t.rd, t.hits, t.count_dev, t.count_terms, t.count_host, max_count, t.counters,        \
+                          t.pkt_util, t.perm, t.budget, t.defer_list, t.defer_count)
+            if (t.count) {
+                if (budget) PGRT_LAUNCH_P8(true, true); else PGRT_LAUNCH_P8(true, false);
+            } else {
+                if (budget) PGRT_LAUNCH_P8(false, true); else PGRT_LAUNCH_P8(false, false);
+            }
+#undef PGRT_LAUNCH_P8
+        } else if (t.count) {
             if (t.gen) PGRT_LAUNCH_P(true, true, 1, false);
             else if (budget) PGRT_LAUNCH_P(true, false, 1, true);
             else PGRT_LAUNCH_P(true, false, 1, false);

@@ -177,6 +177,8 @@ struct TraceLaunch {
     // (count in *defer_count); a second launch finishes them 8 lanes per ray over the 8-wide BVH,
     // starting from those hits.  budget 0: no budget.  defer_expect sizes its grid.
     int budget = 0;
+    // bounce-level packets over the 8-wide BVH (k_trace_pkt8) instead of the binary one
+    bool wide_packets = false;
     int* defer_list = nullptr;
     int* defer_count = nullptr;
     int defer_expect = 0;

@@ -377,6 +377,31 @@ def test_packet_budget_deferral_bit_exact(gpu_ctx, avenger_scene, budget):
         gpu_ctx.set_config(old)
 
 
+@pytest.mark.parametrize("budget", [-1, 8, 0])
+def test_wide_packets_bit_exact(gpu_ctx, avenger_scene, geosphere_scene, budget):
+    """Bounce-level packets over the 8-wide BVH (pgrt_config.packet_width 8): one quantized node
+    per packet step, every lane testing all 8 child boxes; without a budget, with a tiny one
+    (nearly every wave resumed by the 8-lanes-per-ray kernel) and the default.  Packets on every
+    level, the avenger proxy (pinhole and DoF, 1 and 4 samples) and the all-glass geosphere
+    (TIR, deep trees), oracle bit for bit."""
+    old = gpu_ctx.configure(packet_levels=16, packet_budget=budget, packet_width=8)
+    try:
+        for sc, cam in ((avenger_scene, abi.default_camera(96, 64)),
+                        (geosphere_scene, abi.make_camera(64, 48, abi.deg2rad(90.0), (2.0, 0.0, 0.0), (0.0, 0.0, 0.0)))):
+            gpu_ctx.set_scene(sc)
+            gpu_ctx.set_camera(cam)
+            for p in (abi.make_params(spp_side=1, max_level=5),
+                      abi.make_params(spp_side=2, max_level=7, dof=1, jitter=abi.PGRT_JITTER_HASH, frame=5)):
+                img, st = gpu_ctx.render(p)
+                ref, sto = _oracle(sc).render(cam, p)
+                _, exact = assert_frames_match(img, ref)
+                assert exact == 1.0
+                assert (st.rays_primary, st.rays_shadow, st.rays_reflect, st.rays_refract) == \
+                    (sto.rays_primary, sto.rays_shadow, sto.rays_reflect, sto.rays_refract)
+    finally:
+        gpu_ctx.set_config(old)
+
+
 @pytest.mark.parametrize("tail,packets", [(1, 1), (2, abi.PGRT_PACKETS_AUTO), (3, 16), (5, 1), (0, abi.PGRT_PACKETS_AUTO)])
 def test_persistent_tail_bit_exact(gpu_ctx, avenger_scene, geosphere_scene, tail, packets):
     """The deep levels as one persistent launch (tail.hip: children handed to the next level through
