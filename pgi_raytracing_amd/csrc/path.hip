@@ -78,7 +78,7 @@ __global__ __launch_bounds__(kPathBlock) void k_path_shade(SceneView s, FramePar
     }
     const DevMaterial* mats = LDS_TABLES ? smat : s.mats;
     fill_byte_lut(lut255);  // ends with __syncthreads
-    int it_par = 0;
+    int it_par = 0, refr_w = 0;
     const int n = min(fc_count(*fc, level), q.cap);
     const int sbits = s.nlight > 0 ? 32 - __clz(s.nlight) : 0;
     for (int base_i = blockIdx.x * kPathBlock; base_i < n; base_i += gridDim.x * kPathBlock) {
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(kPathBlock) void k_path_shade(SceneView s, FramePar
         a.nshadow = nsh;
         const ShadeSlots sl = shade_alloc<kPathBlock>(alds, it_par, fc, level, 0, sbits, a);
         const unsigned long long mref = __ballot(child && refract);
-        if (__lane_id() == 0 && mref && level + 1 < kMaxLevels) atomicAdd(&fc->refract[level + 1], (int)__popcll(mref));
+        refr_w += (int)__popcll(mref);  // statistics: one atomic per wave and launch (below)
         if (!active) continue;
         if (level == 0) {  // the path's accumulator starts at 0 (oracle: L = {0, 0, 0})
             const float4 e = miss ? r.color : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -186,6 +186,7 @@ __global__ __launch_bounds__(kPathBlock) void k_path_shade(SceneView s, FramePar
             }
         }
     }
+    if (__lane_id() == 0 && refr_w && level + 1 < kMaxLevels) atomicAdd(&fc->refract[level + 1], refr_w);
 }
 
 // lit shadow terms of one bounce, added to the path accumulators in light order

@@ -74,7 +74,7 @@ __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : 6) void k_shade
         for (int k = threadIdx.x; k < s.ntex; k += kShadeBlock) stex[k] = s.tex[k];
         s.tex = stex;  // env_texel / tex_texel read descriptors through s.tex
     }
-    int it_par = 0;
+    int it_par = 0, refr_acc = 0;
     const DevMaterial* mats = LDS_TABLES ? smat : s.mats;
     fill_byte_lut(lut255);  // ends with __syncthreads: the tables above are visible too
     const int n = min(fc_count(*fc, level), q.cap);
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : 6) void k_shade
                 atomicAdd(&fc->shade[level][1], (unsigned long long)__popcll(tm));
             }
         }
-        const ShadeSlots sl = shade_alloc<kShadeBlock>(alds, it_par, fc, level, sq_base, sbits, r);
+        const ShadeSlots sl = shade_alloc<kShadeBlock>(alds, it_par, fc, level, sq_base, sbits, r, &refr_acc);
         if constexpr (l0final) {
             // a final colour (environment texel; padding; a hit at max_level) -> the pixel, now;
             // the others are completed by the finish (n is a multiple of 64: whole waves)
@@ -147,6 +147,7 @@ __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : 6) void k_shade
             shade_emit(s, mats, level, i, r, sl, next, nodes, sq, fc);
         }
     }
+    shade_refract_flush(fc, level, refr_acc);
 }
 
 void launch_shade(const SceneView& s, const FrameParams& fp, int level, Queue q, Queue next, LevelNodes nodes,

@@ -202,6 +202,7 @@ template <int BLOCK>
 struct ShadeAllocLds {
     unsigned long long wtot[2][BLOCK / 64];
     int wrefl[2][BLOCK / 64];  // reflection children per wave
+    int wrefr[2][BLOCK / 64];  // refraction children per wave (statistics)
     unsigned long long bbase;
 };
 
@@ -220,12 +221,17 @@ struct ShadeAllocPending {
 };
 // child_ctr / shadow_ctr: where the block's children (low word) and shadow rays (high word) are
 // counted -- both fc->alloc[level] (one packed atomic) unless the persistent tail counts every
-// tail level's shadow rays on its first level's word (tail.hip)
+// tail level's shadow rays on its first level's word (tail.hip).
+// refr_acc: thread 0's running count of refraction children (statistics, fc->refract), flushed by
+// the caller once per launch (shade_refract_flush); nullptr: one atomic per block and iteration.
+// (A same-address atomic per WAVE, as before r3, serialised ~27k atomics on one word for an
+// 8-frame C2 level 1.)
 template <int BLOCK>
 __device__ __forceinline__ ShadeAllocPending shade_alloc_begin(ShadeAllocLds<BLOCK>& lds, int it_par, FrameCounters* fc,
                                                                int level, int sbits, const ShadeOut& r,
                                                                unsigned long long* child_ctr = nullptr,
-                                                               unsigned long long* shadow_ctr = nullptr) {
+                                                               unsigned long long* shadow_ctr = nullptr,
+                                                               int* refr_acc = nullptr) {
     ShadeAllocPending pa;
     int cpre, ctot, stot;
     wave_prefix_small(r.nchild, 2, cpre, ctot);
@@ -239,13 +245,19 @@ __device__ __forceinline__ ShadeAllocPending shade_alloc_begin(ShadeAllocLds<BLO
     if (__lane_id() == 0) {
         lds.wtot[it_par][w] = wtot;
         lds.wrefl[it_par][w] = (int)__popcll(pa.mrefl);
-        if (rtot && level + 1 < kMaxLevels) atomicAdd(&fc->refract[level + 1], rtot);  // statistics
+        lds.wrefr[it_par][w] = rtot;
     }
     __syncthreads();
     pa.base = 0;
     if (threadIdx.x == 0) {
         unsigned long long btot = 0;
-        for (int k = 0; k < BLOCK / 64; ++k) btot += lds.wtot[it_par][k];
+        int brefr = 0;
+        for (int k = 0; k < BLOCK / 64; ++k) {
+            btot += lds.wtot[it_par][k];
+            brefr += lds.wrefr[it_par][k];
+        }
+        if (refr_acc) *refr_acc += brefr;
+        else if (brefr && level + 1 < kMaxLevels) atomicAdd(&fc->refract[level + 1], brefr);  // statistics
         if (!child_ctr || child_ctr == shadow_ctr) {
             unsigned long long* ctr = child_ctr ? child_ctr : &fc->alloc[level];
             pa.base = btot ? atomicAdd(ctr, btot) : 0ull;
@@ -288,8 +300,13 @@ __device__ __forceinline__ ShadeSlots shade_alloc_end(ShadeAllocLds<BLOCK>& lds,
 }
 template <int BLOCK>
 __device__ __forceinline__ ShadeSlots shade_alloc(ShadeAllocLds<BLOCK>& lds, int& it_par, FrameCounters* fc, int level,
-                                                  int sq_base, int sbits, const ShadeOut& r) {
-    return shade_alloc_end(lds, it_par, sq_base, shade_alloc_begin(lds, it_par, fc, level, sbits, r));
+                                                  int sq_base, int sbits, const ShadeOut& r, int* refr_acc = nullptr) {
+    return shade_alloc_end(lds, it_par, sq_base,
+                           shade_alloc_begin(lds, it_par, fc, level, sbits, r, nullptr, nullptr, refr_acc));
+}
+// thread 0 at the end of a launch: its block's refraction children into fc->refract[level + 1]
+__device__ __forceinline__ void shade_refract_flush(FrameCounters* fc, int level, int refr_acc) {
+    if (threadIdx.x == 0 && refr_acc && level + 1 < kMaxLevels) atomicAdd(&fc->refract[level + 1], refr_acc);
 }
 
 // Phong term of a lit hit for one light (raytracer.cpp:355-382): (blue, green, red, 0)
