@@ -15,7 +15,7 @@ HIPFLAGS_render := -mllvm -disable-machine-licm
 HIPFLAGS_path := -mllvm -disable-machine-licm
 HIPFLAGS_trace := -mllvm -disable-machine-licm
 HIPFLAGS_tail := -mllvm -disable-machine-licm
-OBJS := $(BUILD)/trace.o $(BUILD)/tail.o $(BUILD)/render.o $(BUILD)/bvh.o $(BUILD)/ploc.o $(BUILD)/split.o $(BUILD)/bvh8.o $(BUILD)/path.o $(BUILD)/context.o $(BUILD)/objloader.o
+OBJS := $(BUILD)/trace.o $(BUILD)/tail.o $(BUILD)/render.o $(BUILD)/bvh.o $(BUILD)/ploc.o $(BUILD)/split.o $(BUILD)/bvh8.o $(BUILD)/bvh_layout.o $(BUILD)/path.o $(BUILD)/context.o $(BUILD)/objloader.o
 
 all: $(LIBDIR)/libpgrt.so $(LIBDIR)/libpgrt_image.so oracle $(BUILD)/pg1_pgrt
 

@@ -204,6 +204,10 @@ typedef struct pgrt_config {
                              persistent tail measured slower on C2, profiles/r3/ab_r3h_tail.txt) */
     int packet_width;     /* bounce levels traced as wave packets: 0 / 2 = over the binary BVH (default),
                              8 = over the quantized 8-wide BVH (one 80-B node per packet step) */
+    int bvh_layout;       /* binary node order, applied by pgrt_set_scene: 0 = the builder's creation
+                             order (default), 1 = sibling pairs (the two children of a node in one
+                             128-B line, pairs in depth-first order; neutral on C2 / C5,
+                             profiles/r3/ab_r3u_bvh_layout.txt) */
 } pgrt_config;
 
 /* ---- context ---- */

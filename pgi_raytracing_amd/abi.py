@@ -130,6 +130,7 @@ class Config(C.Structure):
         ("packet_budget", C.c_int),
         ("tail_level", C.c_int),
         ("packet_width", C.c_int),
+        ("bvh_layout", C.c_int),
     ]
 
 

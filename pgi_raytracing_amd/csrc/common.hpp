@@ -63,6 +63,10 @@ struct DevBuf {
         if (log) fprintf(stderr, "pgrt alloc %p %zu\n", (void*)p, count * sizeof(T));
     }
     size_t bytes() const { return n * sizeof(T); }
+    void swap(DevBuf& o) {
+        std::swap(p, o.p);
+        std::swap(n, o.n);
+    }
 };
 
 // ---- device-side scene layout (HBM) -------------------------------------------------------

@@ -485,6 +485,9 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
         sort_tmp.alloc(tmp_bytes);
         build_lbvh(pos.p, n, ctx->tri.p, ctx->nodes.p, scratch.p, sort_tmp.p, tmp_bytes, pad, &bo, st);
     }
+    // node order: the builder's, or sibling pairs in 128-B lines, depth-first (bvh_layout.hip;
+    // measured neutral on C2 and C5, profiles/r3/ab_r3u_bvh_layout.txt)
+    if (cfg.bvh_layout == 1) bo.num_nodes = relayout_bvh(ctx->nodes, bo.num_nodes, &bo.root, st);
     const int m = bo.refs;
     // the 8-wide layout is always built: the multi-lane kernel traces small (deep-level) queues
     // over it; PGRT_BVH_WIDTH=8 also sends the big queues to the one-lane 8-wide kernel
@@ -1754,6 +1757,8 @@ int pgrt_set_config(pgrt_ctx* ctx, const pgrt_config* cfg) {
                      "packet_budget must be -1 (off), 0 (default) or a step count");
         PGRT_REQUIRE(cfg->tail_level >= -1 && cfg->tail_level < kMaxLevels, PGRT_ERR_INVALID_ARGUMENT,
                      "tail_level must be 0 / -1 (off, the default) or a level in [1, 15]");
+        PGRT_REQUIRE(cfg->bvh_layout == 0 || cfg->bvh_layout == 1, PGRT_ERR_INVALID_ARGUMENT,
+                     "bvh_layout must be 0 (builder order) or 1 (sibling pairs)");
         PGRT_REQUIRE(cfg->packet_width == 0 || cfg->packet_width == 2 || cfg->packet_width == 8,
                      PGRT_ERR_INVALID_ARGUMENT, "packet_width must be 0, 2 or 8");
         PGRT_REQUIRE(cfg->rank0_share_a >= 0 && cfg->rank0_share_a <= 64 && cfg->rank0_share_b >= 0 &&

@@ -290,6 +290,8 @@ void build_ploc(const float* pos_dev, const float4* ref_lo, const float4* ref_hi
                 float4* tri_out, BvhNode* nodes_out, BuildOut* out, int* iterations, hipStream_t stream);
 // PLOC over triangle references (split.hip): beta > 0 adds up to beta * n split references
 // (early split clipping); sizes tri (3 float4 per reference) and nodes; returns the count
+// sibling-pair cache-line layout of a built binary BVH (bvh_layout.hip); returns the node count
+int relayout_bvh(DevBuf<BvhNode>& nodes, int num_nodes, int* root, hipStream_t stream);
 int build_ploc_refs(const float* pos_dev, int ntri, float beta, float pad, float extent, DevBuf<float4>& tri,
                     DevBuf<BvhNode>& nodes, BuildOut* out, hipStream_t stream);
 void build_lbvh(const float* pos_dev, int ntri, float4* tri_out, BvhNode* nodes_out, int* scratch_int,

@@ -279,16 +279,20 @@ def test_multi_device_context_equals_render(gpu_ctx, avenger_scene, ranks):
         g.close()
 
 
-@pytest.mark.parametrize("builder,width,split,group", [
-    (abi.PGRT_BVH_LBVH, 2, 0.0, -1), (abi.PGRT_BVH_PLOC, 8, 0.0, -1), (abi.PGRT_BVH_LBVH, 8, 0.0, -1),
-    (abi.PGRT_BVH_PLOC, 2, 0.0, -1), (abi.PGRT_BVH_PLOC, 2, 1.0, -1), (abi.PGRT_BVH_PLOC, 8, 0.5, -1),
-    (abi.PGRT_BVH_PLOC, 2, 0.0, 1 << 30), (abi.PGRT_BVH_LBVH, 2, 0.5, 1 << 30), (abi.PGRT_BVH_PLOC, 2, 0.5, 1 << 30)])
-def test_bvh_layouts_bit_exact(gpu_ctx, avenger_scene, builder, width, split, group):
+@pytest.mark.parametrize("builder,width,split,group,layout", [
+    (abi.PGRT_BVH_LBVH, 2, 0.0, -1, 0), (abi.PGRT_BVH_PLOC, 8, 0.0, -1, 0), (abi.PGRT_BVH_LBVH, 8, 0.0, -1, 0),
+    (abi.PGRT_BVH_PLOC, 2, 0.0, -1, 0), (abi.PGRT_BVH_PLOC, 2, 1.0, -1, 0), (abi.PGRT_BVH_PLOC, 8, 0.5, -1, 0),
+    (abi.PGRT_BVH_PLOC, 2, 0.0, 1 << 30, 0), (abi.PGRT_BVH_LBVH, 2, 0.5, 1 << 30, 0),
+    (abi.PGRT_BVH_PLOC, 2, 0.5, 1 << 30, 0), (abi.PGRT_BVH_PLOC, 2, 0.0, -1, 1), (abi.PGRT_BVH_LBVH, 2, 0.0, -1, 1),
+    (abi.PGRT_BVH_PLOC, 2, 0.5, 1 << 30, 1), (abi.PGRT_BVH_PLOC, 8, 0.0, 1 << 30, 1)])
+def test_bvh_layouts_bit_exact(gpu_ctx, avenger_scene, builder, width, split, group, layout):
     """Every BVH builder / traversal layout / split budget (pgrt_config) gives the same closest
     hits and frames: the hit is order-independent (ties to the smaller triangle index,
     conservative box tests), and split references cover their triangle.  group: queues up to it
-    take 8 (4) lanes per ray over the 8-wide BVH (-1 never)."""
-    old = gpu_ctx.configure(bvh_builder=builder, bvh_width=width, split_beta=split, group_max=group)
+    take 8 (4) lanes per ray over the 8-wide BVH (-1 never).  layout: binary nodes in the
+    builder's order (0, the default) or as sibling pairs in depth-first order (1)."""
+    old = gpu_ctx.configure(bvh_builder=builder, bvh_width=width, split_beta=split, group_max=group,
+                            bvh_layout=layout)
     try:
         gpu_ctx.set_scene(avenger_scene)
         info = gpu_ctx.bvh_info()
