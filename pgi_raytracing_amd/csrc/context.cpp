@@ -729,14 +729,9 @@ int tail_first(const pgrt_ctx* ctx, const SceneView& view, const pgrt_render_par
 }
 
 // step budget of the bounce levels' packet launches (pgrt_config.packet_budget)
-// The default budget follows the level's expected ray count: a small queue (one frame, ~270k expected rays on level 1: a few
-// waves per SIMD) is bound by its slowest waves, so they hand over early (r3f: one-frame level 1
-// 576 -> 309 us at 256 steps, 181 us at 64); a big one (8 frames per call: level 2 ~970k, tens of waves per
-// SIMD) keeps its waves on packets longer, where 8 lanes per deferred ray would cost throughput
-int packet_budget(const pgrt_ctx* ctx, int expect) {
+int packet_budget(const pgrt_ctx* ctx) {
     const int b = ctx->cfg.packet_budget;
-    if (b != 0) return b < 0 ? 0 : b;
-    return expect < kSmallPacketQueue ? kSmallQueuePacketBudget : kDefaultPacketBudget;
+    return b < 0 ? 0 : (b == 0 ? kDefaultPacketBudget : b);
 }
 
 // One sample batch of a PGRT_MODE_PATH frame (path.hip): raygen, then per bounce L the closest
@@ -775,7 +770,7 @@ void enqueue_path_batch(pgrt_ctx* ctx, FrameSlot* sl, const SceneView& view, con
         tl.count = p->profile >= 2;
         tl.packets = packet_level(ctx, L);
         tl.pkt_util = fcd->pkt[L];
-        tl.budget = packet_budget(ctx, ex);
+        tl.budget = packet_budget(ctx);
         tl.wide_packets = L > 0 && ctx->cfg.packet_width == 8;
         tl.defer_list = sl->q_defer.p;
         tl.defer_count = &fcd->defer[L];
@@ -992,7 +987,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 tl.packets = packet_level(ctx, L);  // coherent 8x8-pixel waves -> packet traversal
                 tl.gen = L == 0 && fuse ? &gen : nullptr;
                 tl.pkt_util = fcd->pkt[L];
-                tl.budget = packet_budget(ctx, ex);
+                tl.budget = packet_budget(ctx);
                 tl.wide_packets = L > 0 && ctx->cfg.packet_width == 8;
                 tl.defer_list = sl->q_defer.p;
                 tl.defer_count = &fcd->defer[L];

@@ -274,9 +274,6 @@ constexpr int kDefaultGroupMaxInFlight = 100000;  // with frames in flight the c
 // pgrt_config.packet_budget default: node / triangle steps a bounce-level packet wave takes before
 // its rays go to the 8-lanes-per-ray kernel (calibrated on C2)
 constexpr int kDefaultPacketBudget = 256;
-// levels expected below kSmallPacketQueue rays take the shorter budget (context.cpp packet_budget)
-constexpr int kSmallPacketQueue = 1 << 19;
-constexpr int kSmallQueuePacketBudget = 64;
 struct BuildOut {
     int builder;   // in: kBuilder*
     int leaf_max;  // in: triangles per binary leaf (<= kLeafMaxTris)

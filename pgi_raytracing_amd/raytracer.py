@@ -103,7 +103,9 @@ def lib():
         "pgrt_frame_diag": (ip, [vp, C.POINTER(abi.LevelDiag), ip]),
     }
     for name, (res, args) in sig.items():
-        f = getattr(L, name)
+        f = getattr(L, name, None)
+        if f is None:  # an older build (PGRT_LIB A/B): calling it raises AttributeError
+            continue
         f.restype = res
         f.argtypes = args
     _LIB = L
