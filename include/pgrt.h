@@ -97,7 +97,7 @@ typedef struct pgrt_light {
  * triangle index is (surface offset + Embree primID) in surface attach order.  The library
  * copies everything to HBM; the caller keeps ownership of the arrays. */
 typedef struct pgrt_scene_desc {
-    int num_triangles;
+    int num_triangles;        /* >= 0; 0 = an empty scene: every ray misses (the environment) */
     const float* positions;   /* 9*N: v0.xyz v1.xyz v2.xyz          (vertex buffer)      */
     const float* normals;     /* 9*N: per-vertex normals           (attribute slot 0)   */
     const float* uvs;         /* 6*N: per-vertex (u,v)             (attribute slot 1)   */

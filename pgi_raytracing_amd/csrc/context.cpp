@@ -369,8 +369,30 @@ CameraView make_camera(const pgrt_camera& c) {
 
 void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
     PGRT_REQUIRE(d != nullptr, PGRT_ERR_INVALID_ARGUMENT, "scene descriptor is NULL");
+    // An empty scene (an OBJ without faces: Embree commits it and every rtcIntersect1 misses, so
+    // every pixel is the environment, raytracer.cpp:390-393) becomes one zero-area placeholder
+    // triangle at the origin: Ng = 0, so the closest-hit test never accepts it, and every layout
+    // and kernel path stays the non-empty one.  pgrt_bvh_info reports 0 triangles.
+    static const float kZero9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, kZero6[6] = {0, 0, 0, 0, 0, 0};
+    static const int kMat0 = 0;
+    static const pgrt_material kDefaultMat = {{0.4f, 0.4f, 0.4f}, {0.8f, 0.8f, 0.8f}, 1.0f, 1.5f, 0, -1};
+    pgrt_scene_desc placeholder;
+    const bool empty = d->num_triangles == 0;
+    if (empty) {
+        placeholder = *d;
+        placeholder.num_triangles = 1;
+        placeholder.positions = kZero9;
+        placeholder.normals = kZero9;
+        placeholder.uvs = kZero6;
+        placeholder.material_ids = &kMat0;
+        if (placeholder.num_materials == 0) {
+            placeholder.num_materials = 1;
+            placeholder.materials = &kDefaultMat;
+        }
+        d = &placeholder;
+    }
     const int n = d->num_triangles;
-    PGRT_REQUIRE(n > 0 && n < (1 << 27), PGRT_ERR_INVALID_ARGUMENT, "num_triangles must be in [1, 2^27)");
+    PGRT_REQUIRE(n > 0 && n < (1 << 27), PGRT_ERR_INVALID_ARGUMENT, "num_triangles must be in [0, 2^27)");
     PGRT_REQUIRE(d->positions && d->normals && d->uvs && d->material_ids, PGRT_ERR_INVALID_ARGUMENT,
                  "triangle arrays must be non-NULL");
     PGRT_REQUIRE(d->num_materials > 0 && d->materials, PGRT_ERR_INVALID_ARGUMENT, "at least one material required");
@@ -530,7 +552,7 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
     v.lights = ctx->lights.p;
     ctx->has_scene = true;
     pgrt_bvh_info& bi = ctx->info;
-    bi.num_triangles = n;
+    bi.num_triangles = empty ? 0 : n;
     bi.num_nodes = width == 8 ? wide_nodes : bo.num_nodes;
     bi.max_depth = width == 8 ? wide_depth : bo.max_depth;
     bi.width = width;

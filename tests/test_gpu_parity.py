@@ -160,6 +160,54 @@ def test_geosphere_glass_parity(gpu_ctx, geosphere_scene, cfg):
     assert st.rays_refract == sto.rays_refract > 0
 
 
+def test_empty_scene_renders_environment(gpu_ctx, avenger_scene):
+    """A scene without triangles (an OBJ with no faces: Embree commits it, every rtcIntersect1
+    misses) renders the environment map in every pixel, Whitted and path mode, bit-exact with the
+    oracle's empty scene; the closest-hit query reports misses; no material is required."""
+    from pgi_raytracing_amd.scene import Scene
+
+    env = avenger_scene.textures[avenger_scene.env_texture]
+    sc = Scene(np.zeros(0, np.float32), np.zeros(0, np.float32), np.zeros(0, np.float32), np.zeros(0, np.int32),
+               [], [env], 0, [LightData()])
+    gpu_ctx.set_scene(sc)
+    assert gpu_ctx.bvh_info().num_triangles == 0
+    cam = abi.default_camera(90, 60)
+    gpu_ctx.set_camera(cam)
+    orc = pyoracle.OracleScene(sc, accel=1)
+    for p in (abi.make_params(max_level=5), abi.make_params(spp_side=2, max_level=3, dof=1, jitter=abi.PGRT_JITTER_HASH),
+              abi.make_params(max_level=5, mode=abi.PGRT_MODE_PATH)):
+        img, st = gpu_ctx.render(p)
+        ref, sto = orc.render(cam, p)
+        _, exact = assert_frames_match(img, ref)
+        assert exact == 1.0
+        assert st.rays_primary == sto.rays_primary and st.rays_shadow == 0 and st.rays_reflect == 0
+    hits = gpu_ctx.intersect(_random_rays(avenger_scene, 1000, 5))
+    assert (hits[:, 3].view(np.int32) == -1).all()
+
+
+@pytest.mark.parametrize("wh", [(1, 1), (65, 1), (1, 70), (129, 3)])
+def test_degenerate_image_sizes(gpu_ctx, avenger_scene, wh):
+    """Single-pixel, single-row and single-column images (ragged 64x64 tiles of one pixel's
+    width): bit-exact with the oracle, synchronous and batched."""
+    W, H = wh
+    gpu_ctx.set_scene(avenger_scene)
+    cam = abi.make_camera(W, H, abi.deg2rad(42.185), (-140.0, -175.0, 80.0), (0.0, 0.0, 40.0))
+    gpu_ctx.set_camera(cam)
+    p = abi.make_params(spp_side=2, max_level=5, dof=1, jitter=abi.PGRT_JITTER_HASH)
+    img, st = gpu_ctx.render(p)
+    ref, sto = _oracle(avenger_scene).render(cam, p)
+    _, exact = assert_frames_match(img, ref)
+    assert exact == 1.0 and st.rays_primary == sto.rays_primary == 4 * W * H
+    buf = gpu_ctx.alloc(3 * W * H * 16)
+    try:
+        gpu_ctx.render_frames_device(p, 3, buf)
+        out = gpu_ctx.to_host(buf, (3, H, W, 4))
+        same = (out[0] == img) | (np.isnan(out[0]) & np.isnan(img))
+        assert same.all()
+    finally:
+        gpu_ctx.free(buf)
+
+
 def test_rect_render_equals_crop(gpu_ctx, avenger_scene):
     gpu_ctx.set_scene(avenger_scene)
     cam = abi.default_camera(200, 150)
