@@ -208,6 +208,12 @@ typedef struct pgrt_config {
                              order (default), 1 = sibling pairs (the two children of a node in one
                              128-B line, pairs in depth-first order; neutral on C2 / C5,
                              profiles/r3/ab_r3u_bvh_layout.txt) */
+    int call_order;       /* frames in flight: 1 = each call's level-0 trace waits for the previous
+                             call's level-0 shade (the bulk work of the calls in submission order,
+                             their latency-bound deeper levels overlapping the next call's bulk);
+                             -1 = calls share the GPU freely; 0 = default: ordered for scenes above
+                             262144 triangles (C5 -7 %; the avenger's C2 / C3 lose when ordered,
+                             profiles/r3/ab_r3ab_call_order.txt) */
 } pgrt_config;
 
 /* ---- context ---- */

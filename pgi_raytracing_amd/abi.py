@@ -131,6 +131,7 @@ class Config(C.Structure):
         ("tail_level", C.c_int),
         ("packet_width", C.c_int),
         ("bvh_layout", C.c_int),
+        ("call_order", C.c_int),
     ]
 
 

@@ -262,6 +262,10 @@ struct pgrt_ctx {
     // frame state: frames in flight (set 0 serves the synchronous entry points), each with its
     // independent pipeline slots (tile subsets) on their own streams
     std::vector<std::unique_ptr<FrameSet>> sets;
+    // pgrt_config.call_order: recorded after a call's level-0 shade; the next call's level-0
+    // trace waits for it (calls in flight take the GPU's bulk work in submission order)
+    hipEvent_t l0_token = nullptr;
+    bool l0_token_live = false;
     int frames_in_flight = 1;
     unsigned long long next_ticket = 1;
     DevBuf<int> gstack;        // pgrt_intersect_closest
@@ -304,6 +308,7 @@ struct pgrt_ctx {
             delete m;
         }
         (void)hipSetDevice(device);
+        if (l0_token) (void)hipEventDestroy(l0_token);
         if (comm_ctl) (void)ncclCommDestroy(comm_ctl);
         if (ctl_stream) (void)hipStreamDestroy(ctl_stream);
         if (comm) (void)ncclCommDestroy(comm);
@@ -751,6 +756,15 @@ int tail_first(const pgrt_ctx* ctx, const SceneView& view, const pgrt_render_par
 }
 
 // step budget of the bounce levels' packet launches (pgrt_config.packet_budget)
+// pgrt_config.call_order: level 0 of calls in flight in submission order -- by default for big
+// scenes only (BVH far beyond the L2: concurrent level-0 launches share the MALL and each other's
+// misses; r3ab A/B: C5 18.1 -> 16.9 ms/frame, while the avenger's C2 / C3 lose 7 % / 87 % when
+// their small, cache-resident level 0 is serialised)
+bool call_ordered(const pgrt_ctx* ctx, const SceneView& view) {
+    const int c = ctx->cfg.call_order;
+    return c == 1 || (c == 0 && view.ntri > kPacketBigScene);
+}
+
 int packet_budget(const pgrt_ctx* ctx) {
     const int b = ctx->cfg.packet_budget;
     return b < 0 ? 0 : (b == 0 ? kDefaultPacketBudget : b);
@@ -1021,6 +1035,8 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                     debug_sync(s, "bin", L, bi);
                     tl.perm = sl->q_perm.p;
                 }
+                const bool ordered = L == 0 && K == 1 && ctx->frames_in_flight > 1 && call_ordered(ctx, view);
+                if (ordered && ctx->l0_token_live) PGRT_HIP(hipStreamWaitEvent(s, ctx->l0_token, 0));
                 id = ctx->timer.begin_kernel(CAT_TRACE, CAT_LTRACE + L);
                 const bool launched = launch_trace(view, tl, s);
                 ctx->timer.end_kernel(s, id, launched);
@@ -1032,6 +1048,11 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                              L == 0 ? l0f : L0Final{nullptr, nullptr, fo, nullptr});
                 debug_sync(s, "shade", L, bi);
                 ctx->timer.end(s, id);
+                if (ordered) {
+                    if (!ctx->l0_token) PGRT_HIP(hipEventCreateWithFlags(&ctx->l0_token, hipEventDisableTiming));
+                    PGRT_HIP(hipEventRecord(ctx->l0_token, s));
+                    ctx->l0_token_live = true;
+                }
             }
             if (view.nlight > 0 && p->max_level > 0) {  // every level's shadow rays, one launch
                 TraceLaunch tl;
@@ -1774,6 +1795,8 @@ int pgrt_set_config(pgrt_ctx* ctx, const pgrt_config* cfg) {
                      "packet_budget must be -1 (off), 0 (default) or a step count");
         PGRT_REQUIRE(cfg->tail_level >= -1 && cfg->tail_level < kMaxLevels, PGRT_ERR_INVALID_ARGUMENT,
                      "tail_level must be 0 / -1 (off, the default) or a level in [1, 15]");
+        PGRT_REQUIRE(cfg->call_order == 0 || cfg->call_order == 1 || cfg->call_order == -1, PGRT_ERR_INVALID_ARGUMENT,
+                     "call_order must be 0 (default), 1 (level 0 in submission order) or -1 (free)");
         PGRT_REQUIRE(cfg->bvh_layout == 0 || cfg->bvh_layout == 1, PGRT_ERR_INVALID_ARGUMENT,
                      "bvh_layout must be 0 (builder order) or 1 (sibling pairs)");
         PGRT_REQUIRE(cfg->packet_width == 0 || cfg->packet_width == 2 || cfg->packet_width == 8,

@@ -1040,8 +1040,6 @@ constexpr int kGroup8Max = 150000;
 // queues up to kTailMax rays spread over more waves: kTailRpw rays per wave (r1 A/B: 64, i.e.
 // full waves, was best)
 constexpr int kTailMax = 131072, kTailRpw = 64;
-// scenes above this many triangles take the 8-wave level-0 packet kernel (k_trace_pkt MINW)
-constexpr int kPacketBigScene = 262144;
 
 bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) {
     const int max_count = t.max_count;
