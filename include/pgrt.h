@@ -185,7 +185,7 @@ typedef struct pgrt_config {
                              as wave packets, deeper levels one lane per ray */
     int group_max;        /* queues of <= group_max rays: 8 lanes per ray over the 8-wide BVH;
                              0 = default (400k synchronous, 100k with frames in flight), -1 never */
-    long long max_batch_rays;  /* level-0 rays per sample batch (0 = 16M); smaller values split a
+    long long max_batch_rays;  /* level-0 rays per sample batch (0 = 32M); smaller values split a
                                   frame's samples into more batches (queue memory vs launches) */
     int max_batches_in_flight; /* sample batches queued across frames in flight (0 = no bound) */
     int rank0_share_a, rank0_share_b; /* distributed frames: rank 0 renders a tiles for every b of

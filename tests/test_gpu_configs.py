@@ -55,7 +55,7 @@ def test_c3_multi_batch_64spp_dof(gpu_ctx, avenger_scene):
 
 
 def test_c3_full_size_default_batching_rows(gpu_ctx, avenger_scene):
-    """C3 at its full size (1920x1080, DoF, 64 spp) through the default sample batching (16M
+    """C3 at its full size (1920x1080, DoF, 64 spp) through the default sample batching (32M
     level-0 rays per batch: several batches per frame, each frame's accumulation over them) and
     frames in flight: every 64th row equals the CPU restatement's bit for bit, and those rows
     rendered as GPU rects give the oracle's ray counts per kind exactly (raytracer.cpp:396-437)."""
