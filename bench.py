@@ -105,6 +105,8 @@ def parse():
                     help="A/B only: pgrt_config.packet_levels (default AUTO: chosen per level by libpgrt)")
     ap.add_argument("--group-max", type=int, default=None,
                     help="A/B only: pgrt_config.group_max (queues up to it: 8 lanes per ray)")
+    ap.add_argument("--remainder-first", action="store_true",
+                    help="submit the short call (steps %% frames-per-call frames) first instead of last")
     ap.add_argument("--cfg", action="append", default=[],
                     help="A/B only: pgrt_config field=value (repeatable), e.g. --cfg bvh_width=8")
     a = ap.parse_args()
@@ -342,8 +344,11 @@ def main():
                 gather_ms.append(st.ms_gather)
             return st.rays()
 
-        for k, f0 in enumerate(range(0, n, F)):
-            nf = min(F, n - f0)
+        # call sizes: F frames each, the remainder of n / F either last or (--remainder-first) first
+        sizes = [F] * (n // F)
+        if n % F:
+            sizes = [n % F] + sizes if args.remainder_first else sizes + [n % F]
+        for k, nf in enumerate(sizes):
             pc = params
             out = fb
             if distinct:

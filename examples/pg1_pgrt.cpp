@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <string>
+#include <memory>
 #include <vector>
 
 #include "pgrt_raytracer.hpp"
@@ -52,12 +53,23 @@ static int tutorial_1() {
 
 static int render(int argc, char** argv) {
     if (argc < 5) {
-        std::fprintf(stderr, "usage: %s render <obj> <env> <out.raw> [W H S d dof]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s render <obj> <env> <out.raw> [W H S d dof [devices]]\n", argv[0]);
         return 2;
     }
     const int W = argc > 5 ? std::atoi(argv[5]) : 640, H = argc > 6 ? std::atoi(argv[6]) : 480;
-    pgrt::Raytracer raytracer(W, H, pgrt::deg2rad(42.185f), pgrt::Vector3(-140.0f, -175.0f, 80.0f),
-                              pgrt::Vector3(0.0f, 0.0f, 40.0f));
+    // optional 11th argument: HIP devices "0,1,..." -> one process renders on all of them
+    std::vector<int> devices;
+    if (argc > 10)
+        for (const char* q = argv[10]; *q;) {
+            devices.push_back(std::atoi(q));
+            while (*q && *q != ',') ++q;
+            if (*q == ',') ++q;
+        }
+    const pgrt::Vector3 from(-140.0f, -175.0f, 80.0f), at(0.0f, 0.0f, 40.0f);
+    std::unique_ptr<pgrt::Raytracer> rt =
+        devices.empty() ? std::make_unique<pgrt::Raytracer>(W, H, pgrt::deg2rad(42.185f), from, at)
+                        : std::make_unique<pgrt::Raytracer>(W, H, pgrt::deg2rad(42.185f), from, at, devices);
+    pgrt::Raytracer& raytracer = *rt;
     raytracer.LoadScene(argv[2], argv[3]);
     auto& p = raytracer.params();
     p.spp_side = argc > 7 ? std::atoi(argv[7]) : 3;

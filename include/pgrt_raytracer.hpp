@@ -105,6 +105,23 @@ public:
               const Vector3 view_at, const int hip_device = 0)
         : camera_(width, height, fov_y, view_from, view_at) {
         check(nullptr, pgrt_create(hip_device, &ctx_), "pgrt_create");
+        init();
+    }
+    // one process, several GPUs (pgrt_create_devices): every frame is rendered tile-wise on all of
+    // hip_devices and gathered on hip_devices[0]; the rest of the class is unchanged
+    Raytracer(const int width, const int height, const float fov_y, const Vector3 view_from,
+              const Vector3 view_at, const std::vector<int>& hip_devices)
+        : camera_(width, height, fov_y, view_from, view_at) {
+        check(nullptr, pgrt_create_devices(hip_devices.data(), (int)hip_devices.size(), &ctx_),
+              "pgrt_create_devices");
+        init();
+    }
+    ~Raytracer() { pgrt_destroy(ctx_); }
+    Raytracer(const Raytracer&) = delete;
+    Raytracer& operator=(const Raytracer&) = delete;
+
+private:
+    void init() {
         pgrt_camera c = camera_.desc();
         check(ctx_, pgrt_set_camera(ctx_, &c), "pgrt_set_camera");
         params_.spp_side = 3;          // raytracer.cpp:398
@@ -116,10 +133,8 @@ public:
         params_.jitter = PGRT_JITTER_HASH;
         params_.seed = 1234;
     }
-    ~Raytracer() { pgrt_destroy(ctx_); }
-    Raytracer(const Raytracer&) = delete;
-    Raytracer& operator=(const Raytracer&) = delete;
 
+public:
     float gamma_level = 0.5f;  // UI slider default (raytracer.cpp:450,464-465)
 
     // LoadScene (raytracer.cpp:48-128): LoadOBJ + SphericalMap + one white light, then the

@@ -42,3 +42,20 @@ def test_raytrace_loop_frame_matches_oracle(tmp_path, avenger_obj, avenger_scene
     _, exact = assert_frames_match(img, ref)
     assert exact == 1.0
     assert os.path.getsize(str(raw) + ".pfm") > W * H * 12
+
+
+def test_raytrace_loop_single_process_multi_device(tmp_path, avenger_obj, avenger_scene):
+    """The same C++ raytrace_loop with the facade's multi-device constructor (pgrt_create_devices,
+    ranks 0,0,0 -- three ranks on this box's one GPU, gathered by device copies): the frame is
+    the oracle's bit for bit."""
+    raw = tmp_path / "frame_md.raw"
+    W, H, S, d, dof = 200, 130, 2, 5, 1
+    out = subprocess.run([EXE, "render", avenger_obj, ENV_MAP, str(raw), str(W), str(H), str(S), str(d), str(dof),
+                          "0,0,0"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    img = np.fromfile(raw, np.float32).reshape(H, W, 4)
+    cam = abi.default_camera(W, H)
+    p = abi.make_params(spp_side=S, max_level=d, dof=dof, jitter=abi.PGRT_JITTER_HASH, seed=1234)
+    ref, _ = pyoracle.OracleScene(avenger_scene).render(cam, p)
+    _, exact = assert_frames_match(img, ref)
+    assert exact == 1.0
