@@ -208,6 +208,30 @@ def test_degenerate_image_sizes(gpu_ctx, avenger_scene, wh):
         gpu_ctx.free(buf)
 
 
+def test_maximum_depth_and_samples(gpu_ctx, avenger_scene, geosphere_scene):
+    """The largest parameters pgrt_render_params accepts: max_level 14 (kMaxLevels - 2) on the
+    all-glass geosphere (refraction trees as deep as the queues allow, re-grown on overflow) and
+    spp_side 64 (4096 samples per pixel, many sample batches) on a few pixels -- bit-exact with
+    the oracle."""
+    gpu_ctx.set_scene(geosphere_scene)
+    cam = abi.make_camera(48, 36, abi.deg2rad(90.0), (2.0, 0.0, 0.0), (0.0, 0.0, 0.0))
+    gpu_ctx.set_camera(cam)
+    p = abi.make_params(spp_side=2, max_level=14, jitter=abi.PGRT_JITTER_HASH)
+    img, st = gpu_ctx.render(p)
+    ref, sto = _oracle(geosphere_scene).render(cam, p)
+    _, exact = assert_frames_match(img, ref)
+    assert exact == 1.0 and st.levels == 15
+    assert (st.rays_reflect, st.rays_refract) == (sto.rays_reflect, sto.rays_refract)
+    gpu_ctx.set_scene(avenger_scene)
+    cam = abi.default_camera(8, 4)
+    gpu_ctx.set_camera(cam)
+    p = abi.make_params(spp_side=64, max_level=5, dof=1, jitter=abi.PGRT_JITTER_HASH)
+    img, st = gpu_ctx.render(p)
+    ref, sto = _oracle(avenger_scene).render(cam, p)
+    _, exact = assert_frames_match(img, ref)
+    assert exact == 1.0 and st.rays_primary == sto.rays_primary == 4096 * 32
+
+
 def test_rect_render_equals_crop(gpu_ctx, avenger_scene):
     gpu_ctx.set_scene(avenger_scene)
     cam = abi.default_camera(200, 150)
