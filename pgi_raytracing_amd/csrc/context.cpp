@@ -1151,7 +1151,10 @@ bool read_frame_counters(pgrt_ctx* ctx, FrameSet* fs) {
                 dc = std::max(dc, h.defer[L]);
             }
             hint(sl->expect_count[L], c);
-            hint(sl->expect_defer[L], dc);
+            // deferral hints only from frames that deferred: a level traced without packets (AUTO
+            // turned it off) defers nothing, and its next packet frame (a probe) needs the grid
+            // its last packet frame needed, not the minimum
+            if (dc > 0) hint(sl->expect_defer[L], dc);
         }
         hint(sl->expect_shadow_total, shadow_need);
     }

@@ -1097,7 +1097,11 @@ bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) 
         }
 #undef PGRT_LAUNCH_P
         if (budget) {  // the deferred rays: 8 lanes per ray, from the packet's closest hits
-            const int dex = std::max(t.defer_expect, 1024);
+            // grid from the previous deferral count; with none known (a level's first packet frame,
+            // e.g. AUTO's start or probe on an incoherent scene, where most waves run out of steps),
+            // from the level's rays -- a 1024-ray grid striding over millions of deferred rays made
+            // single launches of 0.1-0.4 s on C5 (profiles/r3/c5_kernel_stats_r3fin.csv)
+            const int dex = std::max(t.defer_expect > 0 ? t.defer_expect : ex, 1024);
             const int g8 = std::min(16384, ceil_div(dex, kTraceBlock / 8));
             if (t.count)
                 hipExtLaunchKernelGGL((k_trace8g<true, 8, true>), dim3(g8), dim3(kTraceBlock), 0, stream, nullptr,
