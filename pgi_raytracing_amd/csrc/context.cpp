@@ -767,9 +767,17 @@ bool call_ordered(const pgrt_ctx* ctx, const SceneView& view) {
     return c == 1 || (c == 0 && view.ntri > kPacketBigScene);
 }
 
-int packet_budget(const pgrt_ctx* ctx) {
+// The default budget follows the level's expected ray count: a small queue (one synchronous
+// frame: ~220k rays on level 1, a few waves per SIMD) is bound by its slowest waves, so they hand
+// over early (r3f: one-frame level 1 576 -> 309 us at 256 steps, 181 us at 64); a big one (8 frames
+// per call: level 1 ~1.7M rays, tens of waves per SIMD) keeps its waves on packets longer, where 8
+// lanes per deferred ray would cost throughput.  Whitted frames of scenes up to kPacketBigScene
+// triangles only: C5's 10^6-triangle soup and the path tracer's diffuse bounces defer far more rays
+// at 64 steps and lose 8-9 % (profiles/r3/ab_r3ak_small_budget.txt; the resume grid was not the cause)
+int packet_budget(const pgrt_ctx* ctx, int expect, bool small_ok) {
     const int b = ctx->cfg.packet_budget;
-    return b < 0 ? 0 : (b == 0 ? kDefaultPacketBudget : b);
+    if (b != 0) return b < 0 ? 0 : b;
+    return small_ok && expect < kSmallPacketQueue ? kSmallQueuePacketBudget : kDefaultPacketBudget;
 }
 
 // One sample batch of a PGRT_MODE_PATH frame (path.hip): raygen, then per bounce L the closest
@@ -808,7 +816,7 @@ void enqueue_path_batch(pgrt_ctx* ctx, FrameSlot* sl, const SceneView& view, con
         tl.count = p->profile >= 2;
         tl.packets = packet_level(ctx, L);
         tl.pkt_util = fcd->pkt[L];
-        tl.budget = packet_budget(ctx);
+        tl.budget = packet_budget(ctx, ex, false);
         tl.wide_packets = L > 0 && ctx->cfg.packet_width == 8;
         tl.defer_list = sl->q_defer.p;
         tl.defer_count = &fcd->defer[L];
@@ -1025,7 +1033,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 tl.packets = packet_level(ctx, L);  // coherent 8x8-pixel waves -> packet traversal
                 tl.gen = L == 0 && fuse ? &gen : nullptr;
                 tl.pkt_util = fcd->pkt[L];
-                tl.budget = packet_budget(ctx);
+                tl.budget = packet_budget(ctx, ex, view.ntri <= kPacketBigScene);
                 tl.wide_packets = L > 0 && ctx->cfg.packet_width == 8;
                 tl.defer_list = sl->q_defer.p;
                 tl.defer_count = &fcd->defer[L];
