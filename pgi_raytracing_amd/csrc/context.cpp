@@ -767,17 +767,18 @@ bool call_ordered(const pgrt_ctx* ctx, const SceneView& view) {
     return c == 1 || (c == 0 && view.ntri > kPacketBigScene);
 }
 
-// The default budget follows the level's expected ray count: a small queue (one synchronous
-// frame: ~220k rays on level 1, a few waves per SIMD) is bound by its slowest waves, so they hand
-// over early (r3f: one-frame level 1 576 -> 309 us at 256 steps, 181 us at 64); a big one (8 frames
-// per call: level 1 ~1.7M rays, tens of waves per SIMD) keeps its waves on packets longer, where 8
-// lanes per deferred ray would cost throughput.  Whitted frames of scenes up to kPacketBigScene
-// triangles only: C5's 10^6-triangle soup and the path tracer's diffuse bounces defer far more rays
-// at 64 steps and lose 8-9 % (profiles/r3/ab_r3ak_small_budget.txt; the resume grid was not the cause)
-int packet_budget(const pgrt_ctx* ctx, int expect, bool small_ok) {
+// The default budget follows the batch size: a one-frame batch (its bounce levels ~220k, ~100k
+// rays: a few waves per SIMD) is bound by its slowest waves, so they hand over early (r3f:
+// one-frame level 1 576 -> 309 us at 256 steps, 181 us at 64); a batch of several frames (8 per
+// call: level 1 ~1.7M rays, tens of waves per SIMD) keeps its waves on packets longer, where 8
+// lanes per deferred ray would cost throughput.  Decided by the batch's level-0 rays, not by the
+// slot's queue hints (those describe whatever batch the slot rendered last).  Whitted frames of
+// scenes up to kPacketBigScene triangles only: C5's 10^6-triangle soup and the path tracer's
+// diffuse bounces defer far more rays at 64 steps and lose 8-9 % (profiles/r3/ab_r3ak_small_budget.txt)
+int packet_budget(const pgrt_ctx* ctx, bool small_batch) {
     const int b = ctx->cfg.packet_budget;
     if (b != 0) return b < 0 ? 0 : b;
-    return small_ok && expect < kSmallPacketQueue ? kSmallQueuePacketBudget : kDefaultPacketBudget;
+    return small_batch ? kSmallBatchPacketBudget : kDefaultPacketBudget;
 }
 
 // One sample batch of a PGRT_MODE_PATH frame (path.hip): raygen, then per bounce L the closest
@@ -816,7 +817,7 @@ void enqueue_path_batch(pgrt_ctx* ctx, FrameSlot* sl, const SceneView& view, con
         tl.count = p->profile >= 2;
         tl.packets = packet_level(ctx, L);
         tl.pkt_util = fcd->pkt[L];
-        tl.budget = packet_budget(ctx, ex, false);
+        tl.budget = packet_budget(ctx, false);
         tl.wide_packets = L > 0 && ctx->cfg.packet_width == 8;
         tl.defer_list = sl->q_defer.p;
         tl.defer_count = &fcd->defer[L];
@@ -1033,7 +1034,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 tl.packets = packet_level(ctx, L);  // coherent 8x8-pixel waves -> packet traversal
                 tl.gen = L == 0 && fuse ? &gen : nullptr;
                 tl.pkt_util = fcd->pkt[L];
-                tl.budget = packet_budget(ctx, ex, view.ntri <= kPacketBigScene);
+                tl.budget = packet_budget(ctx, n0 < kSmallPacketBatch && view.ntri <= kPacketBigScene);
                 tl.wide_packets = L > 0 && ctx->cfg.packet_width == 8;
                 tl.defer_list = sl->q_defer.p;
                 tl.defer_count = &fcd->defer[L];

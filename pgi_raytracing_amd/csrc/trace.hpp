@@ -274,9 +274,10 @@ constexpr int kDefaultGroupMaxInFlight = 100000;  // with frames in flight the c
 // pgrt_config.packet_budget default: node / triangle steps a bounce-level packet wave takes before
 // its rays go to the 8-lanes-per-ray kernel (calibrated on C2)
 constexpr int kDefaultPacketBudget = 256;
-// levels expected below kSmallPacketQueue rays take the shorter budget (context.cpp packet_budget)
-constexpr int kSmallPacketQueue = 1 << 19;
-constexpr int kSmallQueuePacketBudget = 64;
+// batches below kSmallPacketBatch level-0 rays (one 1080p frame: 2.1M) take the shorter budget
+// on their bounce levels (context.cpp packet_budget)
+constexpr int kSmallPacketBatch = 1 << 22;
+constexpr int kSmallBatchPacketBudget = 64;
 // "big" scenes (BVH + triangles far beyond the L2, fetches served by the MALL / HBM): the
 // level-0 packet kernel is built for 8 waves (trace.hip), level 0 of calls in flight is ordered
 // (context.cpp call_ordered)
