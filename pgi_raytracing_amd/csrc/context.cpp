@@ -1033,8 +1033,11 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 tl.count = p->profile >= 2;
                 tl.packets = packet_level(ctx, L);  // coherent 8x8-pixel waves -> packet traversal
                 tl.gen = L == 0 && fuse ? &gen : nullptr;
-                tl.pkt_util = fcd->pkt[L];
                 tl.budget = packet_budget(ctx, n0 < kSmallPacketBatch && view.ntri <= kPacketBigScene);
+                // AUTO samples the packet utilisation of default-budget launches only: a wave cut
+                // short at 64 steps reads as better used than it is, and one-frame batches would
+                // then switch levels to packets for the multi-frame calls too
+                tl.pkt_util = tl.budget == kSmallBatchPacketBudget && ctx->cfg.packet_budget == 0 ? nullptr : fcd->pkt[L];
                 tl.wide_packets = L > 0 && ctx->cfg.packet_width == 8;
                 tl.defer_list = sl->q_defer.p;
                 tl.defer_count = &fcd->defer[L];
