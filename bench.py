@@ -63,7 +63,8 @@ CONFIGS = {
 # PMC-measured HBM traffic per closest-hit launch of the bench's profiled configuration
 # (tools/profile.sh + tools/traffic.py, committed under profiles/)
 TRAFFIC = {"C2": "profiles/r3/traffic_C2.json", "C3": "profiles/r3/traffic_C3.json",
-           "C5": "profiles/r3/traffic_C5.json", "C2-path": "profiles/r2/traffic_C2-path.json"}
+           "C4": "profiles/r3/traffic_C4.json", "C5": "profiles/r3/traffic_C5.json",
+           "C2-path": "profiles/r2/traffic_C2-path.json"}
 
 
 def parse():

@@ -11,7 +11,6 @@ timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > "gpurun_out/bench_${T
 for cfg in C2 C3 C4 C5; do
     extra=""
     steps=""
-    [ $cfg = C4 ] && extra="--no-cpu-baseline"
     [ $cfg = C3 ] && steps="--steps 20 --warmup 3"
     [ $cfg = C4 ] && steps="--steps 6 --warmup 2"
     [ $cfg = C5 ] && steps="--steps 20 --warmup 3"
