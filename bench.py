@@ -254,6 +254,21 @@ def workload(args) -> str:
 
 # ------------------------------------------------------------------ main
 
+class _stdout_to_stderr:
+    """fd 1 -> fd 2 while native libraries initialise: stdout carries only rank 0's JSON line."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -320,10 +335,11 @@ def main():
     comm_ranks = 1
     distributed = world > 1 or args.dist_path
     if distributed:
-        uid = [Context.comm_unique_id() if rank == 0 else None]
-        if dist:
-            dist.broadcast_object_list(uid, src=0)
-        ctx.comm_init(world, rank, uid[0])
+        with _stdout_to_stderr():  # RCCL prints its version banner on stdout at init
+            uid = [Context.comm_unique_id() if rank == 0 else None]
+            if dist:
+                dist.broadcast_object_list(uid, src=0)
+            ctx.comm_init(world, rank, uid[0])
         comm_ranks, _ = ctx.comm_info()
 
     def frame(p):  # synchronous frame (latency, profiled frames)
