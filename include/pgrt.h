@@ -197,7 +197,8 @@ typedef struct pgrt_config {
                              no gain on C2, profiles/r3/ab_r3c_binning.txt) */
     int packet_budget;    /* bounce levels traced as wave packets: a wave still traversing after this
                              many node / triangle steps hands its rays (with their closest hits so
-                             far) to the 8-lanes-per-ray kernel; 0 = default, -1 = no budget */
+                             far) to the 8-lanes-per-ray kernel; 0 = default (64 steps for one-frame
+                             batches of scenes up to 262144 triangles, 256 otherwise), -1 = no budget */
     int tail_level;       /* k >= 1: Whitted levels >= k run as ONE persistent launch that hands each
                              ray's children to the next level as soon as they exist (device-side
                              level iteration); 0 / -1 = one launch per level (the default: the
