@@ -240,6 +240,130 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
     }
 }
 
+// ---------------------------------------------------------------- one lane per ray, lane refill
+//
+// k_trace's waves trace 64 rays in lockstep: a lane whose ray ends early idles until the wave's
+// longest ray is done, so an incoherent queue (bounce levels, shadow rays) keeps a fraction of
+// its lanes busy.  Here a wave owns a fixed sequence of queue slots (row r, column c: slot
+// r * 64 * waves + 64 * wave + c) and walks it with a wave-uniform cursor: once at least
+// `min_idle` lanes have finished their rays, they take the next slots in one step (ballot +
+// mbcnt, no atomics), so the lanes stay busy until the wave's sequence runs out (Aila & Laine
+// 2009, "replacing terminated rays").  Per-ray arithmetic and visit order are k_trace's (same
+// node loop, LDS stack, postponed leaves), so the hit records are identical.
+__global__ __launch_bounds__(kTraceBlock) void k_trace_rf(SceneView s, const float4* __restrict__ ro,
+                                                          const float4* __restrict__ rd,
+                                                          float4* __restrict__ hits,
+                                                          const int* __restrict__ count_dev, int count_terms,
+                                                          int count_host, int cap, float4 const_org,
+                                                          unsigned char* __restrict__ lit,
+                                                          const int* __restrict__ perm, int min_idle) {
+    extern __shared__ int lstack[];  // [depth + 2][kTraceBlock]
+    const int tid = threadIdx.x;
+    const int n = ray_count(count_dev, count_terms, count_host, cap);
+    const int wave = (blockIdx.x * kTraceBlock + tid) >> 6;
+    const unsigned wstride = gridDim.x * kTraceBlock;  // 64 x waves
+    unsigned next = 0;                                 // the wave's next sequence position (uniform)
+    auto slot_of = [&](unsigned q) -> unsigned { return (q >> 6) * wstride + (unsigned)wave * 64u + (q & 63u); };
+    bool exhausted = slot_of(0) >= (unsigned)n;
+    int i = -1;  // the lane's ray (queue index), -1 = idle
+    float ox = 0, oy = 0, oz = 0, tnear = 0, dx = 0, dy = 0, dz = 0, tfar = 0;
+    float idx = 0, idy = 0, idz = 0, oix = 0, oiy = 0, oiz = 0;
+    float best_t = 0, best_u = 0, best_v = 0;
+    int best_prim = -1, sp = 0, node = kSentinel, leaf = 0;
+    for (;;) {
+        // ---- refill: idle lanes take the wave's next slots ----
+        const unsigned long long im = __ballot(i < 0);
+        const int nidle = __popcll(im);
+        if (!exhausted && (nidle >= min_idle || nidle == 64)) {
+            if (i < 0) {
+                const unsigned q = next + __builtin_amdgcn_mbcnt_hi((unsigned)(im >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((unsigned)im, 0u));
+                const unsigned sl = slot_of(q);
+                if (sl < (unsigned)n) {
+                    i = perm ? perm[sl] : (int)sl;
+                    const float4 o4 = ro ? ro[i] : const_org;
+                    const float4 d4 = rd[i];
+                    ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
+                    dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
+                    const float sdx = fabsf(dx) < 1e-30f ? copysignf(1e-30f, dx) : dx;
+                    const float sdy = fabsf(dy) < 1e-30f ? copysignf(1e-30f, dy) : dy;
+                    const float sdz = fabsf(dz) < 1e-30f ? copysignf(1e-30f, dz) : dz;
+                    idx = __builtin_amdgcn_rcpf(sdx), idy = __builtin_amdgcn_rcpf(sdy), idz = __builtin_amdgcn_rcpf(sdz);
+                    oix = ox * idx, oiy = oy * idy, oiz = oz * idz;
+                    best_t = tfar, best_u = 0.0f, best_v = 0.0f;
+                    best_prim = -1;
+                    sp = 0;
+                    lstack[tid] = kSentinel;  // stack[0]
+                    node = s.root;
+                    leaf = 0;
+                    if (node < 0) {
+                        leaf = node;
+                        node = kSentinel;
+                    }
+                    if (!(tfar >= 0.0f)) {  // padding slots / empty segments: no traversal
+                        node = kSentinel;
+                        leaf = 0;
+                    }
+                }
+            }
+            next += (unsigned)nidle;
+            exhausted = slot_of(next) >= (unsigned)n;
+        }
+        if (!__any(i >= 0)) break;  // no ray left in the wave, and the sequence is exhausted
+        // ---- descend internal nodes until every active lane has parked a leaf ----
+        const float bt = __builtin_canonicalizef(best_t);
+        while ((unsigned)node < (unsigned)kSentinel) {
+            const int top = lstack[sp * kTraceBlock + tid];
+            const BvhNode* nd = s.nodes + node;
+            const float4 a = nd->a, b = nd->b, c = nd->c;
+            const int4 d = nd->d;
+            float t0, t1;
+            const bool h0 = box_hit(a.x, a.y, a.z, a.w, c.x, c.y, idx, idy, idz, oix, oiy, oiz, bt, t0);
+            const bool h1 = box_hit(b.x, b.y, b.z, b.w, c.z, c.w, idx, idy, idz, oix, oiy, oiz, bt, t1);
+            const bool any = h0 || h1;
+            const bool first0 = h0 && (!h1 || t0 <= t1);
+            const bool both = h0 && h1;
+            lstack[(sp + 1) * kTraceBlock + tid] = first0 ? d.y : d.x;
+            node = any ? (first0 ? d.x : d.y) : top;
+            sp += both ? 1 : (any ? 0 : -1);
+            if (node < 0 && leaf == 0) {  // first leaf: park it and keep descending
+                leaf = node;
+                node = lstack[sp * kTraceBlock + tid];
+                --sp;
+            }
+            if (!__any(leaf == 0)) break;
+        }
+        // ---- triangle tests for the parked leaves ----
+        while (leaf < 0) {
+            const int first = leaf_first(leaf), end = first + leaf_count(leaf);
+            float4 p0 = s.tri[3 * first], p1 = s.tri[3 * first + 1], p2 = s.tri[3 * first + 2];
+            for (int k = first; k < end; ++k) {
+                const float4 q0 = p0, q1 = p1, q2 = p2;
+                if (k + 1 < end) {
+                    p0 = s.tri[3 * k + 3];
+                    p1 = s.tri[3 * k + 4];
+                    p2 = s.tri[3 * k + 5];
+                }
+                tri_test(q0, q1, q2, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v, best_prim);
+            }
+            leaf = 0;
+            if (node < 0) {  // the node popped after parking is a leaf too: test it now
+                leaf = node;
+                node = lstack[sp * kTraceBlock + tid];
+                --sp;
+            }
+        }
+        // ---- finished rays: write the record, the lane goes idle ----
+        if (i >= 0 && node == kSentinel) {
+            if (lit)  // is_illuminated (raytracer.cpp:163-173): no hit, or the occluder is dielectric
+                lit[i] = (best_prim < 0 || s.prim_glass[best_prim] != 0) ? 1 : 0;
+            else
+                hits[i] = make_float4(best_t, best_u, best_v, __int_as_float(best_prim));
+            i = -1;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- 8-wide traversal
 //
 // Stack entries are node groups (child_base, hit bits << 24 | imask): the children of one wide
@@ -1041,6 +1165,22 @@ constexpr int kGroup8Max = 150000;
 // full waves, was best)
 constexpr int kTailMax = 131072, kTailRpw = 64;
 
+// one-lane queues of full waves: lane refill (k_trace_rf) once this many lanes of a wave are
+// idle; 0 = lockstep k_trace.  PGRT_REFILL overrides (A/B), PGRT_REFILL_GRID scales the grid
+// (resident blocks x factor).
+static int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+static int refill_min_idle() {
+    static const int v = env_int("PGRT_REFILL", 0);
+    return v;
+}
+static int refill_blocks_factor() {
+    static const int v = std::max(1, env_int("PGRT_REFILL_GRID", 1));
+    return v;
+}
+
 bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) {
     const int max_count = t.max_count;
     if (max_count <= 0) return false;
@@ -1136,7 +1276,29 @@ bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) 
     const int entries = s.depth + 2;
     const bool spill = entries * kTraceBlock * 4 > 65536;
     const size_t lds = (size_t)(spill ? kLdsStack : entries) * kTraceBlock * sizeof(int);
-#define PGRT_LAUNCH(C, S)                                                                                       \
+    const int min_idle = refill_min_idle();
+    if (min_idle > 0 && !t.count && !spill && rpw == 64) {
+        // lane refill: a grid of resident blocks, each wave walking its own slot sequence
+        static int cus = 0, resident = 0;
+        static size_t resident_lds = 0;
+        if (!cus) {
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            cus = std::max(1, cus);
+        }
+        if (resident_lds != lds) {  // blocks resident per CU at this stack size (VGPRs and LDS)
+            int per_cu = 0;
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_rf, kTraceBlock, lds);
+            resident = std::max(1, per_cu) * cus;
+            resident_lds = lds;
+        }
+        const int rgrid = std::min(ceil_div(ex, kTraceBlock), resident * refill_blocks_factor());
+        PGRT_TLAUNCH(k_trace_rf, dim3(rgrid), dim3(kTraceBlock), lds, stream, s, t.ro, t.rd, t.hits, t.count_dev,
+                     t.count_terms, t.count_host, max_count, t.const_org, t.lit, t.perm, min_idle);
+        return true;
+    }
+#define PGRT_LAUNCH(C, S)                                                                                      \
     PGRT_TLAUNCH((k_trace<C, S>), dim3(grid), dim3(kTraceBlock), lds, stream, s, t.ro, t.rd, t.hits, t.count_dev, \
                  t.count_terms, t.count_host, max_count, t.gstack, t.counters, rpw, t.const_org, t.lit, t.perm)
     if (t.count) {
