@@ -799,3 +799,44 @@ def test_frames_in_flight_match_synchronous(gpu_ctx, avenger_scene):
         gpu_ctx.set_frames_in_flight(1)
         for b in bufs:
             gpu_ctx.free(b)
+
+
+_REFILL_CHILD = r"""
+import os, sys
+import numpy as np
+root = sys.argv[1]
+sys.path[:0] = [root, os.path.join(root, "oracle"), os.path.join(root, "tools")]
+import pyoracle, scenes
+from pgi_raytracing_amd import abi
+from pgi_raytracing_amd.raytracer import Context, load_obj
+scene = load_obj(scenes.AVENGER_OBJ)
+scene.set_environment(os.path.join(root, "assets", "spherical_map_windows.jpg"))
+ctx = Context(0)
+ctx.set_scene(scene)
+ctx.configure(packet_levels=abi.PGRT_PACKETS_OFF, group_max=-1)
+cam = abi.default_camera(96, 64)
+ctx.set_camera(cam)
+oracle = pyoracle.OracleScene(scene, accel=1)
+for p in (abi.make_params(spp_side=1, max_level=5),
+          abi.make_params(spp_side=2, max_level=5, dof=1, jitter=abi.PGRT_JITTER_HASH, frame=3)):
+    img, _ = ctx.render(p)
+    ref, _ = oracle.render(cam, p)
+    same = (img == ref) | (np.isnan(img) & np.isnan(ref))
+    assert same.all(), f"{(~same).sum()} values differ"
+print("refill ok")
+"""
+
+
+def test_lane_refill_bit_exact(avenger_obj):
+    """The opt-in lane-refill one-lane kernel (k_trace_rf; PGRT_REFILL is read once per process,
+    so a child process renders with it on): every level one lane per ray (packets off, no 8-lane
+    groups) and the shadow queue, bit for bit against the oracle (profiles/r3/ab_r3ba_lane_refill.txt)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PGRT_REFILL="16")
+    r = subprocess.run([sys.executable, "-c", _REFILL_CHILD, root], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0 and "refill ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
