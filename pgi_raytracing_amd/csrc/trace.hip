@@ -1274,7 +1274,10 @@ bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) 
     if (grid > t.gstack_threads / kTraceBlock) grid = t.gstack_threads / kTraceBlock;
     // all-LDS stack when the BVH depth fits (depth + 2 entries per lane, <= 64 KB per block)
     const int entries = s.depth + 2;
-    const bool spill = entries * kTraceBlock * 4 > 65536;
+    // PGRT_TRACE_SPILL=1 (A/B): the short LDS stack (kLdsStack entries, the rest in global memory)
+    // even when the whole stack fits -- 16 KB per block instead of (depth + 2) KB, more blocks per CU
+    static const bool force_spill = env_int("PGRT_TRACE_SPILL", 0) != 0;
+    const bool spill = force_spill || entries * kTraceBlock * 4 > 65536;
     const size_t lds = (size_t)(spill ? kLdsStack : entries) * kTraceBlock * sizeof(int);
     const int min_idle = refill_min_idle();
     if (min_idle > 0 && !t.count && !spill && rpw == 64) {
