@@ -364,6 +364,127 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_rf(SceneView s, const flo
     }
 }
 
+// ---------------------------------------------------------------- one lane per ray, child prefetch
+//
+// Small queues (the deep Whitted levels) take as long as their slowest ray, whose node loop is a
+// chain of dependent steps: fetch the node, test its two child boxes, pick the next node, fetch
+// it.  Here a step issues the fetches of both children of the current node before testing their
+// boxes, so when the walk descends the next node's data is already on its way and the box tests
+// hide most of the fetch latency; only a pop from the stack fetches with the latency exposed.
+// Twice the node bytes per step: meant for latency-bound launches, not wide ones.  Same visit
+// order, arithmetic and results as k_trace.
+__device__ __forceinline__ void load_node(const BvhNode* nodes, int i, float4& a, float4& b, float4& c, int4& d) {
+    const BvhNode* nd = nodes + i;
+    a = nd->a;
+    b = nd->b;
+    c = nd->c;
+    d = nd->d;
+}
+
+__global__ __launch_bounds__(kTraceBlock) void k_trace_pf(SceneView s, const float4* __restrict__ ro,
+                                                          const float4* __restrict__ rd,
+                                                          float4* __restrict__ hits,
+                                                          const int* __restrict__ count_dev, int count_terms,
+                                                          int count_host, int cap, float4 const_org,
+                                                          unsigned char* __restrict__ lit,
+                                                          const int* __restrict__ perm) {
+    extern __shared__ int lstack[];  // [depth + 2][kTraceBlock]
+    const int tid = threadIdx.x;
+    const int n = ray_count(count_dev, count_terms, count_host, cap);
+    for (int slot = blockIdx.x * kTraceBlock + tid; slot < n; slot += gridDim.x * kTraceBlock) {
+        const int i = perm ? perm[slot] : slot;
+        const float4 o4 = ro ? ro[i] : const_org;
+        const float4 d4 = rd[i];
+        const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
+        const float dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
+        const float sdx = fabsf(dx) < 1e-30f ? copysignf(1e-30f, dx) : dx;
+        const float sdy = fabsf(dy) < 1e-30f ? copysignf(1e-30f, dy) : dy;
+        const float sdz = fabsf(dz) < 1e-30f ? copysignf(1e-30f, dz) : dz;
+        const float idx = __builtin_amdgcn_rcpf(sdx), idy = __builtin_amdgcn_rcpf(sdy),
+                    idz = __builtin_amdgcn_rcpf(sdz);
+        const float oix = ox * idx, oiy = oy * idy, oiz = oz * idz;
+        float best_t = tfar, best_u = 0.0f, best_v = 0.0f;
+        int best_prim = -1;
+        int sp = 0;
+        lstack[tid] = kSentinel;  // stack[0]
+        int node = s.root;
+        int leaf = 0;
+        if (node < 0) {
+            leaf = node;
+            node = kSentinel;
+        }
+        if (!(tfar >= 0.0f)) {
+            node = kSentinel;
+            leaf = 0;
+        }
+        // the current node's data (valid whenever node is internal)
+        float4 na = make_float4(0, 0, 0, 0), nb = na, nc = na;
+        int4 ndd = make_int4(0, 0, 0, 0);
+        if ((unsigned)node < (unsigned)kSentinel) load_node(s.nodes, node, na, nb, nc, ndd);
+        while (node != kSentinel || leaf < 0) {
+            const float bt = __builtin_canonicalizef(best_t);
+            while ((unsigned)node < (unsigned)kSentinel) {
+                const int top = lstack[sp * kTraceBlock + tid];
+                // both children's fetches first (a leaf child: the current node again, a cached line)
+                const int k0 = ndd.x >= 0 ? ndd.x : node, k1 = ndd.y >= 0 ? ndd.y : node;
+                float4 a0, b0, c0, a1, b1, c1;
+                int4 d0, d1;
+                load_node(s.nodes, k0, a0, b0, c0, d0);
+                load_node(s.nodes, k1, a1, b1, c1, d1);
+                float t0, t1;
+                const bool h0 = box_hit(na.x, na.y, na.z, na.w, nc.x, nc.y, idx, idy, idz, oix, oiy, oiz, bt, t0);
+                const bool h1 = box_hit(nb.x, nb.y, nb.z, nb.w, nc.z, nc.w, idx, idy, idz, oix, oiy, oiz, bt, t1);
+                const bool any = h0 || h1;
+                const bool first0 = h0 && (!h1 || t0 <= t1);
+                const bool both = h0 && h1;
+                lstack[(sp + 1) * kTraceBlock + tid] = first0 ? ndd.y : ndd.x;
+                const int nxt = any ? (first0 ? ndd.x : ndd.y) : top;
+                sp += both ? 1 : (any ? 0 : -1);
+                // the prefetched child, selected unconditionally (a load used only inside a branch
+                // could be sunk into it, which would undo the prefetch)
+                na = first0 ? a0 : a1;
+                nb = first0 ? b0 : b1;
+                nc = first0 ? c0 : c1;
+                ndd = first0 ? d0 : d1;
+                node = nxt;
+                bool fetch = !any;  // popped: fetch now, latency exposed
+                if (node < 0 && leaf == 0) {  // first leaf: park it and keep descending
+                    leaf = node;
+                    node = lstack[sp * kTraceBlock + tid];
+                    --sp;
+                    fetch = true;
+                }
+                if (fetch && (unsigned)node < (unsigned)kSentinel) load_node(s.nodes, node, na, nb, nc, ndd);
+                if (!__any(leaf == 0)) break;
+            }
+            while (leaf < 0) {
+                const int first = leaf_first(leaf), end = first + leaf_count(leaf);
+                float4 p0 = s.tri[3 * first], p1 = s.tri[3 * first + 1], p2 = s.tri[3 * first + 2];
+                for (int k = first; k < end; ++k) {
+                    const float4 q0 = p0, q1 = p1, q2 = p2;
+                    if (k + 1 < end) {
+                        p0 = s.tri[3 * k + 3];
+                        p1 = s.tri[3 * k + 4];
+                        p2 = s.tri[3 * k + 5];
+                    }
+                    tri_test(q0, q1, q2, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v, best_prim);
+                }
+                leaf = 0;
+                if (node < 0) {  // the node popped after parking is a leaf too: test it now
+                    leaf = node;
+                    node = lstack[sp * kTraceBlock + tid];
+                    --sp;
+                    if ((unsigned)node < (unsigned)kSentinel) load_node(s.nodes, node, na, nb, nc, ndd);
+                }
+            }
+        }
+        if (lit)
+            lit[i] = (best_prim < 0 || s.prim_glass[best_prim] != 0) ? 1 : 0;
+        else
+            hits[i] = make_float4(best_t, best_u, best_v, __int_as_float(best_prim));
+    }
+}
+
 // ---------------------------------------------------------------- 8-wide traversal
 //
 // Stack entries are node groups (child_base, hit bits << 24 | imask): the children of one wide
@@ -1279,6 +1400,15 @@ bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) 
     static const bool force_spill = env_int("PGRT_TRACE_SPILL", 0) != 0;
     const bool spill = force_spill || entries * kTraceBlock * 4 > 65536;
     const size_t lds = (size_t)(spill ? kLdsStack : entries) * kTraceBlock * sizeof(int);
+    // child prefetch for latency-bound one-lane launches: PGRT_TRACE_PF = the largest expected
+    // queue that takes it (A/B; 0 = never)
+    static const int pf_max = env_int("PGRT_TRACE_PF", 0);
+    if (!t.count && !spill && ex <= pf_max) {
+        PGRT_TLAUNCH(k_trace_pf, dim3(std::min(grid, ceil_div(ex, kTraceBlock))), dim3(kTraceBlock), lds, stream, s,
+                     t.ro, t.rd, t.hits, t.count_dev, t.count_terms, t.count_host, max_count, t.const_org, t.lit,
+                     t.perm);
+        return true;
+    }
     const int min_idle = refill_min_idle();
     if (min_idle > 0 && !t.count && !spill && rpw == 64) {
         // lane refill: a grid of resident blocks, each wave walking its own slot sequence
