@@ -1093,6 +1093,21 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 ++trace_launches;
             }
             id = ctx->timer.begin(s, CAT_COMBINE);
+            // PGRT_FUSED_RESOLVE=1 (A/B): 1-spp pending pixels resolve their whole ray tree in one
+            // launch (k_resolve_pending) instead of the per-level combines + finish
+            static const bool fused_resolve = getenv("PGRT_FUSED_RESOLVE") && atoi(getenv("PGRT_FUSED_RESOLVE")) != 0;
+            if (fused_resolve && l0f.pending && fp.nsb == 1) {
+                AllLevelNodes lv{};
+                for (int L = 0; L < levels; ++L) {
+                    lv.color[L] = sl->n_color[L]->p;
+                    lv.link[L] = sl->n_link[L]->p;
+                    lv.att[L] = sl->n_att[L]->p;
+                }
+                launch_resolve_pending(view, fp, sl->tiles.p, lv, sq, fo, l0f.pending, (int)npix, s);
+                debug_sync(s, "resolve", 0, bi);
+                ctx->timer.end(s, id);
+                continue;
+            }
             for (int L = p->max_level - 1; L >= 1; --L) {
                 LevelNodes ln{sl->n_color[L]->p, sl->n_link[L]->p, sl->n_att[L]->p};
                 launch_combine(view, L, ln, sl->n_color[L + 1]->p, sq, fcd, std::min(sl->q_cap, sl->level_cap[L]),

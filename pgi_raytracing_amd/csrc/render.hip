@@ -276,6 +276,67 @@ __global__ __launch_bounds__(kBlock) void k_finish_pending(SceneView s, FramePar
     store_final_1spp(fp, tiles, fo, p, node_color(s, sq, l0, child, p));
 }
 
+// 1-spp pending pixels resolved in one launch: each pixel's ray tree is evaluated depth-first
+// (post-order, the reflection child before the refraction child), so the per-level k_combine
+// passes and the finish are one kernel instead of max_level of them.  Every node's colour is
+// node_color's arithmetic on its children's colours, so the pixels are identical to the
+// level-by-level combine.  The stack is indexed by level (a child is always one level down).
+__global__ __launch_bounds__(kBlock) void k_resolve_pending(SceneView s, FrameParams fp, const int4* __restrict__ tiles,
+                                                            AllLevelNodes lv, ShadowQueue sq, FrameOut fo,
+                                                            const unsigned long long* __restrict__ pending, int npix) {
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= npix) return;
+    const unsigned long long pm = pending[__builtin_amdgcn_readfirstlane(p >> 6)];
+    if (((pm >> (p & 63)) & 1ull) == 0ull) return;
+    int idx[kMaxLevels];
+    int ph[kMaxLevels];  // 0: enter, 1: reflection returned, 2: refraction returned
+    float4 refl[kMaxLevels];
+    int L = 0;
+    idx[0] = p;
+    ph[0] = 0;
+    float4 v = make_float4(0, 0, 0, 0);  // colour of the node finished last
+    for (;;) {
+        const int i = idx[L];
+        const int4 lk = lv.link[L][i];
+        if (lk.x >= 0) {
+            if (ph[L] == 0) {  // descend: reflection child first
+                ph[L] = 1;
+                idx[L + 1] = lk.x;
+                ph[L + 1] = 0;
+                ++L;
+                continue;
+            }
+            if (ph[L] == 1 && lk.y >= 0) {  // reflection done: the refraction child
+                refl[L] = v;
+                ph[L] = 2;
+                idx[L + 1] = lk.y;
+                ph[L + 1] = 0;
+                ++L;
+                continue;
+            }
+            const float4 att = lv.att[L][i];
+            // raytracer.cpp:318-319 (refraction present) or :321 (total internal reflection)
+            const float4 c = ph[L] == 2 ? mix_srgb(refl[L], v, att.w) : v;
+            v = make_float4(c.x * att.x, c.y * att.y, c.z * att.z, 1);
+        } else if (lk.z >= 0) {
+            v = opaque_color(s, sq, lk.z, lk.w);
+        } else {
+            v = lv.color[L][i];
+        }
+        if (L == 0) break;
+        --L;
+    }
+    store_final_1spp(fp, tiles, fo, p, v);
+}
+
+void launch_resolve_pending(const SceneView& s, const FrameParams& fp, const int4* tiles, const AllLevelNodes& lv,
+                            ShadowQueue sq, const FrameOut& fo, const unsigned long long* pending, int npix,
+                            hipStream_t stream) {
+    if (npix <= 0) return;
+    hipLaunchKernelGGL(k_resolve_pending, dim3(ceil_div(npix, kBlock)), dim3(kBlock), 0, stream, s, fp, tiles, lv, sq,
+                       fo, pending, npix);
+}
+
 void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles, LevelNodes l0, const float4* child,
                    ShadowQueue sq, float4* accum, const FrameOut& fo, int npix, bool first, bool last, bool resolved,
                    const unsigned long long* pending, hipStream_t stream) {

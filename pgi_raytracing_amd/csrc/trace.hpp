@@ -128,6 +128,11 @@ struct LevelNodes {  // per-level node records kept until the combine pass
     int4* link;      // dielectric: (refl child, refr child or -1, -, -); opaque: (-1,-1,shadow base, n)
     float4* att;     // dielectric: (att.r, att.g, att.b, R)
 };
+struct AllLevelNodes {  // every level's node records (k_resolve_pending)
+    float4* color[kMaxLevels];
+    int4* link[kMaxLevels];
+    float4* att[kMaxLevels];
+};
 
 struct ShadowQueue {  // one per batch: the shadow rays of every level, level-major
     float4* ro;       // NULL in the compact form (one light: every shadow ray starts at it)
@@ -215,6 +220,9 @@ void launch_combine(const SceneView& s, int level, LevelNodes nodes, const float
 // resolved: level 0's final colours were written by launch_combine(level 0) (several samples
 // per pixel).  l0f.pending != NULL (1 spp, L0Final): only the pixels whose bit is set there are
 // finished (the others were written by the level-0 shade).
+void launch_resolve_pending(const SceneView& s, const FrameParams& fp, const int4* tiles, const AllLevelNodes& lv,
+                            ShadowQueue sq, const FrameOut& fo, const unsigned long long* pending, int npix,
+                            hipStream_t stream);
 void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles, LevelNodes l0, const float4* child,
                    ShadowQueue sq, float4* accum, const FrameOut& fo, int npix, bool first, bool last,
                    bool resolved, const unsigned long long* pending, hipStream_t stream);
