@@ -14,15 +14,15 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off \
 HIPFLAGS_render := -mllvm -disable-machine-licm
 HIPFLAGS_path := -mllvm -disable-machine-licm
 HIPFLAGS_trace := -mllvm -disable-machine-licm
-HIPFLAGS_tail := -mllvm -disable-machine-licm
-OBJS := $(BUILD)/trace.o $(BUILD)/tail.o $(BUILD)/render.o $(BUILD)/bvh.o $(BUILD)/ploc.o $(BUILD)/split.o $(BUILD)/bvh8.o $(BUILD)/bvh_layout.o $(BUILD)/path.o $(BUILD)/context.o $(BUILD)/objloader.o
+HIPFLAGS_subtree := -mllvm -disable-machine-licm
+OBJS := $(BUILD)/trace.o $(BUILD)/render.o $(BUILD)/bvh.o $(BUILD)/ploc.o $(BUILD)/split.o $(BUILD)/bvh8.o $(BUILD)/path.o $(BUILD)/subtree.o $(BUILD)/context.o $(BUILD)/objloader.o
 
 all: $(LIBDIR)/libpgrt.so $(LIBDIR)/libpgrt_image.so oracle $(BUILD)/pg1_pgrt
 
 $(BUILD) $(LIBDIR):
 	mkdir -p $@
 
-HDRS := include/pgrt.h include/pgrt_detmath.h $(SRC)/common.hpp $(SRC)/trace.hpp $(SRC)/traverse.hpp $(SRC)/shade_ops.hpp $(SRC)/camera_ops.hpp $(SRC)/shade_ray.hpp $(SRC)/tiles.hpp $(SRC)/path.hpp
+HDRS := include/pgrt.h include/pgrt_detmath.h $(SRC)/cache_ops.hpp $(SRC)/stamps.hpp $(SRC)/common.hpp $(SRC)/trace.hpp $(SRC)/traverse.hpp $(SRC)/shade_ops.hpp $(SRC)/camera_ops.hpp $(SRC)/shade_ray.hpp $(SRC)/tiles.hpp $(SRC)/path.hpp
 
 $(BUILD)/%.o: $(SRC)/%.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) $(HIPFLAGS_$*) -c $< -o $@

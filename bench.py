@@ -381,11 +381,13 @@ def main():
             rays_n += wait_one()
         return rays_n
 
-    warmup_requested = args.warmup
-    if args.roofline_only:
-        args.warmup = args.steps = 0
-    else:  # every frame set is allocated and warm before the timed region
-        args.warmup = max(args.warmup, in_flight * F)
+    if args.roofline_only:  # the profiled calls below, after two unprofiled ones (AUTO's start frame)
+        args.warmup, args.steps = 2 * F, 0
+    # untimed set-up (not warm-up): one call of F frames per call slot in flight, so every frame
+    # set's queues and framebuffers are allocated before the warm-up and the timed region (a first
+    # use would hipMalloc inside the timed calls); then exactly --warmup untimed frames
+    setup_frames = 0 if args.roofline_only else in_flight * F
+    run_frames(setup_frames)
     run_frames(args.warmup)
     share = None
     if distributed and not args.roofline_only:
@@ -501,6 +503,11 @@ def main():
             roof["traffic"] = t.get("bytes_per_launch")
             roof["traffic_source"] = f"{TRAFFIC[tkey]} ({t.get('round')}; FETCH_SIZE x2 + WRITE_SIZE per launch)"
             roof["traffic_frac"] = round(roof["traffic"] / (avg_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            if t.get("frame") and roof.get("frame"):  # whole-frame DRAM bytes (every kernel of the call)
+                fb = t["frame"]["bytes_per_frame"]
+                roof["frame"]["traffic"] = fb
+                roof["frame"]["traffic_frac"] = round(fb / (roof["frame"]["ms_per_frame"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                roof["frame"]["traffic_by_kernel"] = t["frame"].get("by_kernel_bytes_per_frame")
             if t.get("valu_issue"):
                 roof["valu_issue"] = t["valu_issue"]
                 roof["valu_issue_note"] = t.get("valu_issue_note")
@@ -580,9 +587,9 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "warmup_requested": warmup_requested,
-            "warmup_note": "raised to in_flight x frames_per_call so every frame set is allocated and warm "
-                           "before the timed region",
+            "setup_frames": setup_frames,
+            "setup_note": "untimed set-up before the warm-up: one call of frames_per_call frames per call slot in "
+                          "flight, so every frame set is allocated before the timed region (not counted as warm-up)",
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "frames_in_flight": in_flight,
             "frames_per_call": F,

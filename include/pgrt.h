@@ -191,25 +191,15 @@ typedef struct pgrt_config {
     int rank0_share_a, rank0_share_b; /* distributed frames: rank 0 renders a tiles for every b of
                                          another rank (1..64 each; 0 = the default deal of
                                          pgrt_tile_share; pgrt_tune_distribution sets them) */
-    int ray_binning;      /* 1: the rays of every bounce level traced as wave packets are visited
-                             in direction-octant bins (a counting sort by the octant the shade
-                             records, keeping screen order inside a bin); 0 / -1 = off (default:
-                             no gain on C2, profiles/r3/ab_r3c_binning.txt) */
     int packet_budget;    /* bounce levels traced as wave packets: a wave still traversing after this
                              many node / triangle steps hands its rays (with their closest hits so
                              far) to the 8-lanes-per-ray kernel; 0 = default (64 steps for one-frame
                              batches of scenes up to 262144 triangles, 256 otherwise), -1 = no budget */
-    int tail_level;       /* k >= 1: Whitted levels >= k run as ONE persistent launch that hands each
-                             ray's children to the next level as soon as they exist (device-side
-                             level iteration); 0 / -1 = one launch per level (the default: the
-                             persistent tail measured slower on C2, profiles/r3/ab_r3h_tail.txt) */
-    int packet_width;     /* bounce levels traced as wave packets: 0 / 2 = over the binary BVH (default),
-                             8 = over the quantized 8-wide BVH (one 80-B node per packet step) */
-    int bvh_layout;       /* binary node order, applied by pgrt_set_scene: 0 = the builder's creation
-                             order (default), 1 = sibling pairs (the two children of a node in one
-                             128-B line, pairs in depth-first order; neutral on C2 / C5,
-                             profiles/r3/ab_r3u_bvh_layout.txt) */
-    int call_order;       /* frames in flight: 1 = each call's level-0 trace waits for the previous
+    int subtree_level;    /* Whitted levels >= k evaluated as whole ray trees, one launch (every ray of
+                             level k traces and shades its reflection / refraction / shadow rays
+                             depth first, as the reference's recursive trace does): 0 = default, -1 =
+                             one launch per level, k >= 1 = from level k */
+    int call_order;     /* frames in flight: 1 = each call's level-0 trace waits for the previous
                              call's level-0 shade (the bulk work of the calls in submission order,
                              their latency-bound deeper levels overlapping the next call's bulk);
                              -1 = calls share the GPU freely; 0 = default: ordered for scenes above
@@ -431,6 +421,39 @@ typedef struct pgrt_level_diag {
     uint64_t packet_steps_live;   /* ... and live lane-steps; hit / live = packet utilisation */
 } pgrt_level_diag;
 int pgrt_frame_diag(const pgrt_ctx* ctx, pgrt_level_diag* out, int max_levels);
+
+/* ---- launch timeline (device clock; no rocprof, no HIP events) ----
+ * While enabled, every kernel of every later frame (synchronous and asynchronous calls alike)
+ * stamps the device wall clock (s_memrealtime, 100 MHz) in each of its waves at entry and exit;
+ * when the call is collected, each launch becomes one record: the first wave's start and the last
+ * wave's end.  The stamps cost one 16-B store per wave; the kernels, grids and streams are those
+ * of an unrecorded frame.  pgrt_timeline_read returns the records collected so far (oldest first,
+ * at most max) and removes them; *n receives the count returned.  Enabling or disabling completes
+ * pending frames first. */
+#define PGRT_TL_RAYGEN 0        /* k_raygen */
+#define PGRT_TL_TRACE_PKT 1     /* wave-packet closest hit (level 0 generates its rays) */
+#define PGRT_TL_TRACE 2         /* one lane per ray */
+#define PGRT_TL_TRACE_8G 3      /* 8 (4) lanes per ray over the 8-wide BVH */
+#define PGRT_TL_TRACE_RESUME 4  /* 8 lanes per ray, the deferred rays of a budgeted packet launch */
+#define PGRT_TL_TRACE_SHADOW 5  /* the shadow queue */
+#define PGRT_TL_SHADE 6
+#define PGRT_TL_COMBINE 7
+#define PGRT_TL_FINISH 8
+#define PGRT_TL_EXPORT 9        /* frame counters to the host */
+#define PGRT_TL_UNPACK 10
+#define PGRT_TL_PATH_SHADE 11
+#define PGRT_TL_PATH_RESOLVE 12
+#define PGRT_TL_SUBTREE 13      /* the deep levels as one launch (pgrt_config.subtree_level) */
+typedef struct pgrt_timeline_rec {
+    uint64_t ticket;     /* the call (the ticket an asynchronous call returned; synchronous calls count too) */
+    int slot;            /* pipeline slot (stream) of the call */
+    int kind;            /* PGRT_TL_* */
+    int level;           /* queue level, -1 = none */
+    int waves;           /* waves that stamped */
+    uint64_t start, end; /* device wall clock ticks (100 MHz): first wave in, last wave out */
+} pgrt_timeline_rec;
+int pgrt_timeline_enable(pgrt_ctx* ctx, int on);
+int pgrt_timeline_read(pgrt_ctx* ctx, pgrt_timeline_rec* out, int max, int* n);
 
 /* ---- test hook: evaluates the shared math of pgrt_detmath.h on the device.  in: n (a,b)
  *      pairs; out: n x 8 {sqrtf(a), a/b, powf(a,b), expf(a), atan2f(a,b), asinf(a),

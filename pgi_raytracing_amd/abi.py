@@ -126,11 +126,8 @@ class Config(C.Structure):
         ("max_batches_in_flight", C.c_int),
         ("rank0_share_a", C.c_int),
         ("rank0_share_b", C.c_int),
-        ("ray_binning", C.c_int),
         ("packet_budget", C.c_int),
-        ("tail_level", C.c_int),
-        ("packet_width", C.c_int),
-        ("bvh_layout", C.c_int),
+        ("subtree_level", C.c_int),
         ("call_order", C.c_int),
     ]
 
@@ -174,6 +171,23 @@ class LevelDiag(C.Structure):
                                           "lr_load_cyc64", "wide_visits")] + [("ms_trace", C.c_double), ("ms_shade", C.c_double),
                                                                   ("packet_steps_hit", C.c_uint64),
                                                                   ("packet_steps_live", C.c_uint64)]
+
+
+TIMELINE_KINDS = ("raygen", "trace_pkt", "trace", "trace_8g", "trace_resume", "trace_shadow", "shade", "combine",
+                  "finish", "export", "unpack", "path_shade", "path_resolve", "subtree")  # PGRT_TL_*
+
+
+class TimelineRec(C.Structure):
+    """pgrt_timeline_rec: one launch, device wall clock (100 MHz ticks)."""
+    _fields_ = [
+        ("ticket", C.c_uint64),
+        ("slot", C.c_int),
+        ("kind", C.c_int),
+        ("level", C.c_int),
+        ("waves", C.c_int),
+        ("start", C.c_uint64),
+        ("end", C.c_uint64),
+    ]
 
 
 class BvhInfo(C.Structure):

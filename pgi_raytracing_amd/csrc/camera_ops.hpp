@@ -4,6 +4,8 @@
 // bit-identical.
 #pragma once
 
+#include "cache_ops.hpp"
+
 #include "shade_ops.hpp"
 #include "trace.hpp"
 
@@ -28,7 +30,7 @@ __device__ __forceinline__ void store_pixel(const FrameParams& fp, const int4* t
     if (fo.mode == 0) {
         float* dst = fo.out + (size_t)frame_of_tile(fp, p / (kTile * kTile)) * fp.frame_stride +
                      ((size_t)(py - fo.oy) * (size_t)fo.pitch + (size_t)(px - fo.ox)) * 4;
-        *reinterpret_cast<float4*>(dst) = o;
+        st_stream(reinterpret_cast<float4*>(dst), o);
         return;
     }
     const int tile = p / (kTile * kTile);
@@ -40,11 +42,11 @@ __device__ __forceinline__ void store_pixel(const FrameParams& fp, const int4* t
     }
     const size_t q = gtile * kTile * kTile + (size_t)(py - tr.y) * kTile + (size_t)(px - tr.x);
     if (fo.mode == 1) {
-        *reinterpret_cast<float4*>(fo.out + q * 4) = o;
+        st_stream(reinterpret_cast<float4*>(fo.out + q * 4), o);
     } else {  // 2: RGB only (alpha is always 1): the multi-GPU gather moves 12 B per pixel
-        fo.out[q * 3 + 0] = o.x;
-        fo.out[q * 3 + 1] = o.y;
-        fo.out[q * 3 + 2] = o.z;
+        st_stream_nt(fo.out + q * 3 + 0, o.x);
+        st_stream_nt(fo.out + q * 3 + 1, o.y);
+        st_stream_nt(fo.out + q * 3 + 2, o.z);
     }
 }
 

@@ -143,6 +143,8 @@ struct SceneView {  // kernel-argument view of the device scene
     int env;
     int nlight;
     const DevLight* lights;
+    // this launch's timeline slots (stamps.hpp; set per launch by the launcher), NULL = off
+    unsigned long long* stamps;
 };
 
 struct CameraView {

@@ -19,8 +19,17 @@
 #include "shade_ray.hpp"
 #include "path.hpp"
 #include "tiles.hpp"
+#include "stamps.hpp"
 
 using namespace pgrt;
+
+namespace pgrt {
+namespace {
+thread_local StampLog* t_stamp_log = nullptr;
+}
+void set_stamp_log(StampLog* log) { t_stamp_log = log; }
+StampLog* stamp_log() { return t_stamp_log; }
+}  // namespace pgrt
 
 namespace {
 
@@ -28,8 +37,8 @@ namespace {
 // 10.12 ms, C4 40.6 / 38.4 / 38.8 ms (fewer batches: each pays its deep-level chain once)
 constexpr long long kMaxBatchRays = 32ll << 20;
 constexpr int kTraceGridThreads = 2048 * 256;    // persistent trace grid (global overflow stacks)
-constexpr int kTailGridMax = 1024;                // persistent tail: 4 resident blocks x 256 CUs
 constexpr int kMaxFramesInFlight = 16;
+constexpr long long kStampWaves = 4ll << 20;  // timeline: wave stamps per frame set (64 MB)
 constexpr int kMaxFramesPerCall = 64;
 
 struct StageTimer {
@@ -96,7 +105,7 @@ struct StageTimer {
     }
 };
 
-enum { CAT_RAYGEN, CAT_TRACE, CAT_SHADE, CAT_SHADOW, CAT_COMBINE, CAT_BIN, CAT_LTRACE, CAT_LSHADE = CAT_LTRACE + kMaxLevels,
+enum { CAT_RAYGEN, CAT_TRACE, CAT_SHADE, CAT_SHADOW, CAT_COMBINE, CAT_LTRACE, CAT_LSHADE = CAT_LTRACE + kMaxLevels,
        CAT_N = CAT_LSHADE + kMaxLevels };
 
 }  // namespace
@@ -115,14 +124,9 @@ struct FrameSlot {
     DevBuf<int4> tiles;
     DevBuf<float4> q_ro[2], q_rd[2], q_hit[2];
     DevBuf<float> q_time[2];
-    DevBuf<unsigned char> q_key;  // binning key of the next level's rays (one level at a time)
-    DevBuf<int> q_perm;           // the binned level's traversal order
-    DevBuf<unsigned> q_bins;      // per-chunk bin counts / offsets of the binning sort
     DevBuf<int> q_defer;          // rays a budgeted packet launch handed to the 8-lane kernel
-    // persistent tail (tail.hip): hand-off granules of tail levels > first (5 words per slot) and
-    // the batch epoch their flag words carry (counts up, never 0)
-    std::unique_ptr<DevBuf<unsigned long long>> t_gran[kMaxLevels];
-    unsigned tail_epoch = 0;
+    DevBuf<float4> probe_hits;    // the AUTO probe's side launch: its hit records and deferrals (discarded)
+    DevBuf<int> probe_defer;
     DevBuf<unsigned long long> l0_hit, l0_pending;  // 1-spp level-0 wave masks (L0Final)
     int q_cap = 0;
     std::vector<std::unique_ptr<DevBuf<float4>>> n_color, n_att;
@@ -209,17 +213,33 @@ struct FrameSet {
     // slowest peer) and of rank 0's unpack, read when the frame is waited for
     hipEvent_t ev_g0 = nullptr, ev_g1 = nullptr, ev_g2 = nullptr;
     bool gather_timed = false;
+    // multi-process distributed frames, rank 0: every peer's overflow flag (the tail of its send,
+    // copied to host memory behind the unpack, ev_flags) -- the re-render agreement without a
+    // control collective
+    hipEvent_t ev_flags = nullptr;
+    int* peer_flags = nullptr;  // pinned, kMaxRanks words
+    // a re-gather after an overflow (rank 0): receive / unpack only the ranks marked here
+    bool regather = false;
+    char regather_peer[kMaxRanks] = {};
+    // launch timeline (pgrt_timeline_enable): this call's wave stamps and the launches they belong to
+    DevBuf<unsigned long long> stamps;
+    std::vector<StampLaunch> stamp_launches;
+    long long stamp_used = 0;
     FrameSet() {
         PGRT_HIP(hipEventCreateWithFlags(&ev_ready, hipEventDisableTiming));
         PGRT_HIP(hipEventCreate(&ev_g0));
         PGRT_HIP(hipEventCreate(&ev_g1));
         PGRT_HIP(hipEventCreate(&ev_g2));
+        PGRT_HIP(hipEventCreateWithFlags(&ev_flags, hipEventDisableTiming));
+        PGRT_HIP(hipHostMalloc((void**)&peer_flags, sizeof(int) * kMaxRanks, hipHostMallocMapped | hipHostMallocCoherent));
+        std::fill(peer_flags, peer_flags + kMaxRanks, 0);
     }
     ~FrameSet() {
         for (auto& s : slots)
             if (s->stream) (void)hipStreamSynchronize(s->stream);
-        for (hipEvent_t e : {ev_ready, ev_g0, ev_g1, ev_g2})
+        for (hipEvent_t e : {ev_ready, ev_g0, ev_g1, ev_g2, ev_flags})
             if (e) (void)hipEventDestroy(e);
+        if (peer_flags) (void)hipHostFree(peer_flags);
     }
 };
 }  // namespace pgrt
@@ -273,16 +293,14 @@ struct pgrt_ctx {
     DevBuf<int> gstack;        // pgrt_intersect_closest
     DevBuf<float> out_tmp;
     StageTimer timer;
+    bool timeline_on = false;                     // pgrt_timeline_enable
+    std::vector<pgrt_timeline_rec> timeline;      // collected launch records (pgrt_timeline_read)
+    std::vector<unsigned long long> stamp_host;   // staging of a frame set's stamps
     std::vector<FrameCounters> last_fc;  // per slot and batch, for pgrt_frame_diag
     double level_ms[kMaxLevels][2] = {};  // per-level trace / shade ms of the last profiled call
 
     // multi-GPU
     ncclComm_t comm = nullptr;
-    // control communicator (ncclCommSplit of comm) on its own stream: the per-frame overflow
-    // agreement of distributed frames, never queued behind the gathers on `stream`
-    ncclComm_t comm_ctl = nullptr;
-    hipStream_t ctl_stream = nullptr;
-    DevBuf<int> ctl_buf;
     int world = 1, rank = 0;
     // PGRT_EMULATE_RANK=r/N (measurement tool only, no communicator): distributed frames render
     // rank r's share of an N-GPU frame on this device; the gather becomes a device copy of this
@@ -304,6 +322,21 @@ struct pgrt_ctx {
     int acc_count = 0, acc_w = 0, acc_h = 0;
 
     ~pgrt_ctx() {
+        if (group && comm) {
+            // communicators of one ncclCommInitAll: finalised together in one group (each
+            // finalize may wait on its peers), then destroyed one by one
+            for (pgrt_ctx* m : members) {
+                (void)hipSetDevice(m->device);
+                if (m->stream) (void)hipStreamSynchronize(m->stream);
+            }
+            (void)hipSetDevice(device);
+            if (stream) (void)hipStreamSynchronize(stream);
+            (void)ncclGroupStart();
+            (void)ncclCommFinalize(comm);
+            for (pgrt_ctx* m : members)
+                if (m->comm) (void)ncclCommFinalize(m->comm);
+            (void)ncclGroupEnd();
+        }
         for (pgrt_ctx* m : members) {
             (void)hipSetDevice(m->device);
             if (m->stream) (void)hipStreamSynchronize(m->stream);
@@ -311,8 +344,6 @@ struct pgrt_ctx {
         }
         (void)hipSetDevice(device);
         if (l0_token) (void)hipEventDestroy(l0_token);
-        if (comm_ctl) (void)ncclCommDestroy(comm_ctl);
-        if (ctl_stream) (void)hipStreamDestroy(ctl_stream);
         if (comm) (void)ncclCommDestroy(comm);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -514,9 +545,6 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
         sort_tmp.alloc(tmp_bytes);
         build_lbvh(pos.p, n, ctx->tri.p, ctx->nodes.p, scratch.p, sort_tmp.p, tmp_bytes, pad, &bo, st);
     }
-    // node order: the builder's, or sibling pairs in 128-B lines, depth-first (bvh_layout.hip;
-    // measured neutral on C2 and C5, profiles/r3/ab_r3u_bvh_layout.txt)
-    if (cfg.bvh_layout == 1) bo.num_nodes = relayout_bvh(ctx->nodes, bo.num_nodes, &bo.root, st);
     const int m = bo.refs;
     // the 8-wide layout is always built: the multi-lane kernel traces small (deep-level) queues
     // over it; PGRT_BVH_WIDTH=8 also sends the big queues to the one-lane 8-wide kernel
@@ -558,6 +586,13 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
     v.nlight = d->num_lights;
     v.lights = ctx->lights.p;
     ctx->has_scene = true;
+    // AUTO's packet choice starts over for a new scene: levels 0-2 on packets, level 0 only for
+    // big scenes (their bounce levels are incoherent: r2 / r3 measured AUTO turning 1-2 off
+    // after a start frame of multi-ms packet launches)
+    ctx->auto_packets = n > kPacketBigScene ? 0x1u : 0x7u;
+    ctx->probe_level = -1;
+    ctx->frames_collected = 0;
+    std::fill(ctx->packet_util, ctx->packet_util + kMaxLevels, 0.0);
     pgrt_bvh_info& bi = ctx->info;
     bi.num_triangles = empty ? 0 : n;
     bi.num_nodes = width == 8 ? wide_nodes : bo.num_nodes;
@@ -587,9 +622,6 @@ void ensure_frame_buffers(FrameSlot* sl, int n0, int levels, int nlight, int bat
         }
         sl->l0_hit.alloc((size_t)n0 / 64 + 1);
         sl->l0_pending.alloc((size_t)n0 / 64 + 1);
-        sl->q_key.alloc(n0);
-        sl->q_perm.alloc(n0);
-        sl->q_bins.alloc(((size_t)n0 / 256 + 1) * kBins);
         sl->q_defer.alloc(n0);
         sl->q_cap = n0;
     }
@@ -644,9 +676,6 @@ void grow_after_overflow(FrameSlot* sl, int levels) {
                     sl->q_hit[b].alloc(need);
                     sl->q_time[b].alloc(need);
                 }
-                sl->q_key.alloc(need);
-                sl->q_perm.alloc(need);
-                sl->q_bins.alloc(((size_t)need / 256 + 1) * kBins);
                 sl->q_defer.alloc(need);
                 sl->q_cap = need;
             }
@@ -700,14 +729,15 @@ bool packet_level(const pgrt_ctx* ctx, int L) {
     if (k == PGRT_PACKETS_OFF) return false;
     // (profiled frames never probe: their traversal counts describe the timed frames' choice)
     if (k == PGRT_PACKETS_AUTO)
-        return L == 0 || ((ctx->auto_packets >> L) & 1u) != 0 || (L == ctx->probe_level && !ctx->timer.on);
+        return L == 0 || ((ctx->auto_packets >> L) & 1u) != 0;
     return L < k;
 }
 
-// is level L >= 1 binned by direction octant before its packet traversal (pgrt_config.ray_binning)
-bool binned_level(const pgrt_ctx* ctx, const SceneView& view, int L) {
-    return L >= 1 && ctx->cfg.ray_binning == 1 && packet_level(ctx, L) && trace_packets_available(view);
-}
+// AUTO's probe of a level that is off packets: a SIDE packet launch over the level's first
+// kProbeRays rays (hit records discarded, deferred rays not finished) samples the utilisation; the
+// level itself is traced as usual, so a probe frame costs one bounded launch instead of a whole
+// level on packets (C5's incoherent level 1: multi-ms resume launches, profiles/r3 verdict)
+constexpr int kProbeRays = 65536;
 
 // PGRT_PACKETS_AUTO: a level stays on wave packets while its rays use at least this fraction of
 // the wave's node stream (calibrated on C2 / C5), re-probed while off
@@ -749,12 +779,13 @@ int group_max(const pgrt_ctx* ctx) {
     return ctx->frames_in_flight > 1 ? kDefaultGroupMaxInFlight : kDefaultGroupMax;
 }
 
-// first level of the persistent tail (pgrt_config.tail_level >= 1), -1 = no tail (the default:
-// measured slower than one launch per level on C2)
-int tail_first(const pgrt_ctx* ctx, const SceneView& view, const pgrt_render_params* p) {
-    const int k = ctx->cfg.tail_level;
-    if (k <= 0 || p->mode != PGRT_MODE_WHITTED || !tail_available(view)) return -1;
-    return k <= p->max_level ? k : -1;
+// first level evaluated as whole ray trees in one launch (pgrt_config.subtree_level, subtree.hip),
+// -1 = one launch per level
+int subtree_first(const pgrt_ctx* ctx, const SceneView& view, const pgrt_render_params* p) {
+    const int k = ctx->cfg.subtree_level;
+    if (k < 0 || p->mode != PGRT_MODE_WHITTED || !subtree_available(view)) return -1;
+    if (k > 0) return k <= p->max_level ? k : -1;
+    return -1;
 }
 
 // step budget of the bounce levels' packet launches (pgrt_config.packet_budget)
@@ -781,6 +812,31 @@ int packet_budget(const pgrt_ctx* ctx, bool small_batch) {
     return small_batch ? kSmallBatchPacketBudget : kDefaultPacketBudget;
 }
 
+// AUTO's probe (kProbeRays): after level L's own trace, a side packet launch over its first rays
+// samples the packet utilisation of a level that is off packets (unprofiled frames only)
+void probe_side_launch(pgrt_ctx* ctx, const SceneView& view, FrameSlot* sl, FrameCounters* fcd, const TraceLaunch& tl,
+                       hipStream_t s) {
+    const int L = tl.level;
+    if (ctx->cfg.packet_levels != PGRT_PACKETS_AUTO || L < 1 || L != ctx->probe_level || ctx->timer.on ||
+        packet_level(ctx, L) || !trace_packets_available(view) || tl.max_count <= 0)
+        return;
+    sl->probe_hits.alloc(kProbeRays);
+    sl->probe_defer.alloc(kProbeRays);
+    TraceLaunch pr = tl;
+    pr.hits = sl->probe_hits.p;
+    pr.max_count = std::min(tl.max_count, kProbeRays);
+    pr.expect = pr.max_count;
+    pr.count = false;
+    pr.packets = true;
+    pr.gen = nullptr;
+    pr.budget = kDefaultPacketBudget;  // AUTO samples default-budget launches (packet_budget)
+    pr.pkt_util = fcd->pkt[L];
+    pr.defer_list = sl->probe_defer.p;
+    pr.defer_count = &fcd->probe_defer;
+    pr.resume = false;
+    launch_trace(view, pr, s);
+}
+
 // One sample batch of a PGRT_MODE_PATH frame (path.hip): raygen, then per bounce L the closest
 // hits of the path queue, the bounce's shading, its shadow rays and their resolve; the finish
 // sums each pixel's path accumulators (a resolved level 0) and writes the output like a Whitted
@@ -805,6 +861,7 @@ void enqueue_path_batch(pgrt_ctx* ctx, FrameSlot* sl, const SceneView& view, con
         qn.cap = std::min(sl->q_cap, L + 1 < levels ? sl->level_cap[L + 1] : sl->q_cap);
         const int ex = L == 0 ? n0 : sl->expect_count[L];
         TraceLaunch tl;
+        tl.level = L;
         tl.ro = qc.ro;
         tl.rd = qc.rd;
         tl.hits = qc.hit;
@@ -818,7 +875,6 @@ void enqueue_path_batch(pgrt_ctx* ctx, FrameSlot* sl, const SceneView& view, con
         tl.packets = packet_level(ctx, L);
         tl.pkt_util = fcd->pkt[L];
         tl.budget = packet_budget(ctx, false);
-        tl.wide_packets = L > 0 && ctx->cfg.packet_width == 8;
         tl.defer_list = sl->q_defer.p;
         tl.defer_count = &fcd->defer[L];
         tl.defer_expect = sl->expect_defer[L];
@@ -827,6 +883,7 @@ void enqueue_path_batch(pgrt_ctx* ctx, FrameSlot* sl, const SceneView& view, con
         ctx->timer.end_kernel(s, id, launched);
         ++trace_launches;
         debug_sync(s, "path trace", L, bi);
+        probe_side_launch(ctx, view, sl, fcd, tl, s);
         const PathState ps{L > 0 ? reinterpret_cast<const int*>(sl->n_link[L]->p) : nullptr,
                            L > 0 ? sl->n_att[L]->p : nullptr,
                            L + 1 < levels ? reinterpret_cast<int*>(sl->n_link[L + 1]->p) : nullptr,
@@ -889,6 +946,21 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
     fs->K = K;
     fs->batches = 0;
     while ((int)fs->slots.size() < K) fs->slots.emplace_back(new FrameSlot());
+    // launch timeline (pgrt_timeline_enable): every launch of this call stamps its waves into
+    // fs->stamps, the slot ranges handed out by the launchers through the stamp log
+    StampLog slog;
+    fs->stamp_launches.clear();
+    fs->stamp_used = 0;
+    if (ctx->timeline_on) {
+        fs->stamps.alloc((size_t)kStampWaves * 2);
+        slog.dev = fs->stamps.p;
+        slog.cap = kStampWaves;
+        slog.launches = &fs->stamp_launches;
+    }
+    struct LogScope {  // the thread's log never outlives this call (exceptions included)
+        LogScope(StampLog* l) { set_stamp_log(l); }
+        ~LogScope() { set_stamp_log(nullptr); }
+    } log_scope(ctx->timeline_on ? &slog : nullptr);
     ctx->timer.on = p->profile > 0;
     int trace_launches = 0;
     FrameParams fp0{};
@@ -909,6 +981,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
     for (int j = 0; j < K; ++j) {
         FrameSlot* sl = fs->slots[j].get();
         hipStream_t s = sl->stream;
+        slog.slot = j;
         const int nt = (ntiles - j + K - 1) / K;
         const long long npix = (long long)nt * kTile * kTile;
         const int nsb = (int)std::max(1ll, std::min<long long>(spp, max_batch / npix));
@@ -971,55 +1044,26 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             if (!fuse) launch_raygen(ctx->cam, fp, sl->tiles.p, q[0], n0, fcd, s);
             debug_sync(s, "raygen", 0, bi);
             ctx->timer.end(s, id);
-            const int tail = tail_first(ctx, view, p);
+            // levels >= sub: whole ray trees in one launch (no queues, shades or combines below it)
+            const int sub = subtree_first(ctx, view, p);
             for (int L = 0; L < levels; ++L) {
                 Queue qc = q[L & 1], qn = q[(L + 1) & 1];
                 const int maxc = L == 0 ? n0 : std::min(sl->q_cap, sl->level_cap[L]);
-                if (L == tail) {  // levels tail .. max_level: one persistent launch
-                    TailLaunch tt{};
-                    tt.first = L;
-                    tt.levels = levels;
-                    qc.cap = maxc;
-                    tt.q_first = qc;
-                    long long ex_total = 0;
-                    for (int l = L; l < levels; ++l) {
-                        tt.cap[l] = l == L ? maxc : std::min(sl->q_cap, sl->level_cap[l]);
-                        tt.nodes[l] = LevelNodes{sl->n_color[l]->p, sl->n_link[l]->p, sl->n_att[l]->p};
-                        ex_total += sl->expect_count[l] > 0 ? sl->expect_count[l] : tt.cap[l];
-                        if (l > L) {
-                            if (!sl->t_gran[l]) sl->t_gran[l].reset(new DevBuf<unsigned long long>());
-                            DevBuf<unsigned long long>& g = *sl->t_gran[l];
-                            if (g.n < (size_t)tt.cap[l] * 5) {
-                                // fresh memory: no flag word may hold a live epoch by chance
-                                g.alloc((size_t)tt.cap[l] * 5);
-                                PGRT_HIP(hipMemsetAsync(g.p, 0, g.bytes(), s));
-                            }
-                            tt.gran[l] = g.p;
-                        }
-                    }
-                    tt.sq = sq;
-                    tt.fc = fcd;
-                    if (++sl->tail_epoch == 0) ++sl->tail_epoch;
-                    tt.epoch = sl->tail_epoch;
-                    tt.grid = (int)std::max<long long>(64, std::min<long long>(kTailGridMax, (ex_total + 255) / 256));
-                    int id = ctx->timer.begin(s, CAT_TRACE, CAT_LTRACE + L);
-                    launch_tail(view, fp, tt, s);
-                    ctx->timer.end(s, id);
-                    debug_sync(s, "tail", L, bi);
-                    ++trace_launches;
-                    break;
-                }
                 qc.cap = maxc;
                 qn.cap = std::min(sl->q_cap, L + 1 < levels ? sl->level_cap[L + 1] : sl->q_cap);
-                // the next level's rays get their binning key from this level's shade when the
-                // next level is traced as packets
-                const bool bin_next = L + 1 < levels && binned_level(ctx, view, L + 1);
-                qn.key = bin_next ? sl->q_key.p : nullptr;
-                const bool binned = L >= 1 && binned_level(ctx, view, L);
                 LevelNodes ln{sl->n_color[L]->p, sl->n_link[L]->p, sl->n_att[L]->p};
                 // grid hints: last frame's per-level counts (+25 %); level 0 is exact
                 const int ex = L == 0 ? n0 : sl->expect_count[L];
+                if (L == sub) {
+                    id = ctx->timer.begin(s, CAT_TRACE, CAT_LTRACE + L);
+                    launch_subtree(view, fp, L, qc, ln, fcd, maxc, ex, p->profile >= 2, s);
+                    ctx->timer.end(s, id);
+                    debug_sync(s, "subtree", L, bi);
+                    ++trace_launches;
+                    break;
+                }
                 TraceLaunch tl;
+                tl.level = L;
                 tl.ro = qc.ro;
                 tl.rd = qc.rd;
                 tl.hits = qc.hit;
@@ -1038,17 +1082,9 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 // short at 64 steps reads as better used than it is, and one-frame batches would
                 // then switch levels to packets for the multi-frame calls too
                 tl.pkt_util = tl.budget == kSmallBatchPacketBudget && ctx->cfg.packet_budget == 0 ? nullptr : fcd->pkt[L];
-                tl.wide_packets = L > 0 && ctx->cfg.packet_width == 8;
                 tl.defer_list = sl->q_defer.p;
                 tl.defer_count = &fcd->defer[L];
                 tl.defer_expect = sl->expect_defer[L];
-                if (binned) {
-                    id = ctx->timer.begin(s, CAT_BIN);
-                    launch_bin_rays(sl->q_key.p, fcd, L, maxc, sl->q_perm.p, sl->q_bins.p, ex, s);
-                    ctx->timer.end(s, id);
-                    debug_sync(s, "bin", L, bi);
-                    tl.perm = sl->q_perm.p;
-                }
                 const bool ordered = L == 0 && K == 1 && ctx->frames_in_flight > 1 && call_ordered(ctx, view);
                 if (ordered && ctx->l0_token_live) PGRT_HIP(hipStreamWaitEvent(s, ctx->l0_token, 0));
                 id = ctx->timer.begin_kernel(CAT_TRACE, CAT_LTRACE + L);
@@ -1056,6 +1092,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 ctx->timer.end_kernel(s, id, launched);
                 debug_sync(s, "trace", L, bi);
                 ++trace_launches;
+                probe_side_launch(ctx, view, sl, fcd, tl, s);
                 id = ctx->timer.begin(s, CAT_SHADE, CAT_LSHADE + L);
                 const PinholeOrigin l0{ctx->cam.from[0], ctx->cam.from[1], ctx->cam.from[2], L == 0 && dir_only ? 1 : 0};
                 launch_shade(view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex, l0,
@@ -1074,7 +1111,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 tl.rd = sq.rd;
                 tl.hits = sq.hit;
                 tl.count_dev = fc_shadow_counts(fcd);
-                tl.count_terms = levels;
+                tl.count_terms = sub > 0 ? sub : levels;  // the subtree levels trace their own shadow rays
                 tl.max_count = sq.cap;
                 tl.expect = sl->expect_shadow_total;
                 tl.gstack = sl->gstack.p;
@@ -1093,22 +1130,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 ++trace_launches;
             }
             id = ctx->timer.begin(s, CAT_COMBINE);
-            // PGRT_FUSED_RESOLVE=1 (A/B): 1-spp pending pixels resolve their whole ray tree in one
-            // launch (k_resolve_pending) instead of the per-level combines + finish
-            static const bool fused_resolve = getenv("PGRT_FUSED_RESOLVE") && atoi(getenv("PGRT_FUSED_RESOLVE")) != 0;
-            if (fused_resolve && l0f.pending && fp.nsb == 1) {
-                AllLevelNodes lv{};
-                for (int L = 0; L < levels; ++L) {
-                    lv.color[L] = sl->n_color[L]->p;
-                    lv.link[L] = sl->n_link[L]->p;
-                    lv.att[L] = sl->n_att[L]->p;
-                }
-                launch_resolve_pending(view, fp, sl->tiles.p, lv, sq, fo, l0f.pending, (int)npix, s);
-                debug_sync(s, "resolve", 0, bi);
-                ctx->timer.end(s, id);
-                continue;
-            }
-            for (int L = p->max_level - 1; L >= 1; --L) {
+            for (int L = std::min(p->max_level, sub > 0 ? sub : p->max_level) - 1; L >= 1; --L) {
                 LevelNodes ln{sl->n_color[L]->p, sl->n_link[L]->p, sl->n_att[L]->p};
                 launch_combine(view, L, ln, sl->n_color[L + 1]->p, sq, fcd, std::min(sl->q_cap, sl->level_cap[L]),
                                s, sl->expect_count[L]);
@@ -1138,6 +1160,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
     }
     PGRT_HIP(hipGetLastError());
     fs->stats.trace_launches = trace_launches;
+    fs->stamp_used = slog.used;
 }
 
 // One look at fs's completed frame (host waits for its slots): the counters to the host, the next
@@ -1156,8 +1179,6 @@ bool read_frame_counters(pgrt_ctx* ctx, FrameSet* fs) {
         FrameSlot* sl = fs->slots[j].get();
         for (auto& h : sl->host_fc) {
             overflow |= h.overflow != 0;
-            PGRT_REQUIRE(h.tail_err == 0, PGRT_ERR_HIP,
-                         "persistent tail: a bounded wait ran out (tail_err " + std::to_string(h.tail_err) + ")");
             ctx->last_fc.push_back(h);
         }
         int shadow_need = 0;
@@ -1257,38 +1278,68 @@ void frame_stats(pgrt_ctx* ctx, FrameSet* fs, int retries) {
     st->trace_launches = launches;
     st->levels = levels;
     st->overflow_retries = retries;
-}
-
-// Multi-process distributed frames: did ANY rank's queues overflow?  Every rank asks for every
-// frame in the same order (frames complete in submission order), over the control communicator
-// on its own stream -- not behind the gathers queued on the context stream, so the host waits for
-// the other ranks' answers only, never for later frames.
-bool any_rank_overflowed(pgrt_ctx* ctx, bool mine) {
-    if (!ctx->comm_ctl) return mine;
-    ctx->ctl_buf.alloc(1);
-    int v = mine ? 1 : 0;
-    PGRT_HIP(hipMemcpyAsync(ctx->ctl_buf.p, &v, sizeof(int), hipMemcpyHostToDevice, ctx->ctl_stream));
-    const ncclResult_t r = ncclAllReduce(ctx->ctl_buf.p, ctx->ctl_buf.p, 1, ncclInt32, ncclMax, ctx->comm_ctl,
-                                         ctx->ctl_stream);
-    if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string("ncclAllReduce (overflow flag): ") + ncclGetErrorString(r));
-    PGRT_HIP(hipMemcpyAsync(&v, ctx->ctl_buf.p, sizeof(int), hipMemcpyDeviceToHost, ctx->ctl_stream));
-    PGRT_HIP(hipStreamSynchronize(ctx->ctl_stream));
-    return v != 0;
+    if (fs->stamp_used > 0 && fs->K > 0) {  // the call's launch timeline: (first wave start, last wave end) per launch
+        ctx->stamp_host.resize((size_t)fs->stamp_used * 2);
+        hipStream_t s0 = fs->slots[0]->stream;
+        PGRT_HIP(hipMemcpyAsync(ctx->stamp_host.data(), fs->stamps.p, (size_t)fs->stamp_used * 16,
+                                hipMemcpyDeviceToHost, s0));
+        PGRT_HIP(hipStreamSynchronize(s0));
+        for (const StampLaunch& l : fs->stamp_launches) {
+            unsigned long long a = ~0ull, b = 0;
+            int waves = 0;
+            for (long long w = l.offset; w < l.offset + l.waves; ++w) {
+                const unsigned long long t0 = ctx->stamp_host[2 * w], t1 = ctx->stamp_host[2 * w + 1];
+                if (t0 == 0 || t1 < t0) continue;  // not a stamp of this launch
+                a = std::min(a, t0);
+                b = std::max(b, t1);
+                ++waves;
+            }
+            if (!waves) continue;
+            ctx->timeline.push_back(pgrt_timeline_rec{fs->ticket, l.slot, l.kind, l.level, waves, a, b});
+        }
+        fs->stamp_used = 0;
+    }
 }
 
 void gather_frame(pgrt_ctx* ctx, FrameSet* fs);
+void regather_rank0(pgrt_ctx* ctx, FrameSet* fs, bool own, const std::vector<int>& peers);
+
+// a multi-process distributed frame whose gather goes over RCCL (the overflow flags ride along)
+bool rccl_gather(const pgrt_ctx* ctx, const FrameSet* fs) {
+    return fs->distributed && !ctx->emulated && fs->deal.world > 1 && ctx->comm != nullptr;
+}
 
 // Wait for fs's frame, re-render it after a queue overflow (larger queues), fill fs->stats.  A
-// distributed frame's gather was queued with the frame (device-ordered, start_frame): when any
-// rank overflowed, every rank re-renders and re-gathers it, so the collectives stay matched.
+// distributed frame's gather was queued with the frame (device-ordered, start_frame).  There is no
+// control collective: a rank whose queues overflowed re-renders its tiles and sends them again;
+// rank 0 learns which ranks did from the flag at the tail of every rank's send (gather_end copies
+// them to host memory behind the unpack), receives those ranks' tiles again and unpacks them (and
+// its own, when it overflowed).  Every rank posts its sends / receives for a frame when that frame
+// is collected, and frames are collected in submission order on every rank, so the point-to-point
+// operations stay matched.  Non-zero ranks never wait for another rank; rank 0 waits for the
+// frame's own gather only.
 void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
     int retries = 0;
+    const bool rccl = rccl_gather(ctx, fs);
     for (;;) {
         const bool mine = read_frame_counters(ctx, fs);
-        const bool any = fs->distributed ? any_rank_overflowed(ctx, mine) : mine;
-        if (!any) break;
-        rerender_frame(ctx, fs, mine, retries);
-        if (fs->distributed) gather_frame(ctx, fs);
+        if (!rccl || ctx->rank != 0) {
+            if (!mine) break;
+            rerender_frame(ctx, fs, true, retries);
+            if (fs->distributed) gather_frame(ctx, fs);  // rank != 0: the tiles again, to rank 0
+            continue;
+        }
+        PGRT_HIP(hipEventSynchronize(fs->ev_flags));
+        std::vector<int> peers;
+        for (int r = 1; r < fs->deal.world; ++r)
+            if (fs->peer_flags[r]) peers.push_back(r);
+        if (!mine && peers.empty()) break;
+        if (mine) {
+            rerender_frame(ctx, fs, true, retries);
+        } else {
+            PGRT_REQUIRE(++retries < 8, PGRT_ERR_OUT_OF_MEMORY, "ray queues kept overflowing");
+        }
+        regather_rank0(ctx, fs, mine, peers);
     }
     frame_stats(ctx, fs, retries);
 }
@@ -1318,6 +1369,17 @@ void gather_begin(pgrt_ctx* ctx, FrameSet* fs, UnpackSrc& u) {
     u = unpack_layout(fs->deal, fs->cam_w, fs->cam_h);
     for (int j = 0; j < fs->K; ++j) PGRT_HIP(hipStreamWaitEvent(ctx->stream, fs->slots[j]->ev_done, 0));
     PGRT_HIP(hipEventRecord(fs->ev_g0, ctx->stream));
+    if (!ctx->emulated && fs->deal.world > 1 && ctx->comm) {
+        // this rank's overflow flag after its tiles (the tail of its send): the exported counters
+        FlagSrc f{};
+        f.K = std::min(fs->K, 4);
+        for (int j = 0; j < f.K; ++j) {
+            f.fc[j] = fs->slots[j]->pinned_fc;
+            f.n[j] = (int)fs->slots[j]->host_fc.size();
+        }
+        const size_t tiles = (size_t)fs->nframes * u.count[ctx->rank] * kTile * kTile * 3;
+        launch_overflow_flag(f, reinterpret_cast<int*>(fs->tilebuf.p + tiles), ctx->stream);
+    }
 }
 
 void gather_post(pgrt_ctx* ctx, FrameSet* fs, UnpackSrc& u) {
@@ -1342,27 +1404,37 @@ void gather_post(pgrt_ctx* ctx, FrameSet* fs, UnpackSrc& u) {
     auto ok = [](ncclResult_t r, const char* what) {
         if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(r));
     };
+    // every rank's send: its tiles, then kGatherTail floats (the overflow flag, gather_begin)
     if (me == 0) {
-        const size_t others = (size_t)F * (u.prefix[d.world] - u.count[0]) * tile_floats;
+        const size_t others = (size_t)F * (u.prefix[d.world] - u.count[0]) * tile_floats + (size_t)kGatherTail * (d.world - 1);
         ctx->gathered.alloc(std::max<size_t>(1, others));
         for (int r = 1; r < d.world; ++r) {
-            float* dst = ctx->gathered.p + (size_t)F * (u.prefix[r] - u.count[0]) * tile_floats;
+            float* dst = ctx->gathered.p + (size_t)F * (u.prefix[r] - u.count[0]) * tile_floats + (size_t)kGatherTail * (r - 1);
             u.src[r] = dst;
-            if (u.count[r] > 0)
-                ok(ncclRecv(dst, (size_t)F * u.count[r] * tile_floats, ncclFloat, r, ctx->comm, ctx->stream),
+            if (!fs->regather || fs->regather_peer[r])
+                ok(ncclRecv(dst, (size_t)F * u.count[r] * tile_floats + kGatherTail, ncclFloat, r, ctx->comm, ctx->stream),
                    "ncclRecv");
         }
         u.src[0] = fs->tilebuf.p;
-    } else if (u.count[me] > 0) {
-        ok(ncclSend(fs->tilebuf.p, (size_t)F * u.count[me] * tile_floats, ncclFloat, 0, ctx->comm, ctx->stream),
+    } else {
+        ok(ncclSend(fs->tilebuf.p, (size_t)F * u.count[me] * tile_floats + kGatherTail, ncclFloat, 0, ctx->comm,
+                    ctx->stream),
            "ncclSend");
     }
 }
 
-void gather_end(pgrt_ctx* ctx, FrameSet* fs, const UnpackSrc& u) {
+void gather_end(pgrt_ctx* ctx, FrameSet* fs, const UnpackSrc& u_in) {
     PGRT_HIP(hipEventRecord(fs->ev_g1, ctx->stream));
+    UnpackSrc u = u_in;
+    if (fs->regather)  // a re-gather: only the re-rendered ranks' tiles (the others' were unpacked already)
+        for (int r = 0; r < fs->deal.world; ++r)
+            if (!fs->regather_peer[r]) u.src[r] = nullptr;
     if (ctx->rank == 0)  // every frame of the call in one launch (grid.y = frame)
         launch_unpack_tiles(u, fs->dist_fb, fs->cam_w, fs->cam_h, fs->deal, 3, ctx->stream, 0, fs->nframes);
+    if (ctx->rank == 0 && rccl_gather(ctx, fs) && !ctx->group) {  // the peers' overflow flags -> host
+        launch_peer_flags(u, fs->deal.world, (size_t)fs->nframes * kTile * kTile * 3, fs->peer_flags, ctx->stream);
+        PGRT_HIP(hipEventRecord(fs->ev_flags, ctx->stream));
+    }
     PGRT_HIP(hipEventRecord(fs->ev_g2, ctx->stream));
     // the set's next frame overwrites its tile buffer only after the gather has read it
     PGRT_HIP(hipEventRecord(fs->ev_ready, ctx->stream));
@@ -1381,6 +1453,23 @@ void gather_frame(pgrt_ctx* ctx, FrameSet* fs) {
     gather_post(ctx, fs, u);
     if (group) ok(ncclGroupEnd(), "ncclGroupEnd");
     gather_end(ctx, fs, u);
+}
+
+// rank 0 after an overflow: receive the re-rendered tiles of `peers` again (their re-sends) and
+// unpack those ranks' tiles, and its own when own (re-rendered in place)
+void regather_rank0(pgrt_ctx* ctx, FrameSet* fs, bool own, const std::vector<int>& peers) {
+    fs->regather = true;
+    std::fill(fs->regather_peer, fs->regather_peer + kMaxRanks, 0);
+    fs->regather_peer[0] = own ? 1 : 0;
+    for (int r : peers) fs->regather_peer[r] = 1;
+    std::fill(fs->peer_flags, fs->peer_flags + kMaxRanks, 0);
+    try {
+        gather_frame(ctx, fs);
+    } catch (...) {
+        fs->regather = false;
+        throw;
+    }
+    fs->regather = false;
 }
 
 // device ms of a completed frame's gather (ncclGather incl. the wait for peers) + unpack
@@ -1457,7 +1546,8 @@ void start_frame(pgrt_ctx* ctx, FrameSet* fs, const pgrt_render_params* p, std::
     if (distributed) {
         // this rank's tiles of every frame, frame-major (the gather's layout, unpack_layout)
         fs->deal = deal;
-        fs->tilebuf.alloc(std::max<size_t>(1, (size_t)nframes * tiles.size() * kTile * kTile * 3));
+        // + the overflow flag's tail (gather_begin / collect_frame)
+        fs->tilebuf.alloc((size_t)nframes * tiles.size() * kTile * kTile * 3 + kGatherTail);
         fs->frame_out_tiles = (int)tiles.size();
         out = fs->tilebuf.p;
         out_mode = 2;
@@ -1821,18 +1911,10 @@ int pgrt_set_config(pgrt_ctx* ctx, const pgrt_config* cfg) {
         PGRT_REQUIRE(cfg->max_batch_rays >= 0 && cfg->max_batch_rays <= (1ll << 29), PGRT_ERR_INVALID_ARGUMENT,
                      "max_batch_rays must be in [0, 2^29]");
         PGRT_REQUIRE(cfg->max_batches_in_flight >= 0, PGRT_ERR_INVALID_ARGUMENT, "max_batches_in_flight must be >= 0");
-        PGRT_REQUIRE(cfg->ray_binning >= -1 && cfg->ray_binning <= 1, PGRT_ERR_INVALID_ARGUMENT,
-                     "ray_binning must be 0 / -1 (off, the default) or 1 (on)");
         PGRT_REQUIRE(cfg->packet_budget >= -1, PGRT_ERR_INVALID_ARGUMENT,
                      "packet_budget must be -1 (off), 0 (default) or a step count");
-        PGRT_REQUIRE(cfg->tail_level >= -1 && cfg->tail_level < kMaxLevels, PGRT_ERR_INVALID_ARGUMENT,
-                     "tail_level must be 0 / -1 (off, the default) or a level in [1, 15]");
         PGRT_REQUIRE(cfg->call_order == 0 || cfg->call_order == 1 || cfg->call_order == -1, PGRT_ERR_INVALID_ARGUMENT,
                      "call_order must be 0 (default), 1 (level 0 in submission order) or -1 (free)");
-        PGRT_REQUIRE(cfg->bvh_layout == 0 || cfg->bvh_layout == 1, PGRT_ERR_INVALID_ARGUMENT,
-                     "bvh_layout must be 0 (builder order) or 1 (sibling pairs)");
-        PGRT_REQUIRE(cfg->packet_width == 0 || cfg->packet_width == 2 || cfg->packet_width == 8,
-                     PGRT_ERR_INVALID_ARGUMENT, "packet_width must be 0, 2 or 8");
         PGRT_REQUIRE(cfg->rank0_share_a >= 0 && cfg->rank0_share_a <= 64 && cfg->rank0_share_b >= 0 &&
                          cfg->rank0_share_b <= 64,
                      PGRT_ERR_INVALID_ARGUMENT, "rank0_share_a / rank0_share_b must be in [0, 64]");
@@ -2182,10 +2264,6 @@ int pgrt_comm_init(pgrt_ctx* ctx, int world, int rank, const char id[128]) {
         PGRT_REQUIRE(!ctx->group, PGRT_ERR_INVALID_ARGUMENT,
                      "a multi-device context (pgrt_create_devices) has its own communicators");
         drain_frames(ctx);
-        if (ctx->comm_ctl) {
-            (void)ncclCommDestroy(ctx->comm_ctl);
-            ctx->comm_ctl = nullptr;
-        }
         if (ctx->comm) {
             (void)ncclCommDestroy(ctx->comm);
             ctx->comm = nullptr;
@@ -2197,9 +2275,6 @@ int pgrt_comm_init(pgrt_ctx* ctx, int world, int rank, const char id[128]) {
         std::memcpy(u.internal, id, 128);
         ncclResult_t r = ncclCommInitRank(&ctx->comm, world, u, rank);
         if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
-        r = ncclCommSplit(ctx->comm, 0, rank, &ctx->comm_ctl, nullptr);
-        if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string("ncclCommSplit: ") + ncclGetErrorString(r));
-        if (!ctx->ctl_stream) PGRT_HIP(hipStreamCreateWithFlags(&ctx->ctl_stream, hipStreamNonBlocking));
     });
 }
 
@@ -2251,6 +2326,7 @@ int pgrt_set_frames_in_flight(pgrt_ctx* ctx, int n) {
     return guarded(ctx, [&] {
         drain_frames(ctx);
         ctx->frames_in_flight = n;
+        for (pgrt_ctx* m : ctx->members) m->frames_in_flight = n;  // a multi-device context: every rank
     });
 }
 
@@ -2490,6 +2566,23 @@ int pgrt_render_distributed(pgrt_ctx* ctx, const pgrt_render_params* p, float* r
     rc = pgrt_render_distributed_device(ctx, p, ctx->rank == 0 ? ctx->fb_dev.p : nullptr, st);
     if (rc != PGRT_OK || ctx->rank != 0 || !rgba_host) return rc;
     return pgrt_copy_to_host(ctx, rgba_host, ctx->fb_dev.p, (size_t)W * H * 4 * sizeof(float));
+}
+
+int pgrt_timeline_enable(pgrt_ctx* ctx, int on) {
+    if (!ctx) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        drain_frames(ctx);  // pending frames were enqueued with the old choice
+        ctx->timeline_on = on != 0;
+    });
+}
+
+int pgrt_timeline_read(pgrt_ctx* ctx, pgrt_timeline_rec* out, int max, int* n) {
+    if (!ctx || !n || max < 0 || (max > 0 && !out)) return PGRT_ERR_INVALID_ARGUMENT;
+    const int k = (int)std::min<size_t>((size_t)max, ctx->timeline.size());
+    std::copy(ctx->timeline.begin(), ctx->timeline.begin() + k, out);
+    ctx->timeline.erase(ctx->timeline.begin(), ctx->timeline.begin() + k);
+    *n = k;
+    return PGRT_OK;
 }
 
 int pgrt_frame_diag(const pgrt_ctx* ctx, pgrt_level_diag* out, int max_levels) {

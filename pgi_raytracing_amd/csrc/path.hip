@@ -18,6 +18,8 @@
 #include "shade_ray.hpp"
 #include "path.hpp"
 
+#include "stamps.hpp"
+
 namespace pgrt {
 
 constexpr int kPathBlock = 256;
@@ -67,6 +69,7 @@ __global__ __launch_bounds__(kPathBlock) void k_path_shade(SceneView s, FramePar
                                                            const int4* __restrict__ tiles, int level, Queue q,
                                                            Queue next, PathState ps, ShadowQueue sq,
                                                            FrameCounters* fc) {
+    PGRT_STAMP_BEGIN(s.stamps);
     __shared__ float lut255[256];
     __shared__ DevMaterial smat[LDS_TABLES ? kLdsMats : 1];
     __shared__ DevTexture stex[LDS_TABLES ? kLdsTex : 1];
@@ -187,11 +190,13 @@ __global__ __launch_bounds__(kPathBlock) void k_path_shade(SceneView s, FramePar
         }
     }
     if (__lane_id() == 0 && refr_w && level + 1 < kMaxLevels) atomicAdd(&fc->refract[level + 1], refr_w);
+    PGRT_STAMP_END(s.stamps);
 }
 
 // lit shadow terms of one bounce, added to the path accumulators in light order
 __global__ __launch_bounds__(kPathBlock) void k_path_resolve(SceneView s, int level, ShadowQueue sq, PathState ps,
                                                              const FrameCounters* fc) {
+    PGRT_STAMP_BEGIN(s.stamps);
     const int n = min(fc_shadow(*fc, level), sq.cap);
     for (int k = blockIdx.x * kPathBlock + threadIdx.x; k < n; k += gridDim.x * kPathBlock) {
         const float4 c0 = sq.contrib[k];
@@ -210,14 +215,17 @@ __global__ __launch_bounds__(kPathBlock) void k_path_resolve(SceneView s, int le
         }
         ps.acc[pid] = acc;
     }
+    PGRT_STAMP_END(s.stamps);
 }
 
-void launch_path_shade(const SceneView& s, const FrameParams& fp, int width, const int4* tiles, int level, Queue q,
+void launch_path_shade(const SceneView& s_in, const FrameParams& fp, int width, const int4* tiles, int level, Queue q,
                        Queue next, const PathState& ps, ShadowQueue sq, FrameCounters* fc, int max_count, int expect,
                        hipStream_t stream) {
     if (max_count <= 0) return;
     const int ex = expect > 0 && expect < max_count ? expect : max_count;
     const int grid = std::max(1, std::min(4096, ceil_div(ex, kPathBlock)));
+    SceneView s = s_in;
+    s.stamps = stamp_next(kStampPathShade, level, grid, kPathBlock);
     if (s.nmat <= kLdsMats && s.ntex <= kLdsTex)
         hipLaunchKernelGGL((k_path_shade<true>), dim3(grid), dim3(kPathBlock), 0, stream, s, fp, width, tiles, level,
                            q, next, ps, sq, fc);
@@ -226,11 +234,13 @@ void launch_path_shade(const SceneView& s, const FrameParams& fp, int width, con
                            q, next, ps, sq, fc);
 }
 
-void launch_path_resolve(const SceneView& s, int level, ShadowQueue sq, const PathState& ps, const FrameCounters* fc,
+void launch_path_resolve(const SceneView& s_in, int level, ShadowQueue sq, const PathState& ps, const FrameCounters* fc,
                          int max_count, int expect, hipStream_t stream) {
     if (max_count <= 0) return;
     const int ex = expect > 0 && expect < max_count ? expect : max_count;
     const int grid = std::max(1, std::min(4096, ceil_div(ex, kPathBlock)));
+    SceneView s = s_in;
+    s.stamps = stamp_next(kStampPathResolve, level, grid, kPathBlock);
     hipLaunchKernelGGL(k_path_resolve, dim3(grid), dim3(kPathBlock), 0, stream, s, level, sq, ps, fc);
 }
 

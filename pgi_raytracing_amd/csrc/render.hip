@@ -15,6 +15,8 @@
 #include "camera_ops.hpp"
 #include "shade_ray.hpp"
 #include "tiles.hpp"
+#include "stamps.hpp"
+#include "cache_ops.hpp"
 
 namespace pgrt {
 
@@ -30,21 +32,27 @@ static int grid_for(int max_count, int expect) {
 // ------------------------------------------------------------------ ray generation
 
 __global__ __launch_bounds__(kBlock) void k_raygen(CameraView cam, FrameParams fp, const int4* __restrict__ tiles,
-                                                   Queue q, int n0, FrameCounters* fc) {
+                                                   Queue q, int n0, FrameCounters* fc,
+                                                   unsigned long long* __restrict__ stamps) {
+    PGRT_STAMP_BEGIN(stamps);
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (i == 0) fc->count0 = n0;
-    if (i >= n0) return;
-    float4 o, d;
-    const bool valid = primary_ray(cam, fp, tiles, i, o, d);
-    q.ro[i] = o;
-    q.rd[i] = d;
-    q.time[i] = valid ? PGRT_IOR_AIR : 0.0f;  // raytracer.cpp:416
+    if (i < n0) {
+        float4 o, d;
+        const bool valid = primary_ray(cam, fp, tiles, i, o, d);
+        st_stream(q.ro + i, o);
+        st_stream(q.rd + i, d);
+        st_stream_nt(q.time + i, valid ? PGRT_IOR_AIR : 0.0f);  // raytracer.cpp:416
+    }
+    PGRT_STAMP_END(stamps);
 }
 
 void launch_raygen(const CameraView& cam, const FrameParams& fp, const int4* tiles, Queue q, int n0,
                    FrameCounters* fc, hipStream_t stream) {
     if (n0 <= 0) return;
-    hipLaunchKernelGGL(k_raygen, dim3(ceil_div(n0, kBlock)), dim3(kBlock), 0, stream, cam, fp, tiles, q, n0, fc);
+    const int grid = ceil_div(n0, kBlock);
+    hipLaunchKernelGGL(k_raygen, dim3(grid), dim3(kBlock), 0, stream, cam, fp, tiles, q, n0, fc,
+                       stamp_next(kStampRaygen, 0, grid, kBlock));
 }
 
 // ------------------------------------------------------------------ shading (trace body)
@@ -65,6 +73,7 @@ template <bool LDS_TABLES, bool L0F>
 __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : 6) void k_shade(SceneView s, FrameParams fp, int level, Queue q, Queue next,
                                                        LevelNodes nodes, ShadowQueue sq, FrameCounters* fc,
                                                        PinholeOrigin l0, L0Final l0f) {
+    PGRT_STAMP_BEGIN(s.stamps);
     __shared__ float lut255[256];
     __shared__ DevMaterial smat[LDS_TABLES ? kLdsMats : 1];
     __shared__ DevTexture stex[LDS_TABLES ? kLdsTex : 1];
@@ -95,18 +104,18 @@ __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : 6) void k_shade
     constexpr bool l0final = L0F;
     const float4 no_hit = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
     auto load_hit = [&](int k) {
-        if (!l0final) return q.hit[k];
+        if (!l0final) return ld_stream(q.hit + k);
         const unsigned long long hm = l0f.hit[__builtin_amdgcn_readfirstlane(k >> 6)];
-        return ((hm >> (k & 63)) & 1ull) ? q.hit[k] : no_hit;
+        return ((hm >> (k & 63)) & 1ull) ? ld_stream(q.hit + k) : no_hit;
     };
     {
         const int i0 = blockIdx.x * kShadeBlock + tid;
         if (i0 < n) {
-            nx_d = q.rd[i0];
+            nx_d = ld_stream(q.rd + i0);
             nx_h = load_hit(i0);
             if (!from_cam) {
-                nx_o = q.ro[i0];
-                nx_t = q.time[i0];
+                nx_o = ld_stream(q.ro + i0);
+                nx_t = ld_stream_nt(q.time + i0);
             }
         }
     }
@@ -117,11 +126,11 @@ __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : 6) void k_shade
         const float4 cur_o = from_cam ? cam_o : nx_o;
         const float cur_t = from_cam ? (cur_d.w >= 0.0f ? PGRT_IOR_AIR : 0.0f) : nx_t;
         if (i + stride < n) {
-            nx_d = q.rd[i + stride];
+            nx_d = ld_stream(q.rd + i + stride);
             nx_h = load_hit(i + stride);
             if (!from_cam) {
-                nx_o = q.ro[i + stride];
-                nx_t = q.time[i + stride];
+                nx_o = ld_stream(q.ro + i + stride);
+                nx_t = ld_stream_nt(q.time + i + stride);
             }
         }
         ShadeOut r;
@@ -140,7 +149,7 @@ __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : 6) void k_shade
             // the others are completed by the finish (n is a multiple of 64: whole waves)
             const bool fin = active && r.kind == 0;
             const unsigned long long pend = __ballot(active && !fin);
-            if (active && __lane_id() == 0) l0f.pending[i >> 6] = pend;
+            if (active && __lane_id() == 0) st_stream_nt(l0f.pending + (i >> 6), pend);
             if (fin) store_final_1spp(fp, l0f.tiles, l0f.fo, i, r.color);
             if (active && !fin) shade_emit(s, mats, level, i, r, sl, next, nodes, sq, fc);
         } else if (active) {
@@ -148,14 +157,17 @@ __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : 6) void k_shade
         }
     }
     shade_refract_flush(fc, level, refr_acc);
+    PGRT_STAMP_END(s.stamps);
 }
 
-void launch_shade(const SceneView& s, const FrameParams& fp, int level, Queue q, Queue next, LevelNodes nodes,
+void launch_shade(const SceneView& s_in, const FrameParams& fp, int level, Queue q, Queue next, LevelNodes nodes,
                   ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect,
                   const PinholeOrigin& l0, const L0Final& l0f) {
     if (max_count <= 0) return;
     const int per_block = kShadeBlock / kBlock;  // grid_for counts kBlock-thread blocks
     const int grid = std::max(1, grid_for(max_count, expect) / per_block);
+    SceneView s = s_in;
+    s.stamps = stamp_next(kStampShade, level, grid, kShadeBlock);
     const bool lds = s.nmat <= kLdsMats && s.ntex <= kLdsTex;
 #define PGRT_LAUNCH_SHADE(T, F)                                                                                   \
     hipLaunchKernelGGL((k_shade<T, F>), dim3(grid), dim3(kShadeBlock), 0, stream, s, fp, level, q, next, nodes, sq, \
@@ -184,13 +196,13 @@ __device__ __forceinline__ float4 opaque_color(const SceneView& s, const ShadowQ
         const int k = base + j;
         bool lit;  // is_illuminated (raytracer.cpp:163-173): closest hit decides
         if (sq.lit) {
-            lit = sq.lit[k] != 0;  // decided by the shadow trace (compact queue)
+            lit = ld_stream_nt(sq.lit + k) != 0;  // decided by the shadow trace (compact queue)
         } else {
-            const int prim = __float_as_int(sq.hit[k].w);
+            const int prim = __float_as_int(ld_stream(sq.hit + k).w);
             lit = prim < 0 || s.prim_glass[prim] != 0;  // no occluder, or a dielectric one
         }
         if (lit) {
-            const float4 c = sq.contrib[k];
+            const float4 c = ld_stream(sq.contrib + k);
             blue += c.x;
             green += c.y;
             red += c.z;
@@ -202,40 +214,44 @@ __device__ __forceinline__ float4 opaque_color(const SceneView& s, const ShadowQ
 // final colour of node i of a level whose children (next level) are final
 __device__ __forceinline__ float4 node_color(const SceneView& s, const ShadowQueue& sq, LevelNodes nodes,
                                              const float4* __restrict__ child, int i) {
-    const int4 lk = nodes.link[i];
+    const int4 lk = ld_stream(nodes.link + i);
     if (lk.x >= 0) {
-        const float4 att = nodes.att[i];
-        const float4 refl = child[lk.x];
+        const float4 att = ld_stream(nodes.att + i);
+        const float4 refl = ld_stream(child + lk.x);
         // raytracer.cpp:318-319 (refraction present) or :321 (total internal reflection)
-        const float4 c = lk.y >= 0 ? mix_srgb(refl, child[lk.y], att.w) : refl;
+        const float4 c = lk.y >= 0 ? mix_srgb(refl, ld_stream(child + lk.y), att.w) : refl;
         return make_float4(c.x * att.x, c.y * att.y, c.z * att.z, 1);
     }
     if (lk.z >= 0) return opaque_color(s, sq, lk.z, lk.w);
-    return nodes.color[i];
+    return ld_stream(nodes.color + i);
 }
 
 __global__ __launch_bounds__(kBlock) void k_combine(SceneView s, int level, LevelNodes nodes,
                                                     const float4* __restrict__ child, ShadowQueue sq,
                                                     const FrameCounters* fc, int cap) {
+    PGRT_STAMP_BEGIN(s.stamps);
     const int n = min(fc_count(*fc, level), cap);
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        const int4 lk = nodes.link[i];
+        const int4 lk = ld_stream(nodes.link + i);
         if (lk.x < 0 && lk.z < 0) continue;  // colour written by k_shade
-        nodes.color[i] = node_color(s, sq, nodes, child, i);
+        st_stream(nodes.color + i, node_color(s, sq, nodes, child, i));
     }
+    PGRT_STAMP_END(s.stamps);
 }
 
-void launch_combine(const SceneView& s, int level, LevelNodes nodes, const float4* child, ShadowQueue sq,
+void launch_combine(const SceneView& s_in, int level, LevelNodes nodes, const float4* child, ShadowQueue sq,
                     const FrameCounters* fc, int max_count, hipStream_t stream, int expect) {
     if (max_count <= 0) return;
     const int grid = grid_for(max_count, expect);
+    SceneView s = s_in;
+    s.stamps = stamp_next(kStampCombine, level, grid, kBlock);
     hipLaunchKernelGGL(k_combine, dim3(grid), dim3(kBlock), 0, stream, s, level, nodes, child, sq, fc, max_count);
 }
 
-__global__ __launch_bounds__(kBlock) void k_finish(SceneView s, FrameParams fp, const int4* __restrict__ tiles,
-                                                   LevelNodes l0, const float4* __restrict__ child, ShadowQueue sq,
-                                                   float4* __restrict__ accum, FrameOut fo, int npix, int first,
-                                                   int last, int resolved) {
+__device__ __forceinline__ void finish_body(const SceneView& s, const FrameParams& fp, const int4* __restrict__ tiles,
+                                            const LevelNodes& l0, const float4* __restrict__ child,
+                                            const ShadowQueue& sq, float4* __restrict__ accum, const FrameOut& fo,
+                                            int npix, int first, int last, int resolved) {
     const int p = blockIdx.x * kBlock + threadIdx.x;
     if (p >= npix) return;
     float4 acc = first ? make_float4(0.0f, 0.0f, 0.0f, 1.0f) : accum[p];
@@ -263,84 +279,36 @@ __global__ __launch_bounds__(kBlock) void k_finish(SceneView s, FrameParams fp, 
     store_pixel(fp, tiles, fo, p, px, py, o);
 }
 
+__global__ __launch_bounds__(kBlock) void k_finish(SceneView s, FrameParams fp, const int4* __restrict__ tiles,
+                                                   LevelNodes l0, const float4* __restrict__ child, ShadowQueue sq,
+                                                   float4* __restrict__ accum, FrameOut fo, int npix, int first,
+                                                   int last, int resolved) {
+    PGRT_STAMP_BEGIN(s.stamps);
+    finish_body(s, fp, tiles, l0, child, sq, accum, fo, npix, first, last, resolved);
+    PGRT_STAMP_END(s.stamps);
+}
+
 // 1-spp batch whose level-0 shade finished every final-colour pixel (L0Final): the pixels of the
 // pending masks only
 __global__ __launch_bounds__(kBlock) void k_finish_pending(SceneView s, FrameParams fp, const int4* __restrict__ tiles,
                                                            LevelNodes l0, const float4* __restrict__ child,
                                                            ShadowQueue sq, FrameOut fo,
                                                            const unsigned long long* __restrict__ pending, int npix) {
+    PGRT_STAMP_BEGIN(s.stamps);
     const int p = blockIdx.x * kBlock + threadIdx.x;
-    if (p >= npix) return;
-    const unsigned long long pm = pending[__builtin_amdgcn_readfirstlane(p >> 6)];
-    if (((pm >> (p & 63)) & 1ull) == 0ull) return;
-    store_final_1spp(fp, tiles, fo, p, node_color(s, sq, l0, child, p));
-}
-
-// 1-spp pending pixels resolved in one launch: each pixel's ray tree is evaluated depth-first
-// (post-order, the reflection child before the refraction child), so the per-level k_combine
-// passes and the finish are one kernel instead of max_level of them.  Every node's colour is
-// node_color's arithmetic on its children's colours, so the pixels are identical to the
-// level-by-level combine.  The stack is indexed by level (a child is always one level down).
-__global__ __launch_bounds__(kBlock) void k_resolve_pending(SceneView s, FrameParams fp, const int4* __restrict__ tiles,
-                                                            AllLevelNodes lv, ShadowQueue sq, FrameOut fo,
-                                                            const unsigned long long* __restrict__ pending, int npix) {
-    const int p = blockIdx.x * kBlock + threadIdx.x;
-    if (p >= npix) return;
-    const unsigned long long pm = pending[__builtin_amdgcn_readfirstlane(p >> 6)];
-    if (((pm >> (p & 63)) & 1ull) == 0ull) return;
-    int idx[kMaxLevels];
-    int ph[kMaxLevels];  // 0: enter, 1: reflection returned, 2: refraction returned
-    float4 refl[kMaxLevels];
-    int L = 0;
-    idx[0] = p;
-    ph[0] = 0;
-    float4 v = make_float4(0, 0, 0, 0);  // colour of the node finished last
-    for (;;) {
-        const int i = idx[L];
-        const int4 lk = lv.link[L][i];
-        if (lk.x >= 0) {
-            if (ph[L] == 0) {  // descend: reflection child first
-                ph[L] = 1;
-                idx[L + 1] = lk.x;
-                ph[L + 1] = 0;
-                ++L;
-                continue;
-            }
-            if (ph[L] == 1 && lk.y >= 0) {  // reflection done: the refraction child
-                refl[L] = v;
-                ph[L] = 2;
-                idx[L + 1] = lk.y;
-                ph[L + 1] = 0;
-                ++L;
-                continue;
-            }
-            const float4 att = lv.att[L][i];
-            // raytracer.cpp:318-319 (refraction present) or :321 (total internal reflection)
-            const float4 c = ph[L] == 2 ? mix_srgb(refl[L], v, att.w) : v;
-            v = make_float4(c.x * att.x, c.y * att.y, c.z * att.z, 1);
-        } else if (lk.z >= 0) {
-            v = opaque_color(s, sq, lk.z, lk.w);
-        } else {
-            v = lv.color[L][i];
-        }
-        if (L == 0) break;
-        --L;
+    if (p < npix) {
+        const unsigned long long pm = pending[__builtin_amdgcn_readfirstlane(p >> 6)];
+        if (((pm >> (p & 63)) & 1ull) != 0ull) store_final_1spp(fp, tiles, fo, p, node_color(s, sq, l0, child, p));
     }
-    store_final_1spp(fp, tiles, fo, p, v);
+    PGRT_STAMP_END(s.stamps);
 }
 
-void launch_resolve_pending(const SceneView& s, const FrameParams& fp, const int4* tiles, const AllLevelNodes& lv,
-                            ShadowQueue sq, const FrameOut& fo, const unsigned long long* pending, int npix,
-                            hipStream_t stream) {
-    if (npix <= 0) return;
-    hipLaunchKernelGGL(k_resolve_pending, dim3(ceil_div(npix, kBlock)), dim3(kBlock), 0, stream, s, fp, tiles, lv, sq,
-                       fo, pending, npix);
-}
-
-void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles, LevelNodes l0, const float4* child,
+void launch_finish(const SceneView& s_in, const FrameParams& fp, const int4* tiles, LevelNodes l0, const float4* child,
                    ShadowQueue sq, float4* accum, const FrameOut& fo, int npix, bool first, bool last, bool resolved,
                    const unsigned long long* pending, hipStream_t stream) {
     if (npix <= 0) return;
+    SceneView s = s_in;
+    s.stamps = stamp_next(kStampFinish, 0, ceil_div(npix, kBlock), kBlock);
     if (pending) {
         hipLaunchKernelGGL(k_finish_pending, dim3(ceil_div(npix, kBlock)), dim3(kBlock), 0, stream, s, fp, tiles, l0,
                            child, sq, fo, pending, npix);
@@ -355,8 +323,8 @@ void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles,
 // u.src[r] holds rank r's tiles of `frames` frames (frame-major, u.count[r] tiles per frame in
 // the rank's local order of the tiles.hpp deal, `channels` floats per pixel); blockIdx.y = frame
 // - frame0; every rank's tiles of that frame are unpacked into rgba + frame * W*H*4
-__global__ __launch_bounds__(kBlock) void k_unpack(UnpackSrc u, float4* __restrict__ rgba, int width, int height,
-                                                   TileDeal deal, int channels, int frame0) {
+__device__ __forceinline__ void unpack_body(const UnpackSrc& u, float4* __restrict__ rgba, int width, int height,
+                                            const TileDeal& deal, int channels, int frame0) {
     const int world = deal.world;
     const int frame = frame0 + (int)blockIdx.y;
     const long long idx = (long long)blockIdx.x * kBlock + threadIdx.x;
@@ -373,17 +341,52 @@ __global__ __launch_bounds__(kBlock) void k_unpack(UnpackSrc u, float4* __restri
     if (x >= width || y >= height) return;  // padding of an edge tile
     const long long src = ((long long)frame * u.count[rank] + j) * kTile * kTile + p;
     const float* g = u.src[rank];
+    if (!g) return;  // a rank left out of this unpack (a re-gather of the re-rendered ranks only)
     rgba[(size_t)frame * width * height + (size_t)y * width + x] =
         channels == 4 ? reinterpret_cast<const float4*>(g)[src]
                       : make_float4(g[src * 3], g[src * 3 + 1], g[src * 3 + 2], 1.0f);
+}
+
+__global__ __launch_bounds__(kBlock) void k_unpack(UnpackSrc u, float4* __restrict__ rgba, int width, int height,
+                                                   TileDeal deal, int channels, int frame0,
+                                                   unsigned long long* __restrict__ stamps) {
+    PGRT_STAMP_BEGIN(stamps);
+    unpack_body(u, rgba, width, height, deal, channels, frame0);
+    PGRT_STAMP_END(stamps);
 }
 
 void launch_unpack_tiles(const UnpackSrc& u, float* rgba, int width, int height, const TileDeal& deal, int channels,
                          hipStream_t stream, int frame0, int nframes) {
     const long long total = (long long)u.prefix[deal.world] * kTile * kTile;
     if (total <= 0 || nframes <= 0) return;
-    hipLaunchKernelGGL(k_unpack, dim3((unsigned)((total + kBlock - 1) / kBlock), (unsigned)nframes), dim3(kBlock), 0,
-                       stream, u, reinterpret_cast<float4*>(rgba), width, height, deal, channels, frame0);
+    const unsigned gx = (unsigned)((total + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_unpack, dim3(gx, (unsigned)nframes), dim3(kBlock), 0, stream, u,
+                       reinterpret_cast<float4*>(rgba), width, height, deal, channels, frame0,
+                       stamp_next(kStampUnpack, -1, (long long)gx * nframes, kBlock));
+}
+
+// ------------------------------------------------------------------ distributed overflow flags
+
+__global__ void k_overflow_flag(FlagSrc f, int* out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    int v = 0;
+    for (int j = 0; j < f.K; ++j)
+        for (int b = 0; b < f.n[j]; ++b) v |= f.fc[j][b].overflow;
+    out[0] = v != 0 ? 1 : 0;
+}
+
+void launch_overflow_flag(const FlagSrc& f, int* out, hipStream_t stream) {
+    hipLaunchKernelGGL(k_overflow_flag, dim3(1), dim3(64), 0, stream, f, out);
+}
+
+__global__ void k_peer_flags(UnpackSrc u, int world, size_t floats_per_tile_count, int* flags) {
+    const int r = threadIdx.x;
+    if (r >= 1 && r < world)  // src NULL: a rank not received in this gather
+        flags[r] = u.src[r] ? *reinterpret_cast<const int*>(u.src[r] + floats_per_tile_count * (size_t)u.count[r]) : 0;
+}
+
+void launch_peer_flags(const UnpackSrc& u, int world, size_t floats_per_tile_count, int* flags, hipStream_t stream) {
+    hipLaunchKernelGGL(k_peer_flags, dim3(1), dim3(64), 0, stream, u, world, floats_per_tile_count, flags);
 }
 
 // ------------------------------------------------------------------ progressive accumulation
@@ -417,148 +420,26 @@ void launch_accumulate_frame(const float* frame, float* sum, float* mean, long l
                        reinterpret_cast<float4*>(mean), pixels, count);
 }
 
-// ------------------------------------------------------------------ bounce-level ray binning
-//
-// A level traced as wave packets runs as fast as its slowest wave, and a wave whose 64 rays leave
-// the glass in different directions walks the union of their BVH paths (r2 measurement: skipping
-// waves that spread over > 90 degrees cut a one-frame level-1 launch from 507 to 129 us).  The
-// shade that emits the level's rays writes each ray's direction octant (Queue::key); a STABLE
-// counting sort turns the keys into the order the traversal visits the rays in (perm): bin by
-// bin, and inside a bin in queue order -- which is screen order (the shade appends children in
-// pixel-block order) -- so a wave holds same-octant rays (pairwise <= 90 degrees apart) from
-// neighbouring pixels.  Three passes over chunks of kBlock queue slots: per-chunk bin counts, one
-// block scanning them into per-chunk bin offsets, the scatter.  Deterministic.  (An unstable
-// version that reserved each chunk's range with atomics lost the screen order inside a bin and
-// was slower than no binning, r3b.)
-__device__ __forceinline__ void wave_bin_counts(bool active, unsigned key, unsigned& my_rank, unsigned* wcnt) {
-    my_rank = 0;
-#pragma unroll
-    for (unsigned b = 0; b < (unsigned)kBins; ++b) {
-        const unsigned long long m = __ballot(active && key == b);
-        if (active && key == b) my_rank = (unsigned)lanes_below(m);
-        if (__lane_id() == 0) wcnt[b] = (unsigned)__popcll(m);
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_bin_count(const unsigned char* __restrict__ keys, const FrameCounters* fc,
-                                                      int level, int cap, unsigned* __restrict__ chunk_cnt) {
-    __shared__ unsigned wcnt[kBlock / 64][kBins];
-    const int n = min(fc_count(*fc, level), cap);
-    const int w = threadIdx.x >> 6;
-    for (int c = blockIdx.x; c * kBlock < n; c += gridDim.x) {
-        const int i = c * kBlock + threadIdx.x;
-        const bool active = i < n;
-        unsigned rank;
-        wave_bin_counts(active, active ? keys[i] : 0u, rank, wcnt[w]);
-        __syncthreads();
-        if (threadIdx.x < kBins) {
-            unsigned t = 0;
-            for (int k = 0; k < kBlock / 64; ++k) t += wcnt[k][threadIdx.x];
-            chunk_cnt[(size_t)c * kBins + threadIdx.x] = t;
-        }
-        __syncthreads();
-    }
-}
-
-// one block: per-chunk counts -> per-chunk first slot of each bin (bins in order, chunks in order
-// inside a bin); the bin sizes go to FrameCounters::bins (statistics)
-constexpr int kBinScanBlock = 1024;
-__global__ __launch_bounds__(kBinScanBlock) void k_bin_scan(FrameCounters* fc, int level, int cap,
-                                                            unsigned* __restrict__ chunk_cnt) {
-    __shared__ unsigned part[kBinScanBlock][kBins + 1];  // +1: no bank conflicts on the column walk
-    __shared__ unsigned bin_first[kBins];
-    const int n = min(fc_count(*fc, level), cap);
-    const int nchunks = (n + kBlock - 1) / kBlock;
-    const int per = (nchunks + kBinScanBlock - 1) / kBinScanBlock;  // chunks per thread, contiguous
-    const int c0 = threadIdx.x * per, c1 = min(nchunks, c0 + per);
-    unsigned t[kBins];
-#pragma unroll
-    for (int b = 0; b < kBins; ++b) t[b] = 0;
-    for (int c = c0; c < c1; ++c)
-#pragma unroll
-        for (int b = 0; b < kBins; ++b) t[b] += chunk_cnt[(size_t)c * kBins + b];
-#pragma unroll
-    for (int b = 0; b < kBins; ++b) part[threadIdx.x][b] = t[b];
-    __syncthreads();
-    if (threadIdx.x < kBins) {  // exclusive scan of bin b over the threads (column walk)
-        const int b = threadIdx.x;
-        unsigned acc = 0;
-        for (int k = 0; k < kBinScanBlock; ++k) {
-            const unsigned v = part[k][b];
-            part[k][b] = acc;
-            acc += v;
-        }
-        fc->bins[level][b] = acc;  // bin size
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned acc = 0;
-        for (int b = 0; b < kBins; ++b) {
-            bin_first[b] = acc;
-            acc += fc->bins[level][b];
-        }
-    }
-    __syncthreads();
-    unsigned o[kBins];
-#pragma unroll
-    for (int b = 0; b < kBins; ++b) o[b] = bin_first[b] + part[threadIdx.x][b];
-    for (int c = c0; c < c1; ++c)
-#pragma unroll
-        for (int b = 0; b < kBins; ++b) {
-            const unsigned v = chunk_cnt[(size_t)c * kBins + b];
-            chunk_cnt[(size_t)c * kBins + b] = o[b];  // in place: counts -> first slots
-            o[b] += v;
-        }
-}
-
-__global__ __launch_bounds__(kBlock) void k_bin_scatter(const unsigned char* __restrict__ keys, const FrameCounters* fc,
-                                                        int level, int cap, const unsigned* __restrict__ chunk_first,
-                                                        int* __restrict__ perm) {
-    __shared__ unsigned wcnt[kBlock / 64][kBins];
-    const int n = min(fc_count(*fc, level), cap);
-    const int w = threadIdx.x >> 6;
-    for (int c = blockIdx.x; c * kBlock < n; c += gridDim.x) {
-        const int i = c * kBlock + threadIdx.x;
-        const bool active = i < n;
-        const unsigned key = active ? keys[i] : 0u;
-        unsigned rank;
-        wave_bin_counts(active, key, rank, wcnt[w]);
-        __syncthreads();
-        if (active) {
-            unsigned pos = chunk_first[(size_t)c * kBins + key] + rank;
-            for (int k = 0; k < w; ++k) pos += wcnt[k][key];
-            perm[pos] = i;
-        }
-        __syncthreads();
-    }
-}
-
-void launch_bin_rays(const unsigned char* keys, FrameCounters* fc, int level, int cap, int* perm, unsigned* chunk_buf,
-                     int expect, hipStream_t stream) {
-    if (cap <= 0) return;
-    const int grid = grid_for(cap, expect);
-    hipLaunchKernelGGL(k_bin_count, dim3(grid), dim3(kBlock), 0, stream, keys, fc, level, cap, chunk_buf);
-    hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(kBinScanBlock), 0, stream, fc, level, cap, chunk_buf);
-    hipLaunchKernelGGL(k_bin_scatter, dim3(grid), dim3(kBlock), 0, stream, keys, fc, level, cap, chunk_buf, perm);
-}
-
 // ------------------------------------------------------------------ counter export
 
 // last launch of a slot's frame: the frame counters go to pinned host memory and the device
 // copy is zeroed for the next frame (replaces a D2H copy + a memset: two fewer queue operations
 // per frame)
-__global__ void k_export_counters(uint4* dev, uint4* host, int n16) {
+__global__ void k_export_counters(uint4* dev, uint4* host, int n16, unsigned long long* __restrict__ stamps) {
+    PGRT_STAMP_BEGIN(stamps);
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += gridDim.x * blockDim.x) {
         host[i] = dev[i];
         dev[i] = make_uint4(0u, 0u, 0u, 0u);
     }
+    PGRT_STAMP_END(stamps);
 }
 
 void launch_export_counters(FrameCounters* dev, FrameCounters* host, int n, hipStream_t stream) {
     static_assert(sizeof(FrameCounters) % 16 == 0, "FrameCounters must be a multiple of 16 bytes");
     const int n16 = (int)(sizeof(FrameCounters) / 16) * n;
-    hipLaunchKernelGGL(k_export_counters, dim3((unsigned)std::min(64, (n16 + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                       stream, reinterpret_cast<uint4*>(dev), reinterpret_cast<uint4*>(host), n16);
+    const int grid = std::min(64, (n16 + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_export_counters, dim3((unsigned)grid), dim3(kBlock), 0, stream, reinterpret_cast<uint4*>(dev),
+                       reinterpret_cast<uint4*>(host), n16, stamp_next(kStampExport, -1, grid, kBlock));
 }
 
 // ------------------------------------------------------------------ math self-test

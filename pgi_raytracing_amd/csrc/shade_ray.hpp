@@ -8,6 +8,7 @@
 // wherever the phases run.
 #pragma once
 
+#include "cache_ops.hpp"
 #include "shade_ops.hpp"
 #include "trace.hpp"
 
@@ -219,9 +220,8 @@ struct ShadeAllocPending {
     unsigned long long mrefl, mrefr;
     unsigned long long base;  // thread 0: the atomic's result
 };
-// child_ctr / shadow_ctr: where the block's children (low word) and shadow rays (high word) are
-// counted -- both fc->alloc[level] (one packed atomic) unless the persistent tail counts every
-// tail level's shadow rays on its first level's word (tail.hip).
+// The block's children (low word) and shadow rays (high word) are counted on fc->alloc[level]
+// (one packed atomic).
 // refr_acc: thread 0's running count of refraction children (statistics, fc->refract), flushed by
 // the caller once per launch (shade_refract_flush); nullptr: one atomic per block and iteration.
 // (A same-address atomic per WAVE, as before r3, serialised ~27k atomics on one word for an
@@ -229,8 +229,6 @@ struct ShadeAllocPending {
 template <int BLOCK>
 __device__ __forceinline__ ShadeAllocPending shade_alloc_begin(ShadeAllocLds<BLOCK>& lds, int it_par, FrameCounters* fc,
                                                                int level, int sbits, const ShadeOut& r,
-                                                               unsigned long long* child_ctr = nullptr,
-                                                               unsigned long long* shadow_ctr = nullptr,
                                                                int* refr_acc = nullptr) {
     ShadeAllocPending pa;
     int cpre, ctot, stot;
@@ -258,15 +256,7 @@ __device__ __forceinline__ ShadeAllocPending shade_alloc_begin(ShadeAllocLds<BLO
         }
         if (refr_acc) *refr_acc += brefr;
         else if (brefr && level + 1 < kMaxLevels) atomicAdd(&fc->refract[level + 1], brefr);  // statistics
-        if (!child_ctr || child_ctr == shadow_ctr) {
-            unsigned long long* ctr = child_ctr ? child_ctr : &fc->alloc[level];
-            pa.base = btot ? atomicAdd(ctr, btot) : 0ull;
-        } else {  // separate words: children on the low word of one, shadow rays on the high word of the other
-            const unsigned long long ct = btot & 0xffffffffull, st = btot & ~0xffffffffull;
-            const unsigned long long cb = ct ? atomicAdd(child_ctr, ct) : 0ull;
-            const unsigned long long sb = st ? atomicAdd(shadow_ctr, st) : 0ull;
-            pa.base = (sb & ~0xffffffffull) | (cb & 0xffffffffull);
-        }
+        pa.base = btot ? atomicAdd(&fc->alloc[level], btot) : 0ull;
     }
     return pa;
 }
@@ -302,7 +292,7 @@ template <int BLOCK>
 __device__ __forceinline__ ShadeSlots shade_alloc(ShadeAllocLds<BLOCK>& lds, int& it_par, FrameCounters* fc, int level,
                                                   int sq_base, int sbits, const ShadeOut& r, int* refr_acc = nullptr) {
     return shade_alloc_end(lds, it_par, sq_base,
-                           shade_alloc_begin(lds, it_par, fc, level, sbits, r, nullptr, nullptr, refr_acc));
+                           shade_alloc_begin(lds, it_par, fc, level, sbits, r, refr_acc));
 }
 // thread 0 at the end of a launch: its block's refraction children into fc->refract[level + 1]
 __device__ __forceinline__ void shade_refract_flush(FrameCounters* fc, int level, int refr_acc) {
@@ -343,16 +333,14 @@ __device__ __forceinline__ int4 emit_children(int level, const ShadeOut& r, cons
         atomicOr(&fc->overflow, 1);
         return link;
     }
-    next.ro[sl.refl] = child_org(r);
-    next.rd[sl.refl] = child_dir(r.refl_dir);
-    next.time[sl.refl] = r.n1;
-    if (next.key) next.key[sl.refl] = (unsigned char)dir_octant(r.refl_dir.x, r.refl_dir.y, r.refl_dir.z);
+    st_stream(next.ro + sl.refl, child_org(r));
+    st_stream(next.rd + sl.refl, child_dir(r.refl_dir));
+    st_stream_nt(next.time + sl.refl, r.n1);
     link.x = sl.refl;
     if (r.nchild == 2) {
-        next.ro[sl.refr] = child_org(r);
-        next.rd[sl.refr] = child_dir(r.refr_dir);
-        next.time[sl.refr] = r.n2;
-        if (next.key) next.key[sl.refr] = (unsigned char)dir_octant(r.refr_dir.x, r.refr_dir.y, r.refr_dir.z);
+        st_stream(next.ro + sl.refr, child_org(r));
+        st_stream(next.rd + sl.refr, child_dir(r.refr_dir));
+        st_stream_nt(next.time + sl.refr, r.n2);
         link.y = sl.refr;
     }
     return link;
@@ -366,7 +354,7 @@ __device__ __forceinline__ void emit_node(const SceneView& s, const DevMaterial*
                                           FrameCounters* fc, bool use_pre0 = false,
                                           float4 pre0 = make_float4(0, 0, 0, 0)) {
     if (r.kind == 1) {
-        nodes.att[i] = r.att;
+        st_stream(nodes.att + i, r.att);
     } else if (r.kind == 2 && r.nshadow > 0) {
         if (sl.shadow + r.nshadow > sq.cap) {
             atomicOr(&fc->overflow, 1);
@@ -379,18 +367,19 @@ __device__ __forceinline__ void emit_node(const SceneView& s, const DevMaterial*
                 const V3 lp = v3(L.pos[0], L.pos[1], L.pos[2]);
                 if (dot(nrm, lp) < 0) continue;  // is_illuminated's N.L test (raytracer.cpp:155)
                 // LightSource::GenerateRay(hit): org = light, dir = hit position vector
-                if (sq.ro) sq.ro[k] = make_float4(lp.x, lp.y, lp.z, 0.01f);
-                sq.rd[k] = make_float4(hitp.x, hitp.y, hitp.z, length(v3(lp.x - hitp.x, lp.y - hitp.y, lp.z - hitp.z)));
+                if (sq.ro) st_stream(sq.ro + k, make_float4(lp.x, lp.y, lp.z, 0.01f));
+                st_stream(sq.rd + k,
+                          make_float4(hitp.x, hitp.y, hitp.z, length(v3(lp.x - hitp.x, lp.y - hitp.y, lp.z - hitp.z))));
                 // Phong term for this light (raytracer.cpp:355-382)
-                sq.contrib[k] = (use_pre0 && li == 0) ? pre0 : phong_term(m, L, r);
+                st_stream(sq.contrib + k, (use_pre0 && li == 0) ? pre0 : phong_term(m, L, r));
                 ++k;
             }
             link.z = sl.shadow;
             link.w = r.nshadow;
         }
     }
-    nodes.link[i] = link;
-    if (link.x < 0 && link.z < 0) nodes.color[i] = r.color;  // else derived by k_finish
+    st_stream(nodes.link + i, link);
+    if (link.x < 0 && link.z < 0) st_stream(nodes.color + i, r.color);  // else derived by k_finish
 }
 
 // Phase 3 for an active ray i.

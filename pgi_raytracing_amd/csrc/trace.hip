@@ -23,6 +23,8 @@
 #include "trace.hpp"
 #include "traverse.hpp"
 #include "camera_ops.hpp"
+#include "stamps.hpp"
+#include "cache_ops.hpp"
 
 namespace pgrt {
 
@@ -51,9 +53,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
                                                        float4* __restrict__ hits,
                                                        const int* __restrict__ count_dev, int count_terms,
                                                        int count_host, int cap, int* __restrict__ gstack,
-                                                       unsigned long long* __restrict__ counters, int rpw,
-                                                       float4 const_org, unsigned char* __restrict__ lit,
-                                                       const int* __restrict__ perm) {
+                                                       unsigned long long* __restrict__ counters,
+                                                       float4 const_org, unsigned char* __restrict__ lit) {
+    PGRT_STAMP_BEGIN(s.stamps);
     extern __shared__ int lstack[];  // [entries][kTraceBlock]
     const int tid = threadIdx.x;
     const int lane = __lane_id();
@@ -78,18 +80,16 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
         --spr;
         return v;
     };
-    // rpw rays per wave (lanes >= rpw idle): small queues spread over more waves
-    if (lane >= rpw) return;
-    const int wstride = gridDim.x * (kTraceBlock / 64) * rpw;
-    int stride_i = ((blockIdx.x * kTraceBlock + tid) >> 6) * rpw + lane - wstride;
+    const int wstride = gridDim.x * kTraceBlock;
+    int stride_i = ((blockIdx.x * kTraceBlock + tid) >> 6) * 64 + lane - wstride;
     unsigned long long witer = 0, nspill = 0, mclk = 0, mray[6] = {0, 0, 0, 0, 0, 0};
     int msp = 0;
     for (;;) {
         stride_i += wstride;
         if (stride_i >= n) break;
-        const int i = perm ? perm[stride_i] : stride_i;  // binned level: the ray of this slot
-        const float4 o4 = ro ? ro[i] : const_org;
-        const float4 d4 = rd[i];
+        const int i = stride_i;
+        const float4 o4 = ro ? ld_stream(ro + i) : const_org;
+        const float4 d4 = ld_stream(rd + i);
         const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
         const float dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
         const float sdx = fabsf(dx) < 1e-30f ? copysignf(1e-30f, dx) : dx;
@@ -200,9 +200,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
             if (COUNT) rcyc_leaf += (unsigned long long)(clock64() - tl0);
         }
         if (lit)  // is_illuminated (raytracer.cpp:163-173): no hit, or the occluder is dielectric
-            lit[i] = (best_prim < 0 || s.prim_glass[best_prim] != 0) ? 1 : 0;
+            st_stream_nt(lit + i, (unsigned char)((best_prim < 0 || s.prim_glass[best_prim] != 0) ? 1 : 0));
         else
-            hits[i] = make_float4(best_t, best_u, best_v, __int_as_float(best_prim));
+            st_stream(hits + i, make_float4(best_t, best_u, best_v, __int_as_float(best_prim)));
         if (COUNT) {
             const unsigned long long dt = (unsigned long long)(wall_clock64() - t_start);
             if (dt > mclk) {  // the longest ray's profile
@@ -238,251 +238,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
         // cycles / 64, leaf-phase cycles / 64 (max picks the longest ray's record)
         for (int k = 0; k < 6; ++k) atomicMax(&counters[8 + k], mray[k]);
     }
-}
-
-// ---------------------------------------------------------------- one lane per ray, lane refill
-//
-// k_trace's waves trace 64 rays in lockstep: a lane whose ray ends early idles until the wave's
-// longest ray is done, so an incoherent queue (bounce levels, shadow rays) keeps a fraction of
-// its lanes busy.  Here a wave owns a fixed sequence of queue slots (row r, column c: slot
-// r * 64 * waves + 64 * wave + c) and walks it with a wave-uniform cursor: once at least
-// `min_idle` lanes have finished their rays, they take the next slots in one step (ballot +
-// mbcnt, no atomics), so the lanes stay busy until the wave's sequence runs out (Aila & Laine
-// 2009, "replacing terminated rays").  Per-ray arithmetic and visit order are k_trace's (same
-// node loop, LDS stack, postponed leaves), so the hit records are identical.
-__global__ __launch_bounds__(kTraceBlock) void k_trace_rf(SceneView s, const float4* __restrict__ ro,
-                                                          const float4* __restrict__ rd,
-                                                          float4* __restrict__ hits,
-                                                          const int* __restrict__ count_dev, int count_terms,
-                                                          int count_host, int cap, float4 const_org,
-                                                          unsigned char* __restrict__ lit,
-                                                          const int* __restrict__ perm, int min_idle) {
-    extern __shared__ int lstack[];  // [depth + 2][kTraceBlock]
-    const int tid = threadIdx.x;
-    const int n = ray_count(count_dev, count_terms, count_host, cap);
-    const int wave = (blockIdx.x * kTraceBlock + tid) >> 6;
-    const unsigned wstride = gridDim.x * kTraceBlock;  // 64 x waves
-    unsigned next = 0;                                 // the wave's next sequence position (uniform)
-    auto slot_of = [&](unsigned q) -> unsigned { return (q >> 6) * wstride + (unsigned)wave * 64u + (q & 63u); };
-    bool exhausted = slot_of(0) >= (unsigned)n;
-    int i = -1;  // the lane's ray (queue index), -1 = idle
-    float ox = 0, oy = 0, oz = 0, tnear = 0, dx = 0, dy = 0, dz = 0, tfar = 0;
-    float idx = 0, idy = 0, idz = 0, oix = 0, oiy = 0, oiz = 0;
-    float best_t = 0, best_u = 0, best_v = 0;
-    int best_prim = -1, sp = 0, node = kSentinel, leaf = 0;
-    for (;;) {
-        // ---- refill: idle lanes take the wave's next slots ----
-        const unsigned long long im = __ballot(i < 0);
-        const int nidle = __popcll(im);
-        if (!exhausted && (nidle >= min_idle || nidle == 64)) {
-            if (i < 0) {
-                const unsigned q = next + __builtin_amdgcn_mbcnt_hi((unsigned)(im >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((unsigned)im, 0u));
-                const unsigned sl = slot_of(q);
-                if (sl < (unsigned)n) {
-                    i = perm ? perm[sl] : (int)sl;
-                    const float4 o4 = ro ? ro[i] : const_org;
-                    const float4 d4 = rd[i];
-                    ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
-                    dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
-                    const float sdx = fabsf(dx) < 1e-30f ? copysignf(1e-30f, dx) : dx;
-                    const float sdy = fabsf(dy) < 1e-30f ? copysignf(1e-30f, dy) : dy;
-                    const float sdz = fabsf(dz) < 1e-30f ? copysignf(1e-30f, dz) : dz;
-                    idx = __builtin_amdgcn_rcpf(sdx), idy = __builtin_amdgcn_rcpf(sdy), idz = __builtin_amdgcn_rcpf(sdz);
-                    oix = ox * idx, oiy = oy * idy, oiz = oz * idz;
-                    best_t = tfar, best_u = 0.0f, best_v = 0.0f;
-                    best_prim = -1;
-                    sp = 0;
-                    lstack[tid] = kSentinel;  // stack[0]
-                    node = s.root;
-                    leaf = 0;
-                    if (node < 0) {
-                        leaf = node;
-                        node = kSentinel;
-                    }
-                    if (!(tfar >= 0.0f)) {  // padding slots / empty segments: no traversal
-                        node = kSentinel;
-                        leaf = 0;
-                    }
-                }
-            }
-            next += (unsigned)nidle;
-            exhausted = slot_of(next) >= (unsigned)n;
-        }
-        if (!__any(i >= 0)) break;  // no ray left in the wave, and the sequence is exhausted
-        // ---- descend internal nodes until every active lane has parked a leaf ----
-        const float bt = __builtin_canonicalizef(best_t);
-        while ((unsigned)node < (unsigned)kSentinel) {
-            const int top = lstack[sp * kTraceBlock + tid];
-            const BvhNode* nd = s.nodes + node;
-            const float4 a = nd->a, b = nd->b, c = nd->c;
-            const int4 d = nd->d;
-            float t0, t1;
-            const bool h0 = box_hit(a.x, a.y, a.z, a.w, c.x, c.y, idx, idy, idz, oix, oiy, oiz, bt, t0);
-            const bool h1 = box_hit(b.x, b.y, b.z, b.w, c.z, c.w, idx, idy, idz, oix, oiy, oiz, bt, t1);
-            const bool any = h0 || h1;
-            const bool first0 = h0 && (!h1 || t0 <= t1);
-            const bool both = h0 && h1;
-            lstack[(sp + 1) * kTraceBlock + tid] = first0 ? d.y : d.x;
-            node = any ? (first0 ? d.x : d.y) : top;
-            sp += both ? 1 : (any ? 0 : -1);
-            if (node < 0 && leaf == 0) {  // first leaf: park it and keep descending
-                leaf = node;
-                node = lstack[sp * kTraceBlock + tid];
-                --sp;
-            }
-            if (!__any(leaf == 0)) break;
-        }
-        // ---- triangle tests for the parked leaves ----
-        while (leaf < 0) {
-            const int first = leaf_first(leaf), end = first + leaf_count(leaf);
-            float4 p0 = s.tri[3 * first], p1 = s.tri[3 * first + 1], p2 = s.tri[3 * first + 2];
-            for (int k = first; k < end; ++k) {
-                const float4 q0 = p0, q1 = p1, q2 = p2;
-                if (k + 1 < end) {
-                    p0 = s.tri[3 * k + 3];
-                    p1 = s.tri[3 * k + 4];
-                    p2 = s.tri[3 * k + 5];
-                }
-                tri_test(q0, q1, q2, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v, best_prim);
-            }
-            leaf = 0;
-            if (node < 0) {  // the node popped after parking is a leaf too: test it now
-                leaf = node;
-                node = lstack[sp * kTraceBlock + tid];
-                --sp;
-            }
-        }
-        // ---- finished rays: write the record, the lane goes idle ----
-        if (i >= 0 && node == kSentinel) {
-            if (lit)  // is_illuminated (raytracer.cpp:163-173): no hit, or the occluder is dielectric
-                lit[i] = (best_prim < 0 || s.prim_glass[best_prim] != 0) ? 1 : 0;
-            else
-                hits[i] = make_float4(best_t, best_u, best_v, __int_as_float(best_prim));
-            i = -1;
-        }
-    }
-}
-
-// ---------------------------------------------------------------- one lane per ray, child prefetch
-//
-// Small queues (the deep Whitted levels) take as long as their slowest ray, whose node loop is a
-// chain of dependent steps: fetch the node, test its two child boxes, pick the next node, fetch
-// it.  Here a step issues the fetches of both children of the current node before testing their
-// boxes, so when the walk descends the next node's data is already on its way and the box tests
-// hide most of the fetch latency; only a pop from the stack fetches with the latency exposed.
-// Twice the node bytes per step: meant for latency-bound launches, not wide ones.  Same visit
-// order, arithmetic and results as k_trace.
-__device__ __forceinline__ void load_node(const BvhNode* nodes, int i, float4& a, float4& b, float4& c, int4& d) {
-    const BvhNode* nd = nodes + i;
-    a = nd->a;
-    b = nd->b;
-    c = nd->c;
-    d = nd->d;
-}
-
-__global__ __launch_bounds__(kTraceBlock) void k_trace_pf(SceneView s, const float4* __restrict__ ro,
-                                                          const float4* __restrict__ rd,
-                                                          float4* __restrict__ hits,
-                                                          const int* __restrict__ count_dev, int count_terms,
-                                                          int count_host, int cap, float4 const_org,
-                                                          unsigned char* __restrict__ lit,
-                                                          const int* __restrict__ perm) {
-    extern __shared__ int lstack[];  // [depth + 2][kTraceBlock]
-    const int tid = threadIdx.x;
-    const int n = ray_count(count_dev, count_terms, count_host, cap);
-    for (int slot = blockIdx.x * kTraceBlock + tid; slot < n; slot += gridDim.x * kTraceBlock) {
-        const int i = perm ? perm[slot] : slot;
-        const float4 o4 = ro ? ro[i] : const_org;
-        const float4 d4 = rd[i];
-        const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
-        const float dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
-        const float sdx = fabsf(dx) < 1e-30f ? copysignf(1e-30f, dx) : dx;
-        const float sdy = fabsf(dy) < 1e-30f ? copysignf(1e-30f, dy) : dy;
-        const float sdz = fabsf(dz) < 1e-30f ? copysignf(1e-30f, dz) : dz;
-        const float idx = __builtin_amdgcn_rcpf(sdx), idy = __builtin_amdgcn_rcpf(sdy),
-                    idz = __builtin_amdgcn_rcpf(sdz);
-        const float oix = ox * idx, oiy = oy * idy, oiz = oz * idz;
-        float best_t = tfar, best_u = 0.0f, best_v = 0.0f;
-        int best_prim = -1;
-        int sp = 0;
-        lstack[tid] = kSentinel;  // stack[0]
-        int node = s.root;
-        int leaf = 0;
-        if (node < 0) {
-            leaf = node;
-            node = kSentinel;
-        }
-        if (!(tfar >= 0.0f)) {
-            node = kSentinel;
-            leaf = 0;
-        }
-        // the current node's data (valid whenever node is internal)
-        float4 na = make_float4(0, 0, 0, 0), nb = na, nc = na;
-        int4 ndd = make_int4(0, 0, 0, 0);
-        if ((unsigned)node < (unsigned)kSentinel) load_node(s.nodes, node, na, nb, nc, ndd);
-        while (node != kSentinel || leaf < 0) {
-            const float bt = __builtin_canonicalizef(best_t);
-            while ((unsigned)node < (unsigned)kSentinel) {
-                const int top = lstack[sp * kTraceBlock + tid];
-                // both children's fetches first (a leaf child: the current node again, a cached line)
-                const int k0 = ndd.x >= 0 ? ndd.x : node, k1 = ndd.y >= 0 ? ndd.y : node;
-                float4 a0, b0, c0, a1, b1, c1;
-                int4 d0, d1;
-                load_node(s.nodes, k0, a0, b0, c0, d0);
-                load_node(s.nodes, k1, a1, b1, c1, d1);
-                float t0, t1;
-                const bool h0 = box_hit(na.x, na.y, na.z, na.w, nc.x, nc.y, idx, idy, idz, oix, oiy, oiz, bt, t0);
-                const bool h1 = box_hit(nb.x, nb.y, nb.z, nb.w, nc.z, nc.w, idx, idy, idz, oix, oiy, oiz, bt, t1);
-                const bool any = h0 || h1;
-                const bool first0 = h0 && (!h1 || t0 <= t1);
-                const bool both = h0 && h1;
-                lstack[(sp + 1) * kTraceBlock + tid] = first0 ? ndd.y : ndd.x;
-                const int nxt = any ? (first0 ? ndd.x : ndd.y) : top;
-                sp += both ? 1 : (any ? 0 : -1);
-                // the prefetched child, selected unconditionally (a load used only inside a branch
-                // could be sunk into it, which would undo the prefetch)
-                na = first0 ? a0 : a1;
-                nb = first0 ? b0 : b1;
-                nc = first0 ? c0 : c1;
-                ndd = first0 ? d0 : d1;
-                node = nxt;
-                bool fetch = !any;  // popped: fetch now, latency exposed
-                if (node < 0 && leaf == 0) {  // first leaf: park it and keep descending
-                    leaf = node;
-                    node = lstack[sp * kTraceBlock + tid];
-                    --sp;
-                    fetch = true;
-                }
-                if (fetch && (unsigned)node < (unsigned)kSentinel) load_node(s.nodes, node, na, nb, nc, ndd);
-                if (!__any(leaf == 0)) break;
-            }
-            while (leaf < 0) {
-                const int first = leaf_first(leaf), end = first + leaf_count(leaf);
-                float4 p0 = s.tri[3 * first], p1 = s.tri[3 * first + 1], p2 = s.tri[3 * first + 2];
-                for (int k = first; k < end; ++k) {
-                    const float4 q0 = p0, q1 = p1, q2 = p2;
-                    if (k + 1 < end) {
-                        p0 = s.tri[3 * k + 3];
-                        p1 = s.tri[3 * k + 4];
-                        p2 = s.tri[3 * k + 5];
-                    }
-                    tri_test(q0, q1, q2, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v, best_prim);
-                }
-                leaf = 0;
-                if (node < 0) {  // the node popped after parking is a leaf too: test it now
-                    leaf = node;
-                    node = lstack[sp * kTraceBlock + tid];
-                    --sp;
-                    if ((unsigned)node < (unsigned)kSentinel) load_node(s.nodes, node, na, nb, nc, ndd);
-                }
-            }
-        }
-        if (lit)
-            lit[i] = (best_prim < 0 || s.prim_glass[best_prim] != 0) ? 1 : 0;
-        else
-            hits[i] = make_float4(best_t, best_u, best_v, __int_as_float(best_prim));
-    }
+    PGRT_STAMP_END(s.stamps);
 }
 
 // ---------------------------------------------------------------- 8-wide traversal
@@ -494,7 +250,6 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pf(SceneView s, const flo
 // right away; its internal hits become the current group.
 constexpr int kLdsStack8 = 8;  // 8-B groups: 8 x 8 B x 256 lanes = 16 KB per block
 
-__device__ __forceinline__ float qb(unsigned w, int j) { return (float)((w >> (8 * j)) & 0xffu); }
 
 template <bool COUNT>
 __global__ __launch_bounds__(kTraceBlock) void k_trace8(SceneView s, const float4* __restrict__ ro,
@@ -502,14 +257,15 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8(SceneView s, const float
                                                         const int* __restrict__ count_dev, int count_terms,
                                                         int count_host, int cap, int* __restrict__ gstack,
                                                         unsigned long long* __restrict__ counters) {
+    PGRT_STAMP_BEGIN(s.stamps);
     __shared__ uint2 lstack[kLdsStack8 * kTraceBlock];
     const int tid = threadIdx.x;
     const int n = ray_count(count_dev, count_terms, count_host, cap);
     uint2* gst = reinterpret_cast<uint2*>(gstack + (size_t)(blockIdx.x * kTraceBlock + tid) * kGlobalStack);
     unsigned long long nvis = 0, ntest = 0, mvis = 0, mtest = 0;
     for (int i = blockIdx.x * kTraceBlock + tid; i < n; i += gridDim.x * kTraceBlock) {
-            const float4 o4 = ro[i];
-        const float4 d4 = rd[i];
+        const float4 o4 = ld_stream(ro + i);
+        const float4 d4 = ld_stream(rd + i);
         const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
         const float dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
         const float sdx = fabsf(dx) < 1e-30f ? copysignf(1e-30f, dx) : dx;
@@ -606,7 +362,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8(SceneView s, const float
                 if (!more) break;
             }
         }
-        hits[i] = make_float4(best_t, best_u, best_v, __int_as_float(best_prim));
+        st_stream(hits + i, make_float4(best_t, best_u, best_v, __int_as_float(best_prim)));
         if (COUNT) {
             nvis += rvis;
             ntest += rtest;
@@ -620,95 +376,13 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8(SceneView s, const float
         atomicMax(&counters[2], mvis);
         atomicMax(&counters[3], mtest);
     }
+    PGRT_STAMP_END(s.stamps);
 }
 
 
 // ---------------------------------------------------------------- 8 lanes per ray, 8-wide BVH
 //
-// For small queues (the deep Whitted levels: tens of thousands of rays on 1024 SIMDs) a level
-// takes as long as its slowest ray, and a one-lane traversal of that ray is a chain of ~100
-// dependent node fetches.  Here 8 lanes trace one ray: every lane tests one child box of the
-// current 8-wide node (lane k takes slot k ^ octant, so the group's ballot byte is already in
-// near-to-far order), and the triangles of the node's hit leaves are tested 8 at a time.  The
-// chain shrinks to one fetch per 8-wide node (about a third of the binary depth) plus one per
-// leaf batch.  All 8 lanes hold identical traversal state (ballot / DPP reductions), so the
-// group's control flow is uniform; the node-group stack lives in LDS, one per group.
-constexpr int kGroupStack = 32;  // node groups per ray: >= 8-wide depth + 1
-
-// reduce over the 8 lanes of a group: xor 1, xor 2 (quad DPP), then lane i <-> 7 - i (row
-// half mirror), so every lane ends with the group value
-#ifdef PGRT_GROUP_SHFL  // debugging aid: the same reductions through ds_bpermute
-template <int CTRL>
-__device__ __forceinline__ int dpp_i(int v) {
-    return __shfl_xor(v, CTRL == 0xB1 ? 1 : (CTRL == 0x4E ? 2 : 7), 64);
-}
-#else
-template <int CTRL>
-__device__ __forceinline__ int dpp_i(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
-}
-#endif
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v) {
-    return __int_as_float(dpp_i<CTRL>(__float_as_int(v)));
-}
-constexpr int kDppXor1 = 0xB1;        // quad_perm [1,0,3,2]
-constexpr int kDppXor2 = 0x4E;        // quad_perm [2,3,0,1]
-constexpr int kDppHalfMirror = 0x141;  // row_half_mirror
-
-template <int CTRL>
-__device__ __forceinline__ void merge_hit_step(float& t, float& u, float& v, int& prim) {
-    const float ot = dpp_f<CTRL>(t), ou = dpp_f<CTRL>(u), ov = dpp_f<CTRL>(v);
-    const int op = dpp_i<CTRL>(prim);
-    if (op >= 0 && (prim < 0 || ot < t || (ot == t && op < prim))) {
-        t = ot;
-        u = ou;
-        v = ov;
-        prim = op;
-    }
-}
-
-// group reductions: G = 8 uses xor 1, xor 2 and the half-row mirror; G = 4 the two quad steps
-template <int G>
-__device__ __forceinline__ int group_or(int v) {
-    v |= dpp_i<kDppXor1>(v);
-    v |= dpp_i<kDppXor2>(v);
-    if constexpr (G == 8) v |= dpp_i<kDppHalfMirror>(v);
-    return v;
-}
-template <int G>
-__device__ __forceinline__ void group_merge_hit(float& t, float& u, float& v, int& prim) {
-    merge_hit_step<kDppXor1>(t, u, v, prim);
-    merge_hit_step<kDppXor2>(t, u, v, prim);
-    if constexpr (G == 8) merge_hit_step<kDppHalfMirror>(t, u, v, prim);
-}
-
-// one child slot of a wide node against the ray (conservative quantized slab test)
-struct SlotTest {
-    bool hit, inner;
-    unsigned meta;
-};
-__device__ __forceinline__ SlotTest test_slot(unsigned slot, const uint4& m, const uint4& qx, const uint4& qy,
-                                              const uint4& qz, unsigned imask, float ax, float ay, float az,
-                                              float bx, float by, float bz, bool px, bool py, bool pz,
-                                              float best_t) {
-    const int j = (int)(slot & 3u);
-    const bool hi_half = slot >= 4u;
-    const unsigned lxw = hi_half ? qx.y : qx.x, hxw = hi_half ? qx.w : qx.z;
-    const unsigned lyw = hi_half ? qy.y : qy.x, hyw = hi_half ? qy.w : qy.z;
-    const unsigned lzw = hi_half ? qz.y : qz.x, hzw = hi_half ? qz.w : qz.z;
-    const float lx = qb(lxw, j), hx = qb(hxw, j), ly = qb(lyw, j), hy = qb(hyw, j);
-    const float lz = qb(lzw, j), hz = qb(hzw, j);
-    const float t0 = fmaxf(fmaxf(fmaf(px ? lx : hx, ax, bx), fmaf(py ? ly : hy, ay, by)),
-                           fmaxf(fmaf(pz ? lz : hz, az, bz), 0.0f));
-    const float t1 = fminf(fminf(fmaf(px ? hx : lx, ax, bx), fmaf(py ? hy : ly, ay, by)),
-                           fminf(fmaf(pz ? hz : lz, az, bz), best_t));
-    SlotTest r;
-    r.meta = ((hi_half ? m.w : m.z) >> (8 * j)) & 0xffu;
-    r.hit = r.meta != 0u && t0 <= t1 * 1.000001f;
-    r.inner = ((imask >> slot) & 1u) != 0u;
-    return r;
-}
+// (the group traversal itself is trace8_group, traverse.hpp)
 
 // RESUME: the rays are a budgeted packet launch's deferred rays (perm = the defer list): each
 // starts from the closest hit the packet found so far (hits[i]), which bounds its traversal
@@ -720,6 +394,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8g(SceneView s, const floa
                                                          unsigned long long* __restrict__ counters,
                                                          const int* __restrict__ perm) {
     static_assert(G == 4 || G == 8, "lanes per ray");
+    PGRT_STAMP_BEGIN(s.stamps);
     constexpr int kGroups = kTraceBlock / G;
     __shared__ uint2 gstk[kGroupStack][kGroups];
     const int tid = threadIdx.x;
@@ -729,93 +404,22 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8g(SceneView s, const floa
     const int n = ray_count(count_dev, count_terms, count_host, cap);
     unsigned long long nvis = 0, ntest = 0, mvis = 0, mtest = 0;
     for (int slot_i = blockIdx.x * kGroups + gib; slot_i < n; slot_i += gridDim.x * kGroups) {
-        const int i = perm ? perm[slot_i] : slot_i;  // binned level: the ray of this slot
-        const float4 o4 = ro[i];
-        const float4 d4 = rd[i];
-        const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
-        const float dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
-        const float sdx = fabsf(dx) < 1e-30f ? copysignf(1e-30f, dx) : dx;
-        const float sdy = fabsf(dy) < 1e-30f ? copysignf(1e-30f, dy) : dy;
-        const float sdz = fabsf(dz) < 1e-30f ? copysignf(1e-30f, dz) : dz;
-        const float idx = __builtin_amdgcn_rcpf(sdx), idy = __builtin_amdgcn_rcpf(sdy),
-                    idz = __builtin_amdgcn_rcpf(sdz);
-        const bool px = idx >= 0.0f, py = idy >= 0.0f, pz = idz >= 0.0f;
-        const unsigned oct = (dx > 0.0f ? 1u : 0u) | (dy > 0.0f ? 2u : 0u) | (dz > 0.0f ? 4u : 0u);
-        float best_t = tfar, best_u = 0.0f, best_v = 0.0f;
+        const int i = perm ? ld_stream_nt(perm + slot_i) : slot_i;  // RESUME: the deferred ray of this slot
+        const float4 o4 = ld_stream(ro + i);
+        const float4 d4 = ld_stream(rd + i);
+        float best_t = d4.w, best_u = 0.0f, best_v = 0.0f;
         int best_prim = -1;
         if constexpr (RESUME) {  // the packet's closest hit so far (its t is <= tfar)
-            const float4 h = hits[i];
+            const float4 h = ld_stream(hits + i);
             best_t = h.x;
             best_u = h.y;
             best_v = h.z;
             best_prim = __float_as_int(h.w);
         }
         unsigned rvis = 0, rtest = 0;
-        int sp = 0;
-        unsigned gbase = 0, gbits = (1u << (24 + oct)) | 1u;  // the root: slot 0 of a virtual parent
-        if (!(tfar >= 0.0f)) gbits = 0;
-        unsigned tbase = 0, tbits = 0;
-        for (;;) {
-            while (tbits == 0u) {  // ---- node phase (group-uniform) ----
-                if (gbits <= 0x00ffffffu) {
-                    if (sp == 0) break;
-                    --sp;
-                    const uint2 g = gstk[sp][gib];
-                    gbase = g.x;
-                    gbits = g.y;
-                }
-                const int pb = 31 - __clz((int)gbits);
-                gbits &= ~(1u << pb);
-                const unsigned slot = (unsigned)(pb - 24) ^ oct;
-                const int child = (int)gbase + __popc(gbits & 0xffu & ((1u << slot) - 1u));
-                if (gbits > 0x00ffffffu) {
-                    gstk[sp][gib] = make_uint2(gbase, gbits);  // same value from all lanes of the group
-                    ++sp;
-                }
-                const Bvh8Node* nd = s.nodes8 + child;
-                const float4 p = nd->p;
-                const uint4 m = nd->m, qx = nd->qx, qy = nd->qy, qz = nd->qz;
-                if (COUNT) ++rvis;
-                const unsigned eb = __float_as_uint(p.w);
-                const unsigned imask = eb >> 24;
-                const float ax = __uint_as_float((eb & 0xffu) << 23) * idx;
-                const float ay = __uint_as_float(((eb >> 8) & 0xffu) << 23) * idy;
-                const float az = __uint_as_float(((eb >> 16) & 0xffu) << 23) * idz;
-                const float bx = (p.x - ox) * idx, by = (p.y - oy) * idy, bz = (p.z - oz) * idz;
-                // lane k tests the slot at near-to-far position k (slot k ^ oct) and, for G = 4,
-                // also position k + 4; the ballots then give the group's near-to-far hit byte
-                const SlotTest s0 = test_slot((unsigned)k ^ oct, m, qx, qy, qz, imask, ax, ay, az, bx, by, bz, px,
-                                              py, pz, best_t);
-                int tb = (s0.hit && !s0.inner) ? (int)wide_leaf_bits(s0.meta) : 0;
-                unsigned nb = (unsigned)(__ballot(s0.hit && s0.inner) >> gshift) & ((1u << G) - 1u);
-                if constexpr (G == 4) {
-                    const SlotTest s1 = test_slot((unsigned)(k + 4) ^ oct, m, qx, qy, qz, imask, ax, ay, az, bx, by,
-                                                  bz, px, py, pz, best_t);
-                    if (s1.hit && !s1.inner) tb |= (int)wide_leaf_bits(s1.meta);
-                    nb |= ((unsigned)(__ballot(s1.hit && s1.inner) >> gshift) & 0xfu) << 4;
-                }
-                tb = group_or<G>(tb);
-                gbase = m.x;
-                gbits = (nb << 24) | imask;
-                tbase = m.y;
-                tbits = (unsigned)tb;
-            }
-            if (tbits == 0u) break;
-            // ---- triangle phase: G triangles per round, then the group's closest hit ----
-            while (tbits != 0u) {
-                unsigned mine = tbits;
-                for (int q = 0; q < k; ++q) mine &= mine - 1u;  // this lane's set bit
-                if (mine != 0u) {
-                    const int tr = (int)tbase + __ffs((int)mine) - 1;
-                    const float4 q0 = s.tri8[3 * tr], q1 = s.tri8[3 * tr + 1], q2 = s.tri8[3 * tr + 2];
-                    tri_test(q0, q1, q2, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v, best_prim);
-                }
-                if (COUNT) rtest += (unsigned)min(__popc(tbits), G);
-                for (int q = 0; q < G; ++q) tbits &= tbits - 1u;
-                group_merge_hit<G>(best_t, best_u, best_v, best_prim);
-            }
-        }
-        if (k == 0) hits[i] = make_float4(best_t, best_u, best_v, __int_as_float(best_prim));
+        trace8_group<G, COUNT>(s, o4, d4, k, gshift, &gstk[0][gib], kGroups, best_t, best_u, best_v, best_prim, rvis,
+                               rtest);
+        if (k == 0) st_stream(hits + i, make_float4(best_t, best_u, best_v, __int_as_float(best_prim)));
         if (COUNT && k == 0) {
             nvis += rvis;
             ntest += rtest;
@@ -829,6 +433,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8g(SceneView s, const floa
         atomicMax(&counters[2], mvis);
         atomicMax(&counters[3], mtest);
     }
+    PGRT_STAMP_END(s.stamps);
 }
 
 
@@ -909,7 +514,7 @@ __device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __re
                                           const float4* __restrict__ rd, float4* __restrict__ hits, int n,
                                           unsigned long long* __restrict__ counters, const PrimaryGen& gen,
                                           unsigned long long* __restrict__ util, int (*wstack)[kPktStack],
-                                          const int* __restrict__ perm, int budget, int* __restrict__ defer_list,
+                                          int budget, int* __restrict__ defer_list,
                                           int* __restrict__ defer_count) {
     static_assert(!(GEN && BUDGET), "level 0 has no step budget");
     const int wib = threadIdx.x >> 6;
@@ -925,8 +530,7 @@ __device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __re
     for (int base = (blockIdx.x * kTraceBlock) + wib * 64; base < n; base += gridDim.x * kTraceBlock) {
         const int slot_i = base + lane;
         const bool valid = slot_i < n;
-        // binned level: the ray of this slot (ro / rd / hits indexed by it); level 0: the slot
-        const int i = (!GEN && perm && valid) ? perm[slot_i] : slot_i;
+        const int i = slot_i;
         float4 o4 = make_float4(0, 0, 0, 0), d4 = make_float4(0, 0, 1, -1.0f);
         bool pv = false;
         if (valid) {
@@ -934,14 +538,14 @@ __device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __re
                 pv = primary_ray(gen.cam, gen.fp, gen.tiles, i, o4, d4);  // level 0: no ray queue read
                 // the level-0 shade reads the rays back; pinhole rays share origin, tnear and
                 // medium (store_ro / store_time NULL: the shade takes them from the camera)
-                gen.store_rd[i] = d4;
+                st_stream(gen.store_rd + i, d4);
                 if (gen.store_ro) {
-                    gen.store_ro[i] = o4;
-                    gen.store_time[i] = pv ? PGRT_IOR_AIR : 0.0f;
+                    st_stream(gen.store_ro + i, o4);
+                    st_stream_nt(gen.store_time + i, pv ? PGRT_IOR_AIR : 0.0f);
                 }
             } else {
-                o4 = ro[i];
-                d4 = rd[i];
+                o4 = ld_stream(ro + i);
+                d4 = ld_stream(rd + i);
             }
         }
         const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
@@ -1012,8 +616,8 @@ __device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __re
             if (gen.hitmask) {  // 1-spp level 0 (L0Final): hit records of the hits only + the wave's mask
                 const bool hit = live && best_prim >= 0;
                 const unsigned long long hm = __ballot(hit);
-                if (hit) hits[i] = make_float4(best_t, best_u, best_v, __int_as_float(best_prim));
-                if (lane == 0) gen.hitmask[base >> 6] = hm;
+                if (hit) st_stream(hits + i, make_float4(best_t, best_u, best_v, __int_as_float(best_prim)));
+                if (lane == 0) st_stream_nt(gen.hitmask + (base >> 6), hm);
                 if (COUNT && lane == 0) {
                     nvis += rvis;
                     ntest += rtest;
@@ -1021,7 +625,7 @@ __device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __re
                 continue;
             }
         }
-        if (valid) hits[i] = make_float4(live ? best_t : tfar, best_u, best_v, __int_as_float(best_prim));
+        if (valid) st_stream(hits + i, make_float4(live ? best_t : tfar, best_u, best_v, __int_as_float(best_prim)));
         if constexpr (BUDGET) {
             if (node == kDefer) {  // out of steps: the live rays to the 8-lanes-per-ray kernel
                 const unsigned long long dm = __ballot(live);
@@ -1065,202 +669,25 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void k_trace_pkt(SceneView s, co
                                                            const int* __restrict__ count_dev, int count_terms,
                                                            int count_host, int cap,
                                                            unsigned long long* __restrict__ counters, PrimaryGen gen,
-                                                           unsigned long long* __restrict__ util,
-                                                           const int* __restrict__ perm, int budget,
+                                                           unsigned long long* __restrict__ util, int budget,
                                                            int* __restrict__ defer_list, int* __restrict__ defer_count) {
+    PGRT_STAMP_BEGIN(s.stamps);
     __shared__ int wstack[kTraceBlock / 64][kPktStack];
     const int n = ray_count(count_dev, count_terms, count_host, cap);
     if constexpr (GEN) {
         if (gen.store_count && blockIdx.x == 0 && threadIdx.x == 0) *gen.store_count = n;
         // level 0 is always traced as packets: its utilisation is never sampled
-        pkt_trace<COUNT, GEN, false, false>(s, ro, rd, hits, n, counters, gen, util, wstack, nullptr, 0, nullptr,
-                                            nullptr);
+        pkt_trace<COUNT, GEN, false, false>(s, ro, rd, hits, n, counters, gen, util, wstack, 0, nullptr, nullptr);
     } else {
         // packet utilisation sampled in every 8th block (pgrt_config.packet_levels AUTO)
         if (util != nullptr && (blockIdx.x & 7) == 0)
-            pkt_trace<COUNT, GEN, true, BUDGET>(s, ro, rd, hits, n, counters, gen, util, wstack, perm, budget,
-                                                defer_list, defer_count);
+            pkt_trace<COUNT, GEN, true, BUDGET>(s, ro, rd, hits, n, counters, gen, util, wstack, budget, defer_list,
+                                                defer_count);
         else
-            pkt_trace<COUNT, GEN, false, BUDGET>(s, ro, rd, hits, n, counters, gen, util, wstack, perm, budget,
-                                                 defer_list, defer_count);
+            pkt_trace<COUNT, GEN, false, BUDGET>(s, ro, rd, hits, n, counters, gen, util, wstack, budget, defer_list,
+                                                 defer_count);
     }
-}
-
-// ---------------------------------------------------------------- wave packets, 8-wide BVH
-//
-// The bounce levels' packets are bound by their chain of dependent node fetches (one scalar-load
-// round trip per binary step, a few hundred to a thousand steps for the slowest wave), not by
-// VALU (rocprof: 4-9 % VALU busy).  Here a packet step fetches one 80-B quantized 8-wide node
-// (five scalar 16-B loads, one round trip) and every lane tests its ray against all 8 child
-// boxes: about a third of the binary steps for ~4x the VALU per step.  The wave's node groups
-// are those of k_trace8g (child base, hit bits at 24 + (slot ^ oct) | internal mask), with oct
-// the octant of the first live ray: taking the highest bit first visits the children on the
-// side the packet comes from first.  A visited node's hit leaves are tested at once (scalar
-// triangle loads, every live lane), so each lane keeps the one-lane kernels' closest hit.
-constexpr int kPkt8Stack = 32;  // node groups per wave (>= 8-wide depth + 1, like kGroupStack)
-
-template <bool COUNT, bool SAMPLE, bool BUDGET>
-__device__ __forceinline__ void pkt8_trace(const SceneView& s, const float4* __restrict__ ro,
-                                           const float4* __restrict__ rd, float4* __restrict__ hits, int n,
-                                           unsigned long long* __restrict__ counters,
-                                           unsigned long long* __restrict__ util, uint2 (*wstack)[kPkt8Stack],
-                                           const int* __restrict__ perm, int budget, int* __restrict__ defer_list,
-                                           int* __restrict__ defer_count) {
-    const int wib = threadIdx.x >> 6;
-    const int lane = __lane_id();
-    const cfloat_ptr nodes = (cfloat_ptr)(const void*)s.nodes8;  // 20 floats per node
-    const cfloat_ptr tris = (cfloat_ptr)(const void*)s.tri8;     // 12 floats per triangle
-    unsigned long long nvis = 0, ntest = 0;
-    unsigned useful = 0, live_steps = 0;
-    for (int base = (blockIdx.x * kTraceBlock) + wib * 64; base < n; base += gridDim.x * kTraceBlock) {
-        const int slot_i = base + lane;
-        const bool valid = slot_i < n;
-        const int i = (perm && valid) ? perm[slot_i] : slot_i;
-        float4 o4 = make_float4(0, 0, 0, 0), d4 = make_float4(0, 0, 1, -1.0f);
-        if (valid) {
-            o4 = ro[i];
-            d4 = rd[i];
-        }
-        const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
-        const float dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
-        const float sdx = fabsf(dx) < 1e-30f ? copysignf(1e-30f, dx) : dx;
-        const float sdy = fabsf(dy) < 1e-30f ? copysignf(1e-30f, dy) : dy;
-        const float sdz = fabsf(dz) < 1e-30f ? copysignf(1e-30f, dz) : dz;
-        const float idx = __builtin_amdgcn_rcpf(sdx), idy = __builtin_amdgcn_rcpf(sdy),
-                    idz = __builtin_amdgcn_rcpf(sdz);
-        const bool px = idx >= 0.0f, py = idy >= 0.0f, pz = idz >= 0.0f;
-        const bool live = valid && tfar >= 0.0f;
-        float best_t = live ? tfar : -1.0f;  // a dead lane's boxes all miss (t1 < 0 <= t0)
-        float best_u = 0.0f, best_v = 0.0f;
-        int best_prim = -1;
-        const unsigned long long lmask = __ballot(live);
-        const unsigned myoct = (dx > 0.0f ? 1u : 0u) | (dy > 0.0f ? 2u : 0u) | (dz > 0.0f ? 4u : 0u);
-        const int first_live = lmask ? (int)__builtin_ctzll(lmask) : 0;
-        const unsigned oct = (unsigned)__builtin_amdgcn_readfirstlane(__shfl((int)myoct, first_live, 64));
-        int sp = 0, steps = 0;
-        unsigned gbase = 0, gbits = lmask ? ((1u << (24 + oct)) | 1u) : 0u;  // root: slot 0, base 0
-        unsigned rvis = 0, rtest = 0;
-        bool deferred = false;
-        for (;;) {
-            if (gbits <= 0x00ffffffu) {
-                if (sp == 0) break;
-                --sp;
-                const uint2 g = wstack[wib][sp];
-                gbase = (unsigned)__builtin_amdgcn_readfirstlane((int)g.x);
-                gbits = (unsigned)__builtin_amdgcn_readfirstlane((int)g.y);
-            }
-            if constexpr (BUDGET) {
-                if (++steps > budget) {
-                    deferred = true;
-                    break;
-                }
-            }
-            const int pb = 31 - __clz((int)gbits);
-            gbits &= ~(1u << pb);
-            const unsigned slot = (unsigned)(pb - 24) ^ oct;
-            const int child = (int)gbase + __popc(gbits & 0xffu & ((1u << slot) - 1u));
-            if (gbits > 0x00ffffffu) {  // siblings left: save the group (the same value from every lane)
-                wstack[wib][sp] = make_uint2(gbase, gbits);
-                ++sp;
-            }
-            const cfloat_ptr nd = nodes + 20 * child;
-            const float4 p = cload4(nd);
-            const float4 mf = cload4(nd + 4), qxf = cload4(nd + 8), qyf = cload4(nd + 12), qzf = cload4(nd + 16);
-            const uint4 m = make_uint4(__float_as_uint(mf.x), __float_as_uint(mf.y), __float_as_uint(mf.z),
-                                       __float_as_uint(mf.w));
-            const uint4 qx = make_uint4(__float_as_uint(qxf.x), __float_as_uint(qxf.y), __float_as_uint(qxf.z),
-                                        __float_as_uint(qxf.w));
-            const uint4 qy = make_uint4(__float_as_uint(qyf.x), __float_as_uint(qyf.y), __float_as_uint(qyf.z),
-                                        __float_as_uint(qyf.w));
-            const uint4 qz = make_uint4(__float_as_uint(qzf.x), __float_as_uint(qzf.y), __float_as_uint(qzf.z),
-                                        __float_as_uint(qzf.w));
-            if (COUNT) ++rvis;
-            const unsigned eb = __float_as_uint(p.w);
-            const unsigned imask = eb >> 24;
-            const float ax = __uint_as_float((eb & 0xffu) << 23) * idx;
-            const float ay = __uint_as_float(((eb >> 8) & 0xffu) << 23) * idy;
-            const float az = __uint_as_float(((eb >> 16) & 0xffu) << 23) * idz;
-            const float bx = (p.x - ox) * idx, by = (p.y - oy) * idy, bz = (p.z - oz) * idz;
-            unsigned nb = 0u, tb = 0u;  // wave-uniform: hit internal children (ordered bits), hit leaves' triangles
-            bool any_hit = false;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const SlotTest st = test_slot((unsigned)k, m, qx, qy, qz, imask, ax, ay, az, bx, by, bz, px, py, pz,
-                                              best_t);
-                if (SAMPLE) any_hit |= st.hit;
-                if (__ballot(st.hit) != 0ull) {  // meta / imask are wave-uniform: so is the branch
-                    if (st.inner) nb |= 1u << (24 + ((unsigned)k ^ oct));
-                    else tb |= wide_leaf_bits(st.meta);
-                }
-            }
-            if (SAMPLE && live) {
-                ++live_steps;
-                useful += any_hit ? 1u : 0u;
-            }
-            if constexpr (BUDGET) steps += __popc(tb);
-            const unsigned tbase = m.y;
-            while (tb != 0u) {
-                const int k = (int)tbase + __ffs((int)tb) - 1;
-                tb &= tb - 1u;
-                const cfloat_ptr q = tris + 12 * k;
-                const float4 q0 = cload4(q), q1 = cload4(q + 4), q2 = cload4(q + 8);
-                if (COUNT) ++rtest;
-                if (live) tri_test(q0, q1, q2, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v, best_prim);
-            }
-            gbase = m.x;
-            gbits = nb | imask;
-        }
-        if (valid) hits[i] = make_float4(live ? best_t : tfar, best_u, best_v, __int_as_float(best_prim));
-        if constexpr (BUDGET) {
-            if (deferred) {  // out of steps: the live rays to the 8-lanes-per-ray kernel
-                const unsigned long long dm = __ballot(live);
-                int b = 0;
-                if (lane == 0) b = atomicAdd(defer_count, (int)__popcll(dm));
-                b = __builtin_amdgcn_readfirstlane(b);
-                if (live)
-                    defer_list[b + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(dm >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((unsigned)dm, 0u))] = i;
-            }
-        }
-        if (COUNT && lane == 0) {
-            nvis += rvis;
-            ntest += rtest;
-        }
-    }
-    if (SAMPLE) {
-        unsigned long long u = useful, l = live_steps;
-        for (int off = 32; off >= 1; off >>= 1) {
-            u += __shfl_xor(u, off, 64);
-            l += __shfl_xor(l, off, 64);
-        }
-        if (lane == 0 && l > 0) {
-            atomicAdd(&util[0], u);
-            atomicAdd(&util[1], l);
-        }
-    }
-    if (COUNT && lane == 0) {  // one packet step = one 80-B wide-node visit
-        atomicAdd(&counters[14], nvis);
-        atomicAdd(&counters[1], ntest);
-    }
-}
-
-template <bool COUNT, bool BUDGET>
-__global__ __launch_bounds__(kTraceBlock) void k_trace_pkt8(SceneView s, const float4* __restrict__ ro,
-                                                            const float4* __restrict__ rd, float4* __restrict__ hits,
-                                                            const int* __restrict__ count_dev, int count_terms,
-                                                            int count_host, int cap,
-                                                            unsigned long long* __restrict__ counters,
-                                                            unsigned long long* __restrict__ util,
-                                                            const int* __restrict__ perm, int budget,
-                                                            int* __restrict__ defer_list, int* __restrict__ defer_count) {
-    __shared__ uint2 wstack[kTraceBlock / 64][kPkt8Stack];
-    const int n = ray_count(count_dev, count_terms, count_host, cap);
-    if (util != nullptr && (blockIdx.x & 7) == 0)
-        pkt8_trace<COUNT, true, BUDGET>(s, ro, rd, hits, n, counters, util, wstack, perm, budget, defer_list,
-                                        defer_count);
-    else
-        pkt8_trace<COUNT, false, BUDGET>(s, ro, rd, hits, n, counters, util, wstack, perm, budget, defer_list,
-                                         defer_count);
+    PGRT_STAMP_END(s.stamps);
 }
 
 // Kernel-exact launch timing (profile frames): the closest-hit launch records the caller's
@@ -1282,37 +709,18 @@ bool trace_packets_available(const SceneView& s) {
 
 // 4 lanes per ray (two child slots each) above this many rays, 8 at or below it (r1 A/B)
 constexpr int kGroup8Max = 150000;
-// queues up to kTailMax rays spread over more waves: kTailRpw rays per wave (r1 A/B: 64, i.e.
-// full waves, was best)
-constexpr int kTailMax = 131072, kTailRpw = 64;
 
-// one-lane queues of full waves: lane refill (k_trace_rf) once this many lanes of a wave are
-// idle; 0 = lockstep k_trace.  PGRT_REFILL overrides (A/B), PGRT_REFILL_GRID scales the grid
-// (resident blocks x factor).
-static int env_int(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
-static int refill_min_idle() {
-    static const int v = env_int("PGRT_REFILL", 0);
-    return v;
-}
-static int refill_blocks_factor() {
-    static const int v = std::max(1, env_int("PGRT_REFILL_GRID", 1));
-    return v;
-}
-
-bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) {
+bool launch_trace(const SceneView& s_in, const TraceLaunch& t, hipStream_t stream) {
+    SceneView s = s_in;  // s.stamps: this launch's timeline slots (stamps.hpp)
     const int max_count = t.max_count;
     if (max_count <= 0) return false;
     PGRT_REQUIRE((t.ro && !t.lit) || (!s.wide && !t.packets && !t.gen && !t.allow_group), PGRT_ERR_INVALID_ARGUMENT,
                  "compact shadow queues are traced by the one-lane binary kernel only");
     const int ex = t.expect > 0 && t.expect < max_count ? t.expect : max_count;  // grid sizing only
-    PGRT_REQUIRE(!t.perm || (!s.wide && !t.lit && !t.gen), PGRT_ERR_INVALID_ARGUMENT,
-                 "binned launches are level queues over the binary or grouped 8-wide kernels");
     if (s.wide) {
         int grid = ceil_div(ex, kTraceBlock);
         if (grid > t.gstack_threads / kTraceBlock) grid = t.gstack_threads / kTraceBlock;
+        s.stamps = stamp_next(t.lit || !t.allow_group ? kStampTraceShadow : kStampTrace, t.level, grid, kTraceBlock);
         if (t.count)
             PGRT_TLAUNCH((k_trace8<true>), dim3(grid), dim3(kTraceBlock), 0, stream, s, t.ro, t.rd, t.hits,
                          t.count_dev, t.count_terms, t.count_host, max_count, t.gstack, t.counters);
@@ -1328,24 +736,14 @@ bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) 
         const PrimaryGen g = t.gen ? *t.gen : PrimaryGen{};
         // a step budget on a bounce level: the waves out of steps hand their rays to k_trace8g
         const bool budget = !t.gen && t.budget > 0 && t.defer_list && t.defer_count && s.depth8 + 1 <= kGroupStack;
-        hipEvent_t ev_stop = budget ? nullptr : t_ev_stop;  // profile timing spans both launches
+        hipEvent_t ev_stop = budget && t.resume ? nullptr : t_ev_stop;  // profile timing spans both launches
 #define PGRT_LAUNCH_P(C, G, W, B)                                                                              \
     hipExtLaunchKernelGGL((k_trace_pkt<C, G, W, B>), dim3(grid), dim3(kTraceBlock), 0, stream, t_ev_start, ev_stop, \
                           0, s, t.ro, t.rd, t.hits, t.count_dev, t.count_terms, t.count_host, max_count, t.counters, \
-                          g, t.pkt_util, t.perm, t.budget, t.defer_list, t.defer_count)
+                          g, t.pkt_util, t.budget, t.defer_list, t.defer_count)
         const bool big = s.ntri > kPacketBigScene;
-        if (!t.gen && t.wide_packets && s.depth8 + 1 <= kPkt8Stack) {  // bounce level over the 8-wide BVH
-#define PGRT_LAUNCH_P8(C, B)                                                                                      \
-    hipExtLaunchKernelGGL((k_trace_pkt8<C, B>), dim3(grid), dim3(kTraceBlock), 0, stream, t_ev_start, ev_stop, 0, s, \
-                          t.ro, t.rd, t.hits, t.count_dev, t.count_terms, t.count_host, max_count, t.counters,        \
-                          t.pkt_util, t.perm, t.budget, t.defer_list, t.defer_count)
-            if (t.count) {
-                if (budget) PGRT_LAUNCH_P8(true, true); else PGRT_LAUNCH_P8(true, false);
-            } else {
-                if (budget) PGRT_LAUNCH_P8(false, true); else PGRT_LAUNCH_P8(false, false);
-            }
-#undef PGRT_LAUNCH_P8
-        } else if (t.count) {
+        s.stamps = stamp_next(kStampTracePkt, t.level, grid, kTraceBlock);
+        if (t.count) {
             if (t.gen) PGRT_LAUNCH_P(true, true, 1, false);
             else if (budget) PGRT_LAUNCH_P(true, false, 1, true);
             else PGRT_LAUNCH_P(true, false, 1, false);
@@ -1357,13 +755,14 @@ bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) 
             PGRT_LAUNCH_P(false, false, 1, false);
         }
 #undef PGRT_LAUNCH_P
-        if (budget) {  // the deferred rays: 8 lanes per ray, from the packet's closest hits
+        if (budget && t.resume) {  // the deferred rays: 8 lanes per ray, from the packet's closest hits
             // grid from the previous deferral count; with none known (a level's first packet frame,
             // e.g. AUTO's start or probe on an incoherent scene, where most waves run out of steps),
             // from the level's rays -- a 1024-ray grid striding over millions of deferred rays made
             // single launches of 0.1-0.4 s on C5 (profiles/r3/c5_kernel_stats_r3fin.csv)
             const int dex = std::max(t.defer_expect > 0 ? t.defer_expect : ex, 1024);
             const int g8 = std::min(16384, ceil_div(dex, kTraceBlock / 8));
+            s.stamps = stamp_next(kStampTraceResume, t.level, g8, kTraceBlock);
             if (t.count)
                 hipExtLaunchKernelGGL((k_trace8g<true, 8, true>), dim3(g8), dim3(kTraceBlock), 0, stream, nullptr,
                                       t_ev_stop, 0, s, t.ro, t.rd, t.hits, t.defer_count, 1, 0, max_count, t.counters,
@@ -1379,9 +778,11 @@ bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) 
         // 8 lanes per ray for the smallest queues (the latency floor of the slowest ray),
         // 4 lanes (two child slots each) when there are enough rays to fill the machine
         const bool g4 = ex > kGroup8Max;
+        s.stamps = stamp_next(kStampTrace8g, t.level, std::min(16384, ceil_div(ex, kTraceBlock / (g4 ? 4 : 8))),
+                              kTraceBlock);
 #define PGRT_LAUNCH_G(C, G)                                                                                       \
     PGRT_TLAUNCH((k_trace8g<C, G>), dim3(std::min(16384, ceil_div(ex, kTraceBlock / G))), dim3(kTraceBlock), 0, \
-                 stream, s, t.ro, t.rd, t.hits, t.count_dev, t.count_terms, t.count_host, max_count, t.counters, t.perm)
+                 stream, s, t.ro, t.rd, t.hits, t.count_dev, t.count_terms, t.count_host, max_count, t.counters, nullptr)
         if (t.count) {
             if (g4) PGRT_LAUNCH_G(true, 4); else PGRT_LAUNCH_G(true, 8);
         } else {
@@ -1390,50 +791,16 @@ bool launch_trace(const SceneView& s, const TraceLaunch& t, hipStream_t stream) 
 #undef PGRT_LAUNCH_G
         return true;
     }
-    const int rpw = ex <= kTailMax ? kTailRpw : 64;
-    int grid = ceil_div(ex, (kTraceBlock / 64) * rpw);
+    int grid = ceil_div(ex, kTraceBlock);
     if (grid > t.gstack_threads / kTraceBlock) grid = t.gstack_threads / kTraceBlock;
     // all-LDS stack when the BVH depth fits (depth + 2 entries per lane, <= 64 KB per block)
     const int entries = s.depth + 2;
-    // PGRT_TRACE_SPILL=1 (A/B): the short LDS stack (kLdsStack entries, the rest in global memory)
-    // even when the whole stack fits -- 16 KB per block instead of (depth + 2) KB, more blocks per CU
-    static const bool force_spill = env_int("PGRT_TRACE_SPILL", 0) != 0;
-    const bool spill = force_spill || entries * kTraceBlock * 4 > 65536;
+    const bool spill = entries * kTraceBlock * 4 > 65536;
     const size_t lds = (size_t)(spill ? kLdsStack : entries) * kTraceBlock * sizeof(int);
-    // child prefetch for latency-bound one-lane launches: PGRT_TRACE_PF = the largest expected
-    // queue that takes it (A/B; 0 = never)
-    static const int pf_max = env_int("PGRT_TRACE_PF", 0);
-    if (!t.count && !spill && ex <= pf_max) {
-        PGRT_TLAUNCH(k_trace_pf, dim3(std::min(grid, ceil_div(ex, kTraceBlock))), dim3(kTraceBlock), lds, stream, s,
-                     t.ro, t.rd, t.hits, t.count_dev, t.count_terms, t.count_host, max_count, t.const_org, t.lit,
-                     t.perm);
-        return true;
-    }
-    const int min_idle = refill_min_idle();
-    if (min_idle > 0 && !t.count && !spill && rpw == 64) {
-        // lane refill: a grid of resident blocks, each wave walking its own slot sequence
-        static int cus = 0, resident = 0;
-        static size_t resident_lds = 0;
-        if (!cus) {
-            int dev = 0;
-            (void)hipGetDevice(&dev);
-            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            cus = std::max(1, cus);
-        }
-        if (resident_lds != lds) {  // blocks resident per CU at this stack size (VGPRs and LDS)
-            int per_cu = 0;
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_rf, kTraceBlock, lds);
-            resident = std::max(1, per_cu) * cus;
-            resident_lds = lds;
-        }
-        const int rgrid = std::min(ceil_div(ex, kTraceBlock), resident * refill_blocks_factor());
-        PGRT_TLAUNCH(k_trace_rf, dim3(rgrid), dim3(kTraceBlock), lds, stream, s, t.ro, t.rd, t.hits, t.count_dev,
-                     t.count_terms, t.count_host, max_count, t.const_org, t.lit, t.perm, min_idle);
-        return true;
-    }
+    s.stamps = stamp_next(t.lit || !t.allow_group ? kStampTraceShadow : kStampTrace, t.level, grid, kTraceBlock);
 #define PGRT_LAUNCH(C, S)                                                                                      \
     PGRT_TLAUNCH((k_trace<C, S>), dim3(grid), dim3(kTraceBlock), lds, stream, s, t.ro, t.rd, t.hits, t.count_dev, \
-                 t.count_terms, t.count_host, max_count, t.gstack, t.counters, rpw, t.const_org, t.lit, t.perm)
+                 t.count_terms, t.count_host, max_count, t.gstack, t.counters, t.const_org, t.lit)
     if (t.count) {
         if (spill) PGRT_LAUNCH(true, true); else PGRT_LAUNCH(true, false);
     } else {

@@ -12,10 +12,6 @@ constexpr int kLdsStack = 16;
 constexpr int kGlobalStack = 112;
 constexpr int kTile = 64;         // image tile side (multi-GPU unit, level-0 ray order)
 constexpr int kMaxLevels = 16;    // max_level + 1 <= kMaxLevels
-// bounce-level ray binning (pgrt_config.ray_binning): the rays of a level traced as wave packets
-// are visited in bins of equal direction octant (key = sign bits of the direction), so a wave's
-// 64 rays share their direction signs and, within a bin, the queue's screen-space order
-constexpr int kBins = 8;
 
 // Per-frame device counters (zeroed by one hipMemsetAsync per batch).
 struct FrameCounters {
@@ -39,18 +35,10 @@ struct FrameCounters {
     // profile == 2: per level, shaded rays that hit a triangle and, of those, the ones whose
     // Phong branch sampled a texture (the whole-frame roofline's attribute / texel bytes)
     alignas(128) unsigned long long shade[kMaxLevels][2];
-    // ray binning per level: bin sizes (statistics)
-    alignas(128) unsigned bins[kMaxLevels][kBins];
     // packet launches with a step budget (pgrt_config.packet_budget): rays of the waves that ran
     // out of steps, finished by the 8-lanes-per-ray kernel (count; the list is FrameSlot::q_defer)
     alignas(128) int defer[kMaxLevels];
-    // persistent tail (tail.hip): per tail level the next unclaimed queue slot; rays shaded so far;
-    // set when a bounded wait ran out (a fault report, never a normal outcome)
-    alignas(128) int tail_head[kMaxLevels];
-    alignas(128) int tail_done_level[kMaxLevels];  // rays of each tail level shaded so far
-    alignas(128) int tail_done;
-    alignas(128) int tail_alive;  // blocks of the tail launch still running
-    int tail_err;
+    int probe_defer;  // the AUTO probe's deferral count (its side launch; never read)
 };
 
 __host__ __device__ inline int fc_count(const FrameCounters& f, int L) {
@@ -93,7 +81,6 @@ struct Queue {
     float* time;     // medium IOR (RTCRay::time as used by the reference)
     float4* hit;     // t, u, v, prim bits
     int cap;
-    unsigned char* key = nullptr;  // binning key per ray (written by the shade that emits the rays), or NULL
 };
 
 // direction octant of a ray: the sign bits the packet traversal specialises its node loop on
@@ -128,11 +115,6 @@ struct LevelNodes {  // per-level node records kept until the combine pass
     int4* link;      // dielectric: (refl child, refr child or -1, -, -); opaque: (-1,-1,shadow base, n)
     float4* att;     // dielectric: (att.r, att.g, att.b, R)
 };
-struct AllLevelNodes {  // every level's node records (k_resolve_pending)
-    float4* color[kMaxLevels];
-    int4* link[kMaxLevels];
-    float4* att[kMaxLevels];
-};
 
 struct ShadowQueue {  // one per batch: the shadow rays of every level, level-major
     float4* ro;       // NULL in the compact form (one light: every shadow ray starts at it)
@@ -155,6 +137,7 @@ struct ShadowQueue {  // one per batch: the shadow rays of every level, level-ma
 // per ray.  count: profile == 2 traversal counters into counters[16].
 struct PrimaryGen;  // camera_ops.hpp
 struct TraceLaunch {
+    int level = -1;  // queue level (timeline records), -1: none / the shadow queue
     const float4* ro = nullptr;
     const float4* rd = nullptr;
     float4* hits = nullptr;
@@ -175,18 +158,15 @@ struct TraceLaunch {
     // const_org (xyz, tnear in w); lit != NULL -> write is_illuminated's byte, not the hit
     float4 const_org = make_float4(0, 0, 0, 0);
     unsigned char* lit = nullptr;
-    // binned level: launch slot i traces ray perm[i] (ro / rd / hits indexed by it), NULL = i
-    const int* perm = nullptr;
     // bounce-level packets (packets && !gen): a wave still traversing after `budget` node /
     // triangle steps stores its rays' closest hits so far and appends the rays to defer_list
     // (count in *defer_count); a second launch finishes them 8 lanes per ray over the 8-wide BVH,
     // starting from those hits.  budget 0: no budget.  defer_expect sizes its grid.
     int budget = 0;
-    // bounce-level packets over the 8-wide BVH (k_trace_pkt8) instead of the binary one
-    bool wide_packets = false;
     int* defer_list = nullptr;
     int* defer_count = nullptr;
     int defer_expect = 0;
+    bool resume = true;  // false: the deferred rays are not finished (a side launch that only samples)
 };
 // the packet traversal needs the binary layout and a tree that fits its wave-uniform stack
 bool trace_packets_available(const SceneView& s);
@@ -220,40 +200,22 @@ void launch_combine(const SceneView& s, int level, LevelNodes nodes, const float
 // resolved: level 0's final colours were written by launch_combine(level 0) (several samples
 // per pixel).  l0f.pending != NULL (1 spp, L0Final): only the pixels whose bit is set there are
 // finished (the others were written by the level-0 shade).
-void launch_resolve_pending(const SceneView& s, const FrameParams& fp, const int4* tiles, const AllLevelNodes& lv,
-                            ShadowQueue sq, const FrameOut& fo, const unsigned long long* pending, int npix,
-                            hipStream_t stream);
 void launch_finish(const SceneView& s, const FrameParams& fp, const int4* tiles, LevelNodes l0, const float4* child,
                    ShadowQueue sq, float4* accum, const FrameOut& fo, int npix, bool first, bool last,
                    bool resolved, const unsigned long long* pending, hipStream_t stream);
 // frame sink: sum += frame (count-th frame; count == 1 resets), mean = sum / count
 void launch_accumulate_frame(const float* frame, float* sum, float* mean, long long pixels, int count,
                              hipStream_t stream);
-// stable ray binning of level `level`: per-chunk bin counts (chunk_buf: kBins words per 256 queue
-// slots), their scan, the scatter of the ray indices into perm, bin by bin (expect sizes the grids)
-void launch_bin_rays(const unsigned char* keys, FrameCounters* fc, int level, int cap, int* perm, unsigned* chunk_buf,
-                     int expect, hipStream_t stream);
-// The deep Whitted levels first .. levels-1 as ONE persistent launch (tail.hip): blocks claim 256
-// rays of the shallowest level with unclaimed rays, trace them one lane per ray, shade them and
-// hand their children to the next level through write-through 40-B granules whose last word
-// carries `epoch` (the slot's ready flag), so a ray is traced as soon as its parent is shaded and a
-// level never waits for the slowest ray of the one before it.  Level `first` is the queue the
-// shade of level first-1 wrote (count fc_count(first), capacity first_cap); children of level L go
-// to gran[L+1] (5 words per slot, capacity cap[L+1]); node records and shadow rays as in k_shade,
-// every tail level's shadow rays counted on the high word of fc->alloc[first].
-struct TailLaunch {
-    int first, levels;
-    Queue q_first;
-    unsigned long long* gran[kMaxLevels];
-    int cap[kMaxLevels];
-    LevelNodes nodes[kMaxLevels];
-    ShadowQueue sq;
-    FrameCounters* fc;
-    unsigned epoch;
-    int grid;
-};
-bool tail_available(const SceneView& s);
-void launch_tail(const SceneView& s, const FrameParams& fp, const TailLaunch& t, hipStream_t stream);
+// The deep Whitted levels as one launch (subtree.hip): every ray of level `level` (queue q, count
+// fc_count(level)) evaluates its whole ray tree depth first -- reflection, refraction and shadow
+// rays traced by 8 (4) lanes per ray over the 8-wide BVH -- and writes its final colour as a
+// level-`level` node record (k_combine of level - 1 reads it); the per-level statistics of the
+// deeper levels are counted as k_shade counts them.  expect sizes the grid; count: profile == 2
+// traversal / shading counters.
+constexpr int kSubtreeGroup8Max = 150000;  // 4 lanes per ray above this many rays (as kGroup8Max)
+bool subtree_available(const SceneView& s);
+void launch_subtree(const SceneView& s, const FrameParams& fp, int level, Queue q, LevelNodes nodes,
+                    FrameCounters* fc, int max_count, int expect, bool count, hipStream_t stream);
 // copy `n` FrameCounters to pinned host memory and zero them on the device
 void launch_export_counters(FrameCounters* dev, FrameCounters* host, int n, hipStream_t stream);
 // Distributed frames: rank r's tile-compact buffer (frame-major, count[r] tiles per frame in its
@@ -269,6 +231,19 @@ struct TileDeal;  // tiles.hpp
 // frame); channels 4 (RGBA tiles) or 3 (RGB tiles, alpha 1: the gather format)
 void launch_unpack_tiles(const UnpackSrc& u, float* rgba, int width, int height, const TileDeal& deal, int channels,
                          hipStream_t stream, int frame0, int nframes);
+// Distributed frames without a control collective: a rank's send carries, after its tiles, a tail
+// of kGatherTail floats whose first word is its queue-overflow flag (the OR of every slot's and
+// batch's FrameCounters::overflow, read from the exported counters); rank 0 copies every peer's
+// flag into host memory.  fcs[j]: slot j's exported counters (host-mapped), n[j] batches.
+constexpr int kGatherTail = 4;
+struct FlagSrc {
+    const FrameCounters* fc[4];
+    int n[4];
+    int K;
+};
+void launch_overflow_flag(const FlagSrc& f, int* out, hipStream_t stream);
+// flags[r] = the flag word after rank r's `floats` floats of tiles at u.src[r] (r = 1 .. world-1)
+void launch_peer_flags(const UnpackSrc& u, int world, size_t floats_per_tile_count, int* flags, hipStream_t stream);
 
 // scene / BVH build
 constexpr int kBuilderLbvh = PGRT_BVH_LBVH;  // Karras 2012 over 63-bit Morton codes
@@ -303,8 +278,6 @@ void build_ploc(const float* pos_dev, const float4* ref_lo, const float4* ref_hi
                 float4* tri_out, BvhNode* nodes_out, BuildOut* out, int* iterations, hipStream_t stream);
 // PLOC over triangle references (split.hip): beta > 0 adds up to beta * n split references
 // (early split clipping); sizes tri (3 float4 per reference) and nodes; returns the count
-// sibling-pair cache-line layout of a built binary BVH (bvh_layout.hip); returns the node count
-int relayout_bvh(DevBuf<BvhNode>& nodes, int num_nodes, int* root, hipStream_t stream);
 int build_ploc_refs(const float* pos_dev, int ntri, float beta, float pad, float extent, DevBuf<float4>& tri,
                     DevBuf<BvhNode>& nodes, BuildOut* out, hipStream_t stream);
 void build_lbvh(const float* pos_dev, int ntri, float4* tri_out, BvhNode* nodes_out, int* scratch_int,

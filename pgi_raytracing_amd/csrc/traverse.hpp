@@ -1,6 +1,5 @@
-// traverse.hpp -- the closest-hit building blocks shared by the traversal kernels (trace.hip) and
-// the persistent tail kernel (tail.hip): slab tests against a BVH2 node's child boxes, Embree's
-// triangle test, and one lane's complete closest-hit traversal with its stack in LDS.
+// traverse.hpp -- the closest-hit building blocks of the traversal kernels (trace.hip): slab tests
+// against a BVH2 node's child boxes and Embree's triangle test.
 // Reference: rtcIntersect1 (APP/raytracer.cpp:130-148 get_ray_hit; rtcore_scene.h:96).
 #pragma once
 
@@ -77,77 +76,177 @@ __device__ __forceinline__ void tri_test(float4 q0, float4 q1, float4 q2, float 
                 best_prim);
 }
 
-// One lane's closest hit over the binary BVH (the one-lane kernel's while-while loop with
-// postponed leaves, Aila & Laine 2009), the stack in LDS: lstack[entry * stride + slot], depth + 2
-// entries (the caller sizes it).  o4 = org | tnear, d4 = dir | tfar; tfar < 0 (padding) -> no
-// hit.  Returns (t, u, v, prim bits); prim -1 = no hit (t = tfar).
-__device__ __forceinline__ float4 trace_closest_lds(const SceneView& s, float4 o4, float4 d4, int* lstack, int stride,
-                                                    int slot) {
+__device__ __forceinline__ float qb(unsigned w, int j) { return (float)((w >> (8 * j)) & 0xffu); }
+
+// ---- 8 lanes per ray, 8-wide BVH
+//
+// For small queues (the deep Whitted levels: tens of thousands of rays on 1024 SIMDs) a level
+// takes as long as its slowest ray, and a one-lane traversal of that ray is a chain of ~100
+// dependent node fetches.  Here 8 lanes trace one ray: every lane tests one child box of the
+// current 8-wide node (lane k takes slot k ^ octant, so the group's ballot byte is already in
+// near-to-far order), and the triangles of the node's hit leaves are tested 8 at a time.  The
+// chain shrinks to one fetch per 8-wide node (about a third of the binary depth) plus one per
+// leaf batch.  All 8 lanes hold identical traversal state (ballot / DPP reductions), so the
+// group's control flow is uniform; the node-group stack lives in LDS, one per group.
+constexpr int kGroupStack = 32;  // node groups per ray: >= 8-wide depth + 1
+
+// reduce over the 8 lanes of a group: xor 1, xor 2 (quad DPP), then lane i <-> 7 - i (row
+// half mirror), so every lane ends with the group value
+#ifdef PGRT_GROUP_SHFL  // debugging aid: the same reductions through ds_bpermute
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __shfl_xor(v, CTRL == 0xB1 ? 1 : (CTRL == 0x4E ? 2 : 7), 64);
+}
+#else
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+}
+#endif
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(dpp_i<CTRL>(__float_as_int(v)));
+}
+constexpr int kDppXor1 = 0xB1;        // quad_perm [1,0,3,2]
+constexpr int kDppXor2 = 0x4E;        // quad_perm [2,3,0,1]
+constexpr int kDppHalfMirror = 0x141;  // row_half_mirror
+
+template <int CTRL>
+__device__ __forceinline__ void merge_hit_step(float& t, float& u, float& v, int& prim) {
+    const float ot = dpp_f<CTRL>(t), ou = dpp_f<CTRL>(u), ov = dpp_f<CTRL>(v);
+    const int op = dpp_i<CTRL>(prim);
+    if (op >= 0 && (prim < 0 || ot < t || (ot == t && op < prim))) {
+        t = ot;
+        u = ou;
+        v = ov;
+        prim = op;
+    }
+}
+
+// group reductions: G = 8 uses xor 1, xor 2 and the half-row mirror; G = 4 the two quad steps
+template <int G>
+__device__ __forceinline__ int group_or(int v) {
+    v |= dpp_i<kDppXor1>(v);
+    v |= dpp_i<kDppXor2>(v);
+    if constexpr (G == 8) v |= dpp_i<kDppHalfMirror>(v);
+    return v;
+}
+template <int G>
+__device__ __forceinline__ void group_merge_hit(float& t, float& u, float& v, int& prim) {
+    merge_hit_step<kDppXor1>(t, u, v, prim);
+    merge_hit_step<kDppXor2>(t, u, v, prim);
+    if constexpr (G == 8) merge_hit_step<kDppHalfMirror>(t, u, v, prim);
+}
+
+// one child slot of a wide node against the ray (conservative quantized slab test)
+struct SlotTest {
+    bool hit, inner;
+    unsigned meta;
+};
+__device__ __forceinline__ SlotTest test_slot(unsigned slot, const uint4& m, const uint4& qx, const uint4& qy,
+                                              const uint4& qz, unsigned imask, float ax, float ay, float az,
+                                              float bx, float by, float bz, bool px, bool py, bool pz,
+                                              float best_t) {
+    const int j = (int)(slot & 3u);
+    const bool hi_half = slot >= 4u;
+    const unsigned lxw = hi_half ? qx.y : qx.x, hxw = hi_half ? qx.w : qx.z;
+    const unsigned lyw = hi_half ? qy.y : qy.x, hyw = hi_half ? qy.w : qy.z;
+    const unsigned lzw = hi_half ? qz.y : qz.x, hzw = hi_half ? qz.w : qz.z;
+    const float lx = qb(lxw, j), hx = qb(hxw, j), ly = qb(lyw, j), hy = qb(hyw, j);
+    const float lz = qb(lzw, j), hz = qb(hzw, j);
+    const float t0 = fmaxf(fmaxf(fmaf(px ? lx : hx, ax, bx), fmaf(py ? ly : hy, ay, by)),
+                           fmaxf(fmaf(pz ? lz : hz, az, bz), 0.0f));
+    const float t1 = fminf(fminf(fmaf(px ? hx : lx, ax, bx), fmaf(py ? hy : ly, ay, by)),
+                           fminf(fmaf(pz ? hz : lz, az, bz), best_t));
+    SlotTest r;
+    r.meta = ((hi_half ? m.w : m.z) >> (8 * j)) & 0xffu;
+    r.hit = r.meta != 0u && t0 <= t1 * 1.000001f;
+    r.inner = ((imask >> slot) & 1u) != 0u;
+    return r;
+}
+
+
+// One ray traced by a group of G lanes (k = lane in the group, gshift = the group's first lane in
+// the wave) over the 8-wide BVH; stk[sp * stride] is the group's node-group stack (kGroupStack
+// entries, LDS).  Every lane of the group ends with the closest hit in best_* (in: the bound to
+// start from -- tfar and no hit, or a hit found earlier).  o4 = org | tnear, d4 = dir | tfar;
+// tfar < 0 (padding) -> nothing is traversed.
+template <int G, bool COUNT>
+__device__ __forceinline__ void trace8_group(const SceneView& s, float4 o4, float4 d4, int k, int gshift, uint2* stk,
+                                             int stride, float& best_t, float& best_u, float& best_v, int& best_prim,
+                                             unsigned& rvis, unsigned& rtest) {
     const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
     const float dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
     const float sdx = fabsf(dx) < 1e-30f ? copysignf(1e-30f, dx) : dx;
     const float sdy = fabsf(dy) < 1e-30f ? copysignf(1e-30f, dy) : dy;
     const float sdz = fabsf(dz) < 1e-30f ? copysignf(1e-30f, dz) : dz;
     const float idx = __builtin_amdgcn_rcpf(sdx), idy = __builtin_amdgcn_rcpf(sdy), idz = __builtin_amdgcn_rcpf(sdz);
-    const float oix = ox * idx, oiy = oy * idy, oiz = oz * idz;
-    float best_t = tfar, best_u = 0.0f, best_v = 0.0f;
-    int best_prim = -1;
+    const bool px = idx >= 0.0f, py = idy >= 0.0f, pz = idz >= 0.0f;
+    const unsigned oct = (dx > 0.0f ? 1u : 0u) | (dy > 0.0f ? 2u : 0u) | (dz > 0.0f ? 4u : 0u);
     int sp = 0;
-    lstack[slot] = kSentinel;  // stack[0]
-    int node = s.root;
-    int leaf = 0;  // postponed leaf (negative code) or 0
-    if (node < 0) {
-        leaf = node;
-        node = kSentinel;
-    }
-    if (!(tfar >= 0.0f)) {
-        node = kSentinel;
-        leaf = 0;
-    }
-    while (node != kSentinel || leaf < 0) {
-        const float bt = __builtin_canonicalizef(best_t);
-        while ((unsigned)node < (unsigned)kSentinel) {
-            const int top = lstack[sp * stride + slot];
-            const BvhNode* nd = s.nodes + node;
-            const float4 a = nd->a, b = nd->b, c = nd->c;
-            const int4 d = nd->d;
-            float t0, t1;
-            const bool h0 = box_hit(a.x, a.y, a.z, a.w, c.x, c.y, idx, idy, idz, oix, oiy, oiz, bt, t0);
-            const bool h1 = box_hit(b.x, b.y, b.z, b.w, c.z, c.w, idx, idy, idz, oix, oiy, oiz, bt, t1);
-            const bool any = h0 || h1;
-            const bool first0 = h0 && (!h1 || t0 <= t1);
-            const bool both = h0 && h1;
-            lstack[(sp + 1) * stride + slot] = first0 ? d.y : d.x;  // above the top: free either way
-            node = any ? (first0 ? d.x : d.y) : top;
-            sp += both ? 1 : (any ? 0 : -1);
-            if (node < 0 && leaf == 0) {  // first leaf: park it and keep descending
-                leaf = node;
-                node = lstack[sp * stride + slot];
+    unsigned gbase = 0, gbits = (1u << (24 + oct)) | 1u;  // the root: slot 0 of a virtual parent
+    if (!(tfar >= 0.0f)) gbits = 0;
+    unsigned tbase = 0, tbits = 0;
+    for (;;) {
+        while (tbits == 0u) {  // ---- node phase (group-uniform) ----
+            if (gbits <= 0x00ffffffu) {
+                if (sp == 0) break;
                 --sp;
+                const uint2 g = stk[sp * stride];
+                gbase = g.x;
+                gbits = g.y;
             }
-            if (!__any(leaf == 0)) break;
+            const int pb = 31 - __clz((int)gbits);
+            gbits &= ~(1u << pb);
+            const unsigned slot = (unsigned)(pb - 24) ^ oct;
+            const int child = (int)gbase + __popc(gbits & 0xffu & ((1u << slot) - 1u));
+            if (gbits > 0x00ffffffu) {
+                stk[sp * stride] = make_uint2(gbase, gbits);  // same value from all lanes of the group
+                ++sp;
+            }
+            const Bvh8Node* nd = s.nodes8 + child;
+            const float4 p = nd->p;
+            const uint4 m = nd->m, qx = nd->qx, qy = nd->qy, qz = nd->qz;
+            if (COUNT) ++rvis;
+            const unsigned eb = __float_as_uint(p.w);
+            const unsigned imask = eb >> 24;
+            const float ax = __uint_as_float((eb & 0xffu) << 23) * idx;
+            const float ay = __uint_as_float(((eb >> 8) & 0xffu) << 23) * idy;
+            const float az = __uint_as_float(((eb >> 16) & 0xffu) << 23) * idz;
+            const float bx = (p.x - ox) * idx, by = (p.y - oy) * idy, bz = (p.z - oz) * idz;
+            // lane k tests the slot at near-to-far position k (slot k ^ oct) and, for G = 4, also
+            // position k + 4; the ballots then give the group's near-to-far hit byte
+            const SlotTest s0 =
+                test_slot((unsigned)k ^ oct, m, qx, qy, qz, imask, ax, ay, az, bx, by, bz, px, py, pz, best_t);
+            int tb = (s0.hit && !s0.inner) ? (int)wide_leaf_bits(s0.meta) : 0;
+            unsigned nb = (unsigned)(__ballot(s0.hit && s0.inner) >> gshift) & ((1u << G) - 1u);
+            if constexpr (G == 4) {
+                const SlotTest s1 = test_slot((unsigned)(k + 4) ^ oct, m, qx, qy, qz, imask, ax, ay, az, bx, by, bz,
+                                              px, py, pz, best_t);
+                if (s1.hit && !s1.inner) tb |= (int)wide_leaf_bits(s1.meta);
+                nb |= ((unsigned)(__ballot(s1.hit && s1.inner) >> gshift) & 0xfu) << 4;
+            }
+            tb = group_or<G>(tb);
+            gbase = m.x;
+            gbits = (nb << 24) | imask;
+            tbase = m.y;
+            tbits = (unsigned)tb;
         }
-        while (leaf < 0) {
-            const int first = leaf_first(leaf), end = first + leaf_count(leaf);
-            float4 p0 = s.tri[3 * first], p1 = s.tri[3 * first + 1], p2 = s.tri[3 * first + 2];
-            for (int k = first; k < end; ++k) {
-                const float4 q0 = p0, q1 = p1, q2 = p2;
-                if (k + 1 < end) {
-                    p0 = s.tri[3 * k + 3];
-                    p1 = s.tri[3 * k + 4];
-                    p2 = s.tri[3 * k + 5];
-                }
+        if (tbits == 0u) break;
+        // ---- triangle phase: G triangles per round, then the group's closest hit ----
+        while (tbits != 0u) {
+            unsigned mine = tbits;
+            for (int q = 0; q < k; ++q) mine &= mine - 1u;  // this lane's set bit
+            if (mine != 0u) {
+                const int tr = (int)tbase + __ffs((int)mine) - 1;
+                const float4 q0 = s.tri8[3 * tr], q1 = s.tri8[3 * tr + 1], q2 = s.tri8[3 * tr + 2];
                 tri_test(q0, q1, q2, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v, best_prim);
             }
-            leaf = 0;
-            if (node < 0) {  // the node popped after parking is a leaf too: test it now
-                leaf = node;
-                node = lstack[sp * stride + slot];
-                --sp;
-            }
+            if (COUNT) rtest += (unsigned)min(__popc(tbits), G);
+            for (int q = 0; q < G; ++q) tbits &= tbits - 1u;
+            group_merge_hit<G>(best_t, best_u, best_v, best_prim);
         }
     }
-    return make_float4(best_t, best_u, best_v, __int_as_float(best_prim));
 }
 
 }  // namespace pgrt

@@ -101,6 +101,8 @@ def lib():
         "pgrt_obj_surface_range": (ip, [vp, ip, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "pgrt_selftest_math": (ip, [vp, fp, ip, fp]),
         "pgrt_frame_diag": (ip, [vp, C.POINTER(abi.LevelDiag), ip]),
+        "pgrt_timeline_enable": (ip, [vp, ip]),
+        "pgrt_timeline_read": (ip, [vp, C.POINTER(abi.TimelineRec), ip, C.POINTER(C.c_int)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name, None)
@@ -269,6 +271,27 @@ class Context:
         _check(self.h, self.L.pgrt_occluded(self.h, abi.fptr(rays), rays.shape[0],
                                             occ.ctypes.data_as(C.POINTER(C.c_int))))
         return occ.astype(bool)
+
+    def timeline_enable(self, on: bool = True):
+        """pgrt_timeline_enable: every later frame's launches stamp the device clock."""
+        _check(self.h, self.L.pgrt_timeline_enable(self.h, 1 if on else 0))
+
+    def timeline_read(self) -> list:
+        """pgrt_timeline_read: the launch records collected so far (and clears them), as dicts with
+        us_start / us_end in microseconds of the device clock."""
+        out = []
+        arr = (abi.TimelineRec * 4096)()
+        while True:
+            n = C.c_int(0)
+            _check(self.h, self.L.pgrt_timeline_read(self.h, arr, 4096, C.byref(n)))
+            for i in range(n.value):
+                r = arr[i]
+                out.append({"ticket": int(r.ticket), "slot": r.slot, "kind": abi.TIMELINE_KINDS[r.kind]
+                            if 0 <= r.kind < len(abi.TIMELINE_KINDS) else str(r.kind), "level": r.level,
+                            "waves": r.waves, "start": int(r.start), "end": int(r.end),
+                            "us_start": r.start / 100.0, "us_end": r.end / 100.0})
+            if n.value < 4096:
+                return out
 
     def frame_diag(self) -> list:
         """Per-level counters of the last frame (traversal counts need params.profile == 2)."""

@@ -351,20 +351,17 @@ def test_multi_device_context_equals_render(gpu_ctx, avenger_scene, ranks):
         g.close()
 
 
-@pytest.mark.parametrize("builder,width,split,group,layout", [
-    (abi.PGRT_BVH_LBVH, 2, 0.0, -1, 0), (abi.PGRT_BVH_PLOC, 8, 0.0, -1, 0), (abi.PGRT_BVH_LBVH, 8, 0.0, -1, 0),
-    (abi.PGRT_BVH_PLOC, 2, 0.0, -1, 0), (abi.PGRT_BVH_PLOC, 2, 1.0, -1, 0), (abi.PGRT_BVH_PLOC, 8, 0.5, -1, 0),
-    (abi.PGRT_BVH_PLOC, 2, 0.0, 1 << 30, 0), (abi.PGRT_BVH_LBVH, 2, 0.5, 1 << 30, 0),
-    (abi.PGRT_BVH_PLOC, 2, 0.5, 1 << 30, 0), (abi.PGRT_BVH_PLOC, 2, 0.0, -1, 1), (abi.PGRT_BVH_LBVH, 2, 0.0, -1, 1),
-    (abi.PGRT_BVH_PLOC, 2, 0.5, 1 << 30, 1), (abi.PGRT_BVH_PLOC, 8, 0.0, 1 << 30, 1)])
-def test_bvh_layouts_bit_exact(gpu_ctx, avenger_scene, builder, width, split, group, layout):
+@pytest.mark.parametrize("builder,width,split,group", [
+    (abi.PGRT_BVH_LBVH, 2, 0.0, -1), (abi.PGRT_BVH_PLOC, 8, 0.0, -1), (abi.PGRT_BVH_LBVH, 8, 0.0, -1),
+    (abi.PGRT_BVH_PLOC, 2, 0.0, -1), (abi.PGRT_BVH_PLOC, 2, 1.0, -1), (abi.PGRT_BVH_PLOC, 8, 0.5, -1),
+    (abi.PGRT_BVH_PLOC, 2, 0.0, 1 << 30), (abi.PGRT_BVH_LBVH, 2, 0.5, 1 << 30),
+    (abi.PGRT_BVH_PLOC, 2, 0.5, 1 << 30), (abi.PGRT_BVH_PLOC, 8, 0.0, 1 << 30)])
+def test_bvh_layouts_bit_exact(gpu_ctx, avenger_scene, builder, width, split, group):
     """Every BVH builder / traversal layout / split budget (pgrt_config) gives the same closest
     hits and frames: the hit is order-independent (ties to the smaller triangle index,
     conservative box tests), and split references cover their triangle.  group: queues up to it
-    take 8 (4) lanes per ray over the 8-wide BVH (-1 never).  layout: binary nodes in the
-    builder's order (0, the default) or as sibling pairs in depth-first order (1)."""
-    old = gpu_ctx.configure(bvh_builder=builder, bvh_width=width, split_beta=split, group_max=group,
-                            bvh_layout=layout)
+    take 8 (4) lanes per ray over the 8-wide BVH (-1 never)."""
+    old = gpu_ctx.configure(bvh_builder=builder, bvh_width=width, split_beta=split, group_max=group)
     try:
         gpu_ctx.set_scene(avenger_scene)
         info = gpu_ctx.bvh_info()
@@ -390,15 +387,13 @@ def test_bvh_layouts_bit_exact(gpu_ctx, avenger_scene, builder, width, split, gr
         gpu_ctx.set_scene(avenger_scene)
 
 
-@pytest.mark.parametrize("packets,binning", [(abi.PGRT_PACKETS_OFF, 0), (1, 0), (abi.PGRT_PACKETS_AUTO, 0), (16, 0),
-                                             (abi.PGRT_PACKETS_AUTO, 1), (16, 1)])
-def test_packet_levels_bit_exact(gpu_ctx, avenger_scene, packets, binning):
+@pytest.mark.parametrize("packets", [abi.PGRT_PACKETS_OFF, 1, abi.PGRT_PACKETS_AUTO, 16])
+def test_packet_levels_bit_exact(gpu_ctx, avenger_scene, packets):
     """Every packet-traversal depth (none: k_raygen + one lane per ray; level 0 only, which
-    generates its rays in the traversal; the default; every level), with and without the
-    direction-octant binning of the packet-traced bounce levels (ray_binning 1), renders the
-    oracle's frame bit for bit, frames in flight and batched frames included."""
+    generates its rays in the traversal; the default; every level) renders the oracle's frame bit
+    for bit, frames in flight and batched frames included."""
     gpu_ctx.set_scene(avenger_scene)
-    old = gpu_ctx.configure(packet_levels=packets, ray_binning=binning)
+    old = gpu_ctx.configure(packet_levels=packets)
     try:
         W, H = 96, 64
         cam = abi.default_camera(W, H)
@@ -453,44 +448,20 @@ def test_packet_budget_deferral_bit_exact(gpu_ctx, avenger_scene, budget):
         gpu_ctx.set_config(old)
 
 
-@pytest.mark.parametrize("budget", [-1, 8, 0])
-def test_wide_packets_bit_exact(gpu_ctx, avenger_scene, geosphere_scene, budget):
-    """Bounce-level packets over the 8-wide BVH (pgrt_config.packet_width 8): one quantized node
-    per packet step, every lane testing all 8 child boxes; without a budget, with a tiny one
-    (nearly every wave resumed by the 8-lanes-per-ray kernel) and the default.  Packets on every
-    level, the avenger proxy (pinhole and DoF, 1 and 4 samples) and the all-glass geosphere
-    (TIR, deep trees), oracle bit for bit."""
-    old = gpu_ctx.configure(packet_levels=16, packet_budget=budget, packet_width=8)
+@pytest.mark.parametrize("sub,packets", [(1, abi.PGRT_PACKETS_AUTO), (2, abi.PGRT_PACKETS_AUTO), (3, 16),
+                                         (5, abi.PGRT_PACKETS_OFF), (7, abi.PGRT_PACKETS_AUTO)])
+def test_subtree_levels_bit_exact(gpu_ctx, avenger_scene, geosphere_scene, sub, packets):
+    """Levels >= sub as whole ray trees in one launch (subtree.hip: reflection, refraction and shadow
+    rays of each level-sub ray traced and shaded depth first, as the reference's recursive trace
+    does): the avenger at d = 5 / 7 (pinhole, DoF samples), the all-glass geosphere at d = 8 (total
+    internal reflection chains), batched frames in flight -- oracle bit for bit, and the same ray
+    counts per kind."""
+    old = gpu_ctx.configure(subtree_level=sub, packet_levels=packets)
     try:
-        for sc, cam in ((avenger_scene, abi.default_camera(96, 64)),
-                        (geosphere_scene, abi.make_camera(64, 48, abi.deg2rad(90.0), (2.0, 0.0, 0.0), (0.0, 0.0, 0.0)))):
-            gpu_ctx.set_scene(sc)
-            gpu_ctx.set_camera(cam)
-            for p in (abi.make_params(spp_side=1, max_level=5),
-                      abi.make_params(spp_side=2, max_level=7, dof=1, jitter=abi.PGRT_JITTER_HASH, frame=5)):
-                img, st = gpu_ctx.render(p)
-                ref, sto = _oracle(sc).render(cam, p)
-                _, exact = assert_frames_match(img, ref)
-                assert exact == 1.0
-                assert (st.rays_primary, st.rays_shadow, st.rays_reflect, st.rays_refract) == \
-                    (sto.rays_primary, sto.rays_shadow, sto.rays_reflect, sto.rays_refract)
-    finally:
-        gpu_ctx.set_config(old)
-
-
-@pytest.mark.parametrize("tail,packets", [(1, 1), (2, abi.PGRT_PACKETS_AUTO), (3, 16), (5, 1), (0, abi.PGRT_PACKETS_AUTO)])
-def test_persistent_tail_bit_exact(gpu_ctx, avenger_scene, geosphere_scene, tail, packets):
-    """The deep levels as one persistent launch (tail.hip: children handed to the next level through
-    write-through granules, levels overlapping): every start level, with packets before it or not,
-    renders the oracle's frames bit for bit -- the avenger at d = 7 (pinhole and DoF samples), the
-    all-glass geosphere at d = 8 (total internal reflection, long glass chains), batched frames in
-    flight -- and counts the same rays per kind."""
-    old = gpu_ctx.configure(tail_level=tail, packet_levels=packets)
-    try:
-        for scene, cfgs in ((avenger_scene, (dict(spp_side=1, max_level=7),
+        for scene, cfgs in ((avenger_scene, (dict(spp_side=1, max_level=5), dict(spp_side=1, max_level=7),
                                              dict(spp_side=2, max_level=7, dof=1, jitter=abi.PGRT_JITTER_HASH,
                                                   frame=2))),
-                             (geosphere_scene, (dict(spp_side=2, max_level=8, jitter=abi.PGRT_JITTER_HASH),))):
+                            (geosphere_scene, (dict(spp_side=2, max_level=8, jitter=abi.PGRT_JITTER_HASH),))):
             gpu_ctx.set_scene(scene)
             W, H = 96, 64
             cam = (abi.default_camera(W, H) if scene is avenger_scene else
@@ -501,9 +472,9 @@ def test_persistent_tail_bit_exact(gpu_ctx, avenger_scene, geosphere_scene, tail
                 img, st = gpu_ctx.render(p)
                 ref, sto = _oracle(scene).render(cam, p)
                 _, exact = assert_frames_match(img, ref)
-                assert exact == 1.0
+                assert exact == 1.0, f"{c}"
                 assert (st.rays_primary, st.rays_shadow, st.rays_reflect, st.rays_refract) == \
-                    (sto.rays_primary, sto.rays_shadow, sto.rays_reflect, sto.rays_refract)
+                    (sto.rays_primary, sto.rays_shadow, sto.rays_reflect, sto.rays_refract), f"{c}"
         gpu_ctx.set_scene(avenger_scene)
         cam = abi.default_camera(96, 64)
         gpu_ctx.set_camera(cam)
@@ -799,44 +770,3 @@ def test_frames_in_flight_match_synchronous(gpu_ctx, avenger_scene):
         gpu_ctx.set_frames_in_flight(1)
         for b in bufs:
             gpu_ctx.free(b)
-
-
-_REFILL_CHILD = r"""
-import os, sys
-import numpy as np
-root = sys.argv[1]
-sys.path[:0] = [root, os.path.join(root, "oracle"), os.path.join(root, "tools")]
-import pyoracle, scenes
-from pgi_raytracing_amd import abi
-from pgi_raytracing_amd.raytracer import Context, load_obj
-scene = load_obj(scenes.AVENGER_OBJ)
-scene.set_environment(os.path.join(root, "assets", "spherical_map_windows.jpg"))
-ctx = Context(0)
-ctx.set_scene(scene)
-ctx.configure(packet_levels=abi.PGRT_PACKETS_OFF, group_max=-1)
-cam = abi.default_camera(96, 64)
-ctx.set_camera(cam)
-oracle = pyoracle.OracleScene(scene, accel=1)
-for p in (abi.make_params(spp_side=1, max_level=5),
-          abi.make_params(spp_side=2, max_level=5, dof=1, jitter=abi.PGRT_JITTER_HASH, frame=3)):
-    img, _ = ctx.render(p)
-    ref, _ = oracle.render(cam, p)
-    same = (img == ref) | (np.isnan(img) & np.isnan(ref))
-    assert same.all(), f"{(~same).sum()} values differ"
-print("refill ok")
-"""
-
-
-def test_lane_refill_bit_exact(avenger_obj):
-    """The opt-in lane-refill one-lane kernel (k_trace_rf; PGRT_REFILL is read once per process,
-    so a child process renders with it on): every level one lane per ray (packets off, no 8-lane
-    groups) and the shadow queue, bit for bit against the oracle (profiles/r3/ab_r3ba_lane_refill.txt)."""
-    import os
-    import subprocess
-    import sys
-
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, PGRT_REFILL="16")
-    r = subprocess.run([sys.executable, "-c", _REFILL_CHILD, root], env=env, capture_output=True, text=True,
-                       timeout=240)
-    assert r.returncode == 0 and "refill ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

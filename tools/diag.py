@@ -27,7 +27,7 @@ def main():
         if not os.environ.get("DIAG_NOENV"):
             sc.set_environment(env)
     ctx = Context(0)
-    for kv in filter(None, os.environ.get("DIAG_CFG", "").split(",")):  # e.g. DIAG_CFG=ray_binning=-1
+    for kv in filter(None, os.environ.get("DIAG_CFG", "").split(",")):  # e.g. DIAG_CFG=packet_budget=-1
         k, v = kv.split("=", 1)
         ctx.configure(**{k: float(v) if "." in v else int(v)})
     t = time.time()

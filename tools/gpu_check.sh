@@ -35,6 +35,9 @@ for s in "$@"; do
         bench_ident) step bench_ident 300 python bench.py --steps 20 --warmup 5 --frames identical --no-cpu-baseline ;;
         bench_long) step bench_long 300 python bench.py --no-cpu-baseline ;;
         bench_long_ident) step bench_long_ident 300 python bench.py --no-cpu-baseline --frames identical ;;
+        # device-stamped launch timeline: one synchronous frame and the driver's 20-frame region
+        timeline) step timeline 300 python tools/frame_timeline.py --out gpurun_out/timeline.json ;;
+        bench_nocpu) step bench_nocpu 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done

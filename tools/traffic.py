@@ -31,6 +31,47 @@ def per_dispatch(path, counter):
     return vals, names
 
 
+def frame_calls(names, calls=5):
+    """Dispatch ids of the bench's profile=1 roofline calls: every call ends with ONE
+    k_export_counters per pipeline slot (one slot with frames in flight); --roofline-only runs
+    warm-up calls, `calls` profile=1 calls, then one profile=2 (instrumented) call -- the segments
+    before the last one, the last `calls` of them."""
+    ids = sorted(names, key=lambda d: int(d))
+    segs, cur = [], []
+    for d in ids:
+        cur.append(d)
+        if "k_export_counters" in names[d]:
+            segs.append(cur)
+            cur = []
+    return segs[-1 - calls:-1] if len(segs) > calls else []
+
+
+def frame_bytes(fetch, fn, write, wn, frames_per_call, calls=5):
+    """Whole-frame DRAM bytes (every kernel of a call: traces, shades, combines, finish, counter
+    export) per frame, from the profile=1 calls; the per-kind split too."""
+    fsegs, wsegs = frame_calls(fn, calls), frame_calls(wn, calls)
+    if not fsegs or not wsegs:
+        return None
+    kind = lambda n: n.split("(")[0].split("<")[0].replace("void pgrt::", "").strip()
+    by = collections.defaultdict(float)
+    tot_f = sum(fetch[d] for s in fsegs for d in s)
+    tot_w = sum(write[d] for s in wsegs for d in s)
+    for s in fsegs:
+        for d in s:
+            by[kind(fn[d])] += 2 * fetch[d]
+    for s in wsegs:
+        for d in s:
+            by[kind(wn[d])] += write[d]
+    frames = frames_per_call * len(fsegs)
+    return {
+        "bytes_per_frame": int(round((2 * tot_f / len(fsegs) + tot_w / len(wsegs)) * 1024 / frames_per_call)),
+        "fetch_bytes_per_frame": int(round(2 * tot_f * 1024 / frames)),
+        "write_bytes_per_frame": int(round(tot_w * 1024 * len(fsegs) / len(wsegs) / frames)),
+        "calls": len(fsegs), "frames_per_call": frames_per_call,
+        "by_kernel_bytes_per_frame": {k: int(round(v * 1024 / frames)) for k, v in sorted(by.items(), key=lambda x: -x[1])},
+    }
+
+
 def main():
     root, out, rnd = sys.argv[1], sys.argv[2], sys.argv[3]
     workload = sys.argv[4] if len(sys.argv) > 4 else "C2 avenger-proxy 1920x1080 Whitted d=5 (bench.py default)"
@@ -79,6 +120,12 @@ def main():
         res["valu_issue_note"] = ("frac = SQ_INSTS_VALU x 2 cyc / (1024 SIMDs x GRBM_GUI_ACTIVE / 8): the fraction of "
                                   "the chip's VALU issue slots the launch used (1.0 = every SIMD issuing a wave64 "
                                   "VALU instruction every 2 cycles)")
+    fpc = int(os.environ.get("FRAMES_PER_CALL", "8"))
+    fr = frame_bytes(fetch, fn, write, wn, fpc)
+    if fr:
+        res["frame"] = fr
+        res["frame_note"] = ("every kernel of the profile=1 roofline calls (FETCH_SIZE x2 + WRITE_SIZE), per frame; "
+                             "calls delimited by their k_export_counters dispatch")
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))
