@@ -19,25 +19,35 @@
 #ifndef PGRT_STREAM_CACHE
 #define PGRT_STREAM_CACHE 1
 #endif
+#ifndef PGRT_STREAM_ST
+#define PGRT_STREAM_ST PGRT_STREAM_CACHE
+#endif
+#ifndef PGRT_STREAM_LD
+#define PGRT_STREAM_LD PGRT_STREAM_CACHE
+#endif
 
 namespace pgrt {
 
 typedef float pg_f4 __attribute__((ext_vector_type(4)));
 typedef int pg_i4 __attribute__((ext_vector_type(4)));
 
-// write-once 16-B records: write-through, the line leaves the XCD's L2
+// write-once 16-B records: write-through, the line leaves the XCD's L2.  The store is inline asm
+// (no builtin carries sc1 on a plain global store), so the compiler's hazard recognizer does not
+// see it: a VALU write of its data VGPRs right after it (the VMEM store-data hazard of stores
+// wider than 8 bytes, 1 wait state on gfx9+) would change the stored value -- the asm carries its
+// own s_nop.
 __device__ __forceinline__ void st_stream(float4* p, float4 v) {
-#if PGRT_STREAM_CACHE
+#if PGRT_STREAM_ST
     const pg_f4 w = {v.x, v.y, v.z, v.w};
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(w));
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(w));
 #else
     *p = v;
 #endif
 }
 __device__ __forceinline__ void st_stream(int4* p, int4 v) {
-#if PGRT_STREAM_CACHE
+#if PGRT_STREAM_ST
     const pg_i4 w = {v.x, v.y, v.z, v.w};
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(w));
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(w));
 #else
     *p = v;
 #endif
@@ -45,7 +55,7 @@ __device__ __forceinline__ void st_stream(int4* p, int4 v) {
 // narrow write-once values: nontemporal
 template <class T>
 __device__ __forceinline__ void st_stream_nt(T* p, T v) {
-#if PGRT_STREAM_CACHE
+#if PGRT_STREAM_ST
     __builtin_nontemporal_store(v, p);
 #else
     *p = v;
@@ -53,7 +63,7 @@ __device__ __forceinline__ void st_stream_nt(T* p, T v) {
 }
 // read-once streaming inputs: nontemporal loads
 __device__ __forceinline__ float4 ld_stream(const float4* p) {
-#if PGRT_STREAM_CACHE
+#if PGRT_STREAM_LD
     const pg_f4 v = __builtin_nontemporal_load(reinterpret_cast<const pg_f4*>(p));
     return make_float4(v.x, v.y, v.z, v.w);
 #else
@@ -61,7 +71,7 @@ __device__ __forceinline__ float4 ld_stream(const float4* p) {
 #endif
 }
 __device__ __forceinline__ int4 ld_stream(const int4* p) {
-#if PGRT_STREAM_CACHE
+#if PGRT_STREAM_LD
     const pg_i4 v = __builtin_nontemporal_load(reinterpret_cast<const pg_i4*>(p));
     return make_int4(v.x, v.y, v.z, v.w);
 #else
@@ -70,7 +80,7 @@ __device__ __forceinline__ int4 ld_stream(const int4* p) {
 }
 template <class T>
 __device__ __forceinline__ T ld_stream_nt(const T* p) {
-#if PGRT_STREAM_CACHE
+#if PGRT_STREAM_LD
     return __builtin_nontemporal_load(p);
 #else
     return *p;

@@ -497,6 +497,25 @@ def test_subtree_levels_bit_exact(gpu_ctx, avenger_scene, geosphere_scene, sub, 
         gpu_ctx.set_scene(avenger_scene)
 
 
+def test_auto_probe_frames_unchanged(gpu_ctx, avenger_scene):
+    """PGRT_PACKETS_AUTO re-probes a level that is off packets every 32 collected calls with a side
+    packet launch over the level's first rays (hit records discarded): 70 calls of the same frame
+    (several probes) stay bit-identical to the oracle."""
+    gpu_ctx.set_scene(avenger_scene)  # AUTO starts over per scene
+    old = gpu_ctx.configure(packet_levels=abi.PGRT_PACKETS_AUTO)
+    try:
+        cam = abi.default_camera(80, 48)
+        gpu_ctx.set_camera(cam)
+        p = abi.make_params(spp_side=1, max_level=6, jitter=abi.PGRT_JITTER_HASH, frame=4)
+        ref, _ = _oracle(avenger_scene).render(cam, p)
+        for k in range(70):
+            img, _ = gpu_ctx.render(p)
+            _, exact = assert_frames_match(img, ref)
+            assert exact == 1.0, f"call {k}"
+    finally:
+        gpu_ctx.set_config(old)
+
+
 @pytest.mark.parametrize("octant", range(8))
 def test_packet_sign_octants_bit_exact(gpu_ctx, avenger_scene, octant):
     """The packet kernel runs one of 8 node loops per direction-sign combination (near / far
