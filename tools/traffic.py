@@ -79,7 +79,10 @@ def main():
     write, wn = per_dispatch(os.path.join(root, "pmc_write"), "WRITE_SIZE")
 
     def trace_ids(names):  # the uninstrumented closest-hit launches (COUNT=false variants)
-        return [d for d, n in names.items() if "k_trace" in n and "<true" not in n]
+        # (k_subtree: the deep levels' closest hits + their shading in one launch, timed by
+        # bench.py as a closest-hit launch; its <int, bool, false> variants are uninstrumented)
+        return [d for d, n in names.items() if ("k_trace" in n and "<true" not in n)
+                or ("k_subtree" in n and n.split("(")[0].rstrip().endswith("false>"))]
 
     # a budgeted bounce-level packet launch is followed by k_trace8g<..., RESUME = true> over its
     # deferred rays: bench.py times the pair as ONE closest-hit launch (launch_trace), so their
