@@ -451,6 +451,8 @@ typedef struct pgrt_timeline_rec {
     int level;           /* queue level, -1 = none */
     int waves;           /* waves that stamped */
     uint64_t start, end; /* device wall clock ticks (100 MHz): first wave in, last wave out */
+    uint32_t wave_p50, wave_p90, wave_max; /* wave durations (ticks): median, 90th percentile, longest */
+    uint32_t last_in;    /* ticks from start to the last wave's entry (launch fill / tail split) */
 } pgrt_timeline_rec;
 int pgrt_timeline_enable(pgrt_ctx* ctx, int on);
 int pgrt_timeline_read(pgrt_ctx* ctx, pgrt_timeline_rec* out, int max, int* n);

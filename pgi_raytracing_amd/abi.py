@@ -187,6 +187,10 @@ class TimelineRec(C.Structure):
         ("waves", C.c_int),
         ("start", C.c_uint64),
         ("end", C.c_uint64),
+        ("wave_p50", C.c_uint32),
+        ("wave_p90", C.c_uint32),
+        ("wave_max", C.c_uint32),
+        ("last_in", C.c_uint32),
     ]
 
 

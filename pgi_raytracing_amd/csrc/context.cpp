@@ -1284,18 +1284,30 @@ void frame_stats(pgrt_ctx* ctx, FrameSet* fs, int retries) {
         PGRT_HIP(hipMemcpyAsync(ctx->stamp_host.data(), fs->stamps.p, (size_t)fs->stamp_used * 16,
                                 hipMemcpyDeviceToHost, s0));
         PGRT_HIP(hipStreamSynchronize(s0));
+        std::vector<uint32_t> dur;
         for (const StampLaunch& l : fs->stamp_launches) {
-            unsigned long long a = ~0ull, b = 0;
-            int waves = 0;
+            unsigned long long a = ~0ull, b = 0, last = 0;
+            dur.clear();
             for (long long w = l.offset; w < l.offset + l.waves; ++w) {
                 const unsigned long long t0 = ctx->stamp_host[2 * w], t1 = ctx->stamp_host[2 * w + 1];
                 if (t0 == 0 || t1 < t0) continue;  // not a stamp of this launch
                 a = std::min(a, t0);
                 b = std::max(b, t1);
-                ++waves;
+                last = std::max(last, t0);
+                dur.push_back((uint32_t)std::min<unsigned long long>(t1 - t0, 0xffffffffull));
             }
-            if (!waves) continue;
-            ctx->timeline.push_back(pgrt_timeline_rec{fs->ticket, l.slot, l.kind, l.level, waves, a, b});
+            if (dur.empty()) continue;
+            auto pct = [&](size_t q) {  // q-th percentile of the wave durations
+                const size_t k = std::min(dur.size() - 1, dur.size() * q / 100);
+                std::nth_element(dur.begin(), dur.begin() + k, dur.end());
+                return dur[k];
+            };
+            pgrt_timeline_rec r{fs->ticket, l.slot, l.kind, l.level, (int)dur.size(), a, b, 0, 0, 0, 0};
+            r.wave_p50 = pct(50);
+            r.wave_p90 = pct(90);
+            r.wave_max = *std::max_element(dur.begin(), dur.end());
+            r.last_in = (uint32_t)(last - a);
+            ctx->timeline.push_back(r);
         }
         fs->stamp_used = 0;
     }

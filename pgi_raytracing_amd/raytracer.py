@@ -289,7 +289,9 @@ class Context:
                 out.append({"ticket": int(r.ticket), "slot": r.slot, "kind": abi.TIMELINE_KINDS[r.kind]
                             if 0 <= r.kind < len(abi.TIMELINE_KINDS) else str(r.kind), "level": r.level,
                             "waves": r.waves, "start": int(r.start), "end": int(r.end),
-                            "us_start": r.start / 100.0, "us_end": r.end / 100.0})
+                            "us_start": r.start / 100.0, "us_end": r.end / 100.0,
+                            "wave_us": (r.wave_p50 / 100.0, r.wave_p90 / 100.0, r.wave_max / 100.0),
+                            "last_in_us": r.last_in / 100.0})
             if n.value < 4096:
                 return out
 

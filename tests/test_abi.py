@@ -222,3 +222,41 @@ def test_loader_missing_file_reports_error():
 
     with pytest.raises(PgrtError):
         load_obj("/nonexistent/file.obj")
+
+
+# ctypes mirror <-> C header: every struct the Python host passes across the boundary must have
+# the header's size and field offsets (a drifted field silently shifts everything after it)
+_STRUCTS = {
+    "Material": "pgrt_material", "Texture": "pgrt_texture", "Light": "pgrt_light",
+    "SceneDesc": "pgrt_scene_desc", "Camera": "pgrt_camera", "RenderParams": "pgrt_render_params",
+    "Config": "pgrt_config", "Stats": "pgrt_stats", "LevelDiag": "pgrt_level_diag",
+    "TimelineRec": "pgrt_timeline_rec", "BvhInfo": "pgrt_bvh_info",
+}
+
+
+# ctypes names that differ from the header's (a Python keyword; an array spelled out field by field)
+_C_NAME = {("Camera", "from_"): "from", **{("LevelDiag", n): f"longest_ray[{i}]" for i, n in enumerate(
+    ("lr_visits", "lr_tests", "lr_leaves", "lr_node_cyc64", "lr_leaf_cyc64", "lr_load_cyc64"))}}
+
+
+def test_ctypes_structs_match_header(tmp_path):
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("no C compiler")
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "pgrt.h"', "int main(void) {"]
+    expect = []
+    for py, c in _STRUCTS.items():
+        cls = getattr(abi, py)
+        lines.append(f'printf("{py} %zu\\n", sizeof({c}));')
+        expect.append(f"{py} {C.sizeof(cls)}")
+        for name, *_ in cls._fields_:
+            lines.append(f'printf("{py}.{name} %zu\\n", offsetof({c}, {_C_NAME.get((py, name), name)}));')
+            expect.append(f"{py}.{name} {getattr(cls, name).offset}")
+    lines += ["return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    assert [g for g in got if g] == expect

@@ -516,6 +516,38 @@ def test_auto_probe_frames_unchanged(gpu_ctx, avenger_scene):
         gpu_ctx.set_config(old)
 
 
+def test_timeline_records_and_frames_unchanged(gpu_ctx, avenger_scene):
+    """pgrt_timeline_enable: a stamped frame is the oracle's frame bit for bit, every launch of it
+    leaves one record (wave-ordered spans on the device clock, percentiles within the span), and
+    reading removes the records."""
+    gpu_ctx.set_scene(avenger_scene)
+    cam = abi.default_camera(96, 64)
+    gpu_ctx.set_camera(cam)
+    p = abi.make_params(spp_side=1, max_level=5, jitter=abi.PGRT_JITTER_HASH, frame=2)
+    ref, _ = _oracle(avenger_scene).render(cam, p)
+    gpu_ctx.timeline_enable(True)
+    try:
+        img, _ = gpu_ctx.render(p)
+        recs = gpu_ctx.timeline_read()
+    finally:
+        gpu_ctx.timeline_enable(False)
+    _, exact = assert_frames_match(img, ref)
+    assert exact == 1.0
+    kinds = {r["kind"] for r in recs}
+    assert {"shade", "finish", "export"} <= kinds, kinds
+    assert any(r["kind"].startswith("trace") and r["level"] == 0 for r in recs)
+    for r in recs:
+        span = r["end"] - r["start"]
+        assert r["waves"] > 0 and span >= 0
+        p50, p90, mx = r["wave_us"]
+        assert p50 <= p90 <= mx <= span / 100.0 + 1e-6
+        assert 0 <= r["last_in_us"] <= span / 100.0 + 1e-6
+    assert gpu_ctx.timeline_read() == []
+    img2, _ = gpu_ctx.render(p)  # off again: no records
+    assert gpu_ctx.timeline_read() == []
+    assert np.array_equal(img2, img)
+
+
 @pytest.mark.parametrize("octant", range(8))
 def test_packet_sign_octants_bit_exact(gpu_ctx, avenger_scene, octant):
     """The packet kernel runs one of 8 node loops per direction-sign combination (near / far

@@ -33,6 +33,7 @@ W, H, D = 1920, 1080, 5
 
 def rel(recs, t0):
     return [dict(kind=r["kind"], level=r["level"], slot=r["slot"], ticket=r["ticket"], waves=r["waves"],
+                 wave_us=r["wave_us"], last_in_us=r["last_in_us"],
                  start_us=round(r["us_start"] - t0, 2), end_us=round(r["us_end"] - t0, 2),
                  dur_us=round(r["us_end"] - r["us_start"], 2)) for r in sorted(recs, key=lambda r: r["start"])]
 
@@ -155,7 +156,8 @@ def main():
         print(k, json.dumps({kk: vv for kk, vv in v.items() if kk != "launches"}))
         for r in v["launches"]:
             print(f"   {r['start_us']:9.1f} {r['end_us']:9.1f} {r['dur_us']:8.1f}  t{r['ticket']} s{r['slot']} "
-                  f"{r['kind']:<13} L{r['level']:<3} waves {r['waves']}")
+                  f"{r['kind']:<13} L{r['level']:<3} waves {r['waves']:6d}  wave p50/p90/max "
+                  f"{r['wave_us'][0]:6.1f} {r['wave_us'][1]:6.1f} {r['wave_us'][2]:6.1f}  last in {r['last_in_us']:6.1f}")
 
 
 if __name__ == "__main__":
