@@ -2,7 +2,7 @@
 # r4b: parity (the subtree launch included), then same-box A/B: r3 head / the pruned library without
 # the streaming cache policy / with it (default), device timelines, the driver's line per subtree level
 set -u
-cd "$(dirname "$0")/.."
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_r4b.log 2>&1

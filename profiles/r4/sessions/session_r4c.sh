@@ -2,7 +2,7 @@
 # r4c: where does the r3-head -> r4 C2 regression come from: same-box A/B with the stamps compiled
 # out, then per-kernel rocprofv3 stats of the driver's line for r3 head and the r4 library
 set -u
-cd "$(dirname "$0")/.."
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 bash tools/ab_pair.sh r4c ablib/r3head/libpgrt.so ablib/nostamp/libpgrt.so 3 || exit 1

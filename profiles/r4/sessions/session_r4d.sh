@@ -2,7 +2,7 @@
 # r4d: which change broke test_gpu_frames_equal_golden: the library variants on the golden and
 # frame-parity tests
 set -u
-cd "$(dirname "$0")/.."
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 for L in ablib/r3head/libpgrt.so ablib/nocache/libpgrt.so ablib/stonly/libpgrt.so ablib/ldonly/libpgrt.so base; do

@@ -2,7 +2,7 @@
 # r4e: stamps with a non-clobbering entry clock vs stamps compiled out (same box, interleaved),
 # then the device timeline of the fixed build
 set -u
-cd "$(dirname "$0")/.."
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 bash tools/ab_pair.sh r4e base ablib/nostamp/libpgrt.so 3 || exit 1

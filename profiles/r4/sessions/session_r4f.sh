@@ -2,7 +2,7 @@
 # r4f: GPU tests + smoke on the fixed-stamps build, the C2 profile passes (frame traffic),
 # timeline with wave percentiles, the driver's bench line
 set -u
-cd "$(dirname "$0")/.."
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 bash tools/gpu_check.sh tests smoke || exit 1

@@ -2,7 +2,7 @@
 # r4g: the L2 policy of the streaming data (cache_ops.hpp) on vs off, and early split clipping, on
 # the driver's line and the synchronous frame's device timeline
 set -u
-cd "$(dirname "$0")/.."
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 bash tools/ab_pair.sh r4g base ablib/nocache/libpgrt.so 3 || exit 1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # r4h: the synchronous frame's chain under speed-only configs: subtree levels, packet levels
 set -u
-cd "$(dirname "$0")/.."
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 tl() {  # name [args]

@@ -2,7 +2,7 @@
 # r4i: work donation between the 8-lane groups of a wave (trace8_donate): parity, then same-box
 # A/B against PGRT_DONATE=0 on the driver's line and the synchronous frame's timeline
 set -u
-cd "$(dirname "$0")/.."
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_r4i.log 2>&1; rc=$?
