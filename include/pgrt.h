@@ -197,14 +197,21 @@ typedef struct pgrt_config {
                              batches of scenes up to 262144 triangles, 256 otherwise), -1 = no budget */
     int subtree_level;    /* Whitted levels >= k evaluated as whole ray trees, one launch (every ray of
                              level k traces and shades its reflection / refraction / shadow rays
-                             depth first, as the reference's recursive trace does): 0 = default, -1 =
-                             one launch per level, k >= 1 = from level k */
+                             depth first, as the reference's recursive trace does): 0 = default
+                             (from level 3 for one-frame batches of scenes up to 262144 triangles,
+                             one launch per level otherwise), -1 = one launch per level, k >= 1 =
+                             from level k */
     int call_order;     /* frames in flight: 1 = each call's level-0 trace waits for the previous
                              call's level-0 shade (the bulk work of the calls in submission order,
                              their latency-bound deeper levels overlapping the next call's bulk);
                              -1 = calls share the GPU freely; 0 = default: ordered for scenes above
                              262144 triangles (C5 -7 %; the avenger's C2 / C3 lose when ordered,
                              profiles/r3/ab_r3ab_call_order.txt) */
+    int tile_order;     /* synchronous one-frame renders (two pipeline slots): 0 = default, the tiles
+                             whose primary rays hit a dielectric in the previous frame of the same
+                             size form the first slot, so the deep reflection / refraction levels
+                             (the frame's critical path) start after a short level 0 while the
+                             other slot's level 0 still runs; -1 = tiles dealt round-robin */
 } pgrt_config;
 
 /* ---- context ---- */

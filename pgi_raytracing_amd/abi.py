@@ -129,6 +129,7 @@ class Config(C.Structure):
         ("packet_budget", C.c_int),
         ("subtree_level", C.c_int),
         ("call_order", C.c_int),
+        ("tile_order", C.c_int),
     ]
 
 

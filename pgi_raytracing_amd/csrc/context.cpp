@@ -142,6 +142,10 @@ struct FrameSlot {
     int pinned_fc_n = 0;
     int4* pinned_tiles = nullptr;
     int pinned_tiles_n = 0;
+    // per-tile deep flags of a synchronous frame (FrameParams::tile_deep), zeroed by the export
+    DevBuf<int> tile_deep;
+    int* pinned_deep = nullptr;
+    int pinned_deep_n = 0;
     void ensure_pinned(int batches, int ntiles) {
         if (pinned_fc_n < batches) {
             if (pinned_fc) (void)hipHostFree(pinned_fc);
@@ -156,19 +160,38 @@ struct FrameSlot {
             pinned_tiles_n = ntiles;
         }
     }
+    // the deep flags of ntiles tiles: device copy zeroed once (the export kernel re-zeroes it)
+    void ensure_deep(int ntiles, hipStream_t s) {
+        if (pinned_deep_n < ntiles) {
+            if (pinned_deep) (void)hipHostFree(pinned_deep);
+            PGRT_HIP(hipHostMalloc((void**)&pinned_deep, sizeof(int) * ntiles,
+                                   hipHostMallocMapped | hipHostMallocCoherent));
+            pinned_deep_n = ntiles;
+        }
+        if (tile_deep.n < (size_t)ntiles) {
+            tile_deep.alloc(ntiles);
+            PGRT_HIP(hipMemsetAsync(tile_deep.p, 0, sizeof(int) * tile_deep.n, s));
+        }
+    }
     DevBuf<float4> accum;
     DevBuf<int> gstack;
     std::vector<int4> tiles_dev;  // host copy of the device tile list
     int expect_count[kMaxLevels] = {0};  // grid hints from the previous frame (0 = unknown)
     int expect_defer[kMaxLevels] = {0};
     int expect_shadow_total = 0;
-    FrameSlot() {
-        PGRT_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    // first: the frame's slot 0 -- the deep tiles of a synchronous frame (deal_tiles), whose chain
+    // of small latency-bound launches is the frame's critical path -- on a high-priority stream,
+    // so its launches take CUs before slot 1's level-0 blocks
+    explicit FrameSlot(bool first) {
+        int lo = 0, hi = 0;
+        PGRT_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        PGRT_HIP(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, first ? hi : lo));
         PGRT_HIP(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
     }
     ~FrameSlot() {
         if (pinned_fc) (void)hipHostFree(pinned_fc);
         if (pinned_tiles) (void)hipHostFree(pinned_tiles);
+        if (pinned_deep) (void)hipHostFree(pinned_deep);
         if (ev_done) (void)hipEventDestroy(ev_done);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -207,6 +230,7 @@ struct FrameSet {
     float* host_dst = nullptr;
     size_t host_bytes = 0;
     int cam_w = 0, cam_h = 0;  // image size at submission (the gather's layout)
+    bool deep_rec = false;     // the level-0 shades record deep tiles (FrameParams::tile_deep)
     pgrt_stats stats{};
     std::chrono::steady_clock::time_point t0;
     // distributed frames: device time of the gather (ncclGather, including the wait for the
@@ -276,6 +300,10 @@ struct pgrt_ctx {
     double packet_util[kMaxLevels] = {};  // last measured utilisation per level (0 = never measured)
     unsigned long long frames_collected = 0;
     int probe_level = -1;  // level traced as packets in the next frame to refresh its utilisation
+    // pgrt_config.tile_order: the image tiles (64x64 grid of a deep_w x deep_h frame) whose
+    // primary rays hit a dielectric in the last synchronous frame of that size
+    std::vector<unsigned char> deep_tiles;
+    int deep_w = 0, deep_h = 0;
     pgrt_bvh_info info{};
 
     CameraView cam{};
@@ -779,13 +807,48 @@ int group_max(const pgrt_ctx* ctx) {
     return ctx->frames_in_flight > 1 ? kDefaultGroupMaxInFlight : kDefaultGroupMax;
 }
 
+// The tiles of each pipeline slot.  Round-robin (slot j gets tiles j, j + K, ...; multi-frame
+// calls, tile-compact and distributed outputs rely on it: FrameParams::frame_tiles, store_pixel).
+// A synchronous one-frame render into a framebuffer records which tiles' primary rays hit a
+// dielectric (pgrt_config.tile_order) and, when the last frame of the same size had some, deals
+// those tiles to slot 0 and the rest to slot 1: the frame's critical path is the chain of deep
+// reflection / refraction levels (~20 dependent launches, each as long as its slowest ray), and
+// it then starts after a level 0 over the deep tiles only, while slot 1's level 0 -- most of the
+// pixels, no deep levels -- runs beside it.  Results do not depend on the deal (pixels are
+// independent), only the schedule does.
+std::vector<std::vector<int4>> deal_tiles(pgrt_ctx* ctx, FrameSet* fs, int K) {
+    const std::vector<int4>& tiles = fs->tiles;
+    std::vector<std::vector<int4>> deal(K);
+    fs->deep_rec = K == 2 && fs->nframes == 1 && fs->out_mode == 0 && !fs->distributed &&
+                   ctx->cfg.tile_order == 0 && fs->params.mode == PGRT_MODE_WHITTED && fs->params.max_level > 0;
+    if (fs->deep_rec && ctx->deep_w == fs->cam_w && ctx->deep_h == fs->cam_h && !ctx->deep_tiles.empty()) {
+        const int tx = (fs->cam_w + kTile - 1) / kTile;
+        for (const int4& t : tiles) {
+            const size_t id = (size_t)(t.y / kTile) * (size_t)tx + (size_t)(t.x / kTile);
+            const bool deep = t.x >= 0 && t.y >= 0 && id < ctx->deep_tiles.size() && ctx->deep_tiles[id] != 0;
+            deal[deep ? 0 : 1].push_back(t);
+        }
+        // no deep tiles, or most of the frame: the round-robin halves are the better split
+        if (!deal[0].empty() && 2 * deal[0].size() <= tiles.size()) return deal;
+        deal[0].clear();
+        deal[1].clear();
+    }
+    for (size_t t = 0; t < tiles.size(); ++t) deal[t % K].push_back(tiles[t]);
+    return deal;
+}
+
 // first level evaluated as whole ray trees in one launch (pgrt_config.subtree_level, subtree.hip),
 // -1 = one launch per level
-int subtree_first(const pgrt_ctx* ctx, const SceneView& view, const pgrt_render_params* p) {
+// Default: from level kSubtreeLevelSmall for one-frame batches of scenes up to kPacketBigScene
+// triangles (the synchronous frame: levels 3.. are a few ten thousand rays whose per-level
+// launches each last as long as their slowest ray; r4l timeline 0.583-0.597 -> 0.563 ms), one
+// launch per level otherwise (the subtree launch's 8 lanes per ray cost multi-frame calls
+// throughput: r4h driver line 0.179 -> 0.209 ms/frame).
+int subtree_first(const pgrt_ctx* ctx, const SceneView& view, const pgrt_render_params* p, bool small_batch) {
     const int k = ctx->cfg.subtree_level;
     if (k < 0 || p->mode != PGRT_MODE_WHITTED || !subtree_available(view)) return -1;
     if (k > 0) return k <= p->max_level ? k : -1;
-    return -1;
+    return small_batch && view.ntri <= kPacketBigScene && kSubtreeLevelSmall <= p->max_level ? kSubtreeLevelSmall : -1;
 }
 
 // step budget of the bounce levels' packet launches (pgrt_config.packet_budget)
@@ -945,7 +1008,8 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
     const bool fuse = packet_level(ctx, 0) && trace_packets_available(view);
     fs->K = K;
     fs->batches = 0;
-    while ((int)fs->slots.size() < K) fs->slots.emplace_back(new FrameSlot());
+    while ((int)fs->slots.size() < K) fs->slots.emplace_back(new FrameSlot(fs->slots.empty()));
+    const std::vector<std::vector<int4>> deal = deal_tiles(ctx, fs, K);
     // launch timeline (pgrt_timeline_enable): every launch of this call stamps its waves into
     // fs->stamps, the slot ranges handed out by the launchers through the stamp log
     StampLog slog;
@@ -982,7 +1046,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
         FrameSlot* sl = fs->slots[j].get();
         hipStream_t s = sl->stream;
         slog.slot = j;
-        const int nt = (ntiles - j + K - 1) / K;
+        const int nt = (int)deal[j].size();
         const long long npix = (long long)nt * kTile * kTile;
         const int nsb = (int)std::max(1ll, std::min<long long>(spp, max_batch / npix));
         PGRT_REQUIRE(npix * nsb < (1ll << 30), PGRT_ERR_INVALID_ARGUMENT,
@@ -997,7 +1061,8 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
         PGRT_HIP(hipStreamWaitEvent(s, fs->ev_ready, 0));
         // the pinned tile list may still feed this slot's previous upload
         PGRT_HIP(hipEventSynchronize(sl->ev_done));
-        for (int t = j, q = 0; t < ntiles; t += K, ++q) sl->pinned_tiles[q] = tiles[t];
+        std::copy(deal[j].begin(), deal[j].end(), sl->pinned_tiles);
+        if (fs->deep_rec) sl->ensure_deep(nt, s);
         // the device tile list is re-uploaded only when it changed
         if (sl->tiles_dev.size() != (size_t)nt || !std::equal(sl->tiles_dev.begin(), sl->tiles_dev.end(),
                                                                sl->pinned_tiles, [](const int4& a, const int4& b) {
@@ -1010,6 +1075,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
         FrameParams fp = fp0;
         fp.ntiles = nt;
         fp.slot = j;
+        fp.tile_deep = fs->deep_rec ? sl->tile_deep.p : nullptr;
         for (int bi = 0; bi < batches; ++bi) {
             const int s0 = bi * nsb;
             fp.s0 = s0;
@@ -1045,7 +1111,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             debug_sync(s, "raygen", 0, bi);
             ctx->timer.end(s, id);
             // levels >= sub: whole ray trees in one launch (no queues, shades or combines below it)
-            const int sub = subtree_first(ctx, view, p);
+            const int sub = subtree_first(ctx, view, p, n0 < kSmallPacketBatch);
             for (int L = 0; L < levels; ++L) {
                 Queue qc = q[L & 1], qn = q[(L + 1) & 1];
                 const int maxc = L == 0 ? n0 : std::min(sl->q_cap, sl->level_cap[L]);
@@ -1148,7 +1214,8 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
         }
         sl->host_fc.resize(batches);
         // the frame's counters to pinned host memory, zeroed on the device for the next frame
-        launch_export_counters(sl->fc.p, sl->pinned_fc, batches, s);
+        launch_export_counters(sl->fc.p, sl->pinned_fc, batches, fs->deep_rec ? sl->tile_deep.p : nullptr,
+                               sl->pinned_deep, nt, s);
         debug_sync(s, "export", 0, 0);
         PGRT_HIP(hipEventRecord(sl->ev_done, s));
     }
@@ -1173,6 +1240,21 @@ bool read_frame_counters(pgrt_ctx* ctx, FrameSet* fs) {
         std::copy(sl->pinned_fc, sl->pinned_fc + sl->host_fc.size(), sl->host_fc.begin());
     }
     PGRT_HIP(hipGetLastError());
+    if (fs->deep_rec) {  // pgrt_config.tile_order: the deep tiles of this frame for the next deal
+        const int tx = (fs->cam_w + kTile - 1) / kTile, ty = (fs->cam_h + kTile - 1) / kTile;
+        ctx->deep_tiles.assign((size_t)tx * ty, 0);
+        ctx->deep_w = fs->cam_w;
+        ctx->deep_h = fs->cam_h;
+        for (int j = 0; j < K; ++j) {
+            const FrameSlot* sl = fs->slots[j].get();
+            for (size_t q = 0; q < sl->tiles_dev.size() && (int)q < sl->pinned_deep_n; ++q) {
+                const int4 t = sl->tiles_dev[q];
+                const size_t id = (size_t)(t.y / kTile) * (size_t)tx + (size_t)(t.x / kTile);
+                if (t.x >= 0 && t.y >= 0 && id < ctx->deep_tiles.size() && sl->pinned_deep[q] != 0)
+                    ctx->deep_tiles[id] = 1;
+            }
+        }
+    }
     bool overflow = false;
     ctx->last_fc.clear();
     for (int j = 0; j < K; ++j) {
@@ -1925,6 +2007,8 @@ int pgrt_set_config(pgrt_ctx* ctx, const pgrt_config* cfg) {
         PGRT_REQUIRE(cfg->max_batches_in_flight >= 0, PGRT_ERR_INVALID_ARGUMENT, "max_batches_in_flight must be >= 0");
         PGRT_REQUIRE(cfg->packet_budget >= -1, PGRT_ERR_INVALID_ARGUMENT,
                      "packet_budget must be -1 (off), 0 (default) or a step count");
+        PGRT_REQUIRE(cfg->tile_order == 0 || cfg->tile_order == -1, PGRT_ERR_INVALID_ARGUMENT,
+                     "tile_order must be 0 (default: deep tiles first) or -1 (round-robin)");
         PGRT_REQUIRE(cfg->call_order == 0 || cfg->call_order == 1 || cfg->call_order == -1, PGRT_ERR_INVALID_ARGUMENT,
                      "call_order must be 0 (default), 1 (level 0 in submission order) or -1 (free)");
         PGRT_REQUIRE(cfg->rank0_share_a >= 0 && cfg->rank0_share_a <= 64 && cfg->rank0_share_b >= 0 &&

@@ -135,6 +135,10 @@ __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : 6) void k_shade
         }
         ShadeOut r;
         shade_eval(s, mats, lut255, level, fp.max_level, active, cur_o, cur_d, cur_t, cur_h, r);
+        if (level == 0 && fp.tile_deep) {  // a wave lies in one tile (4096 * nsb rays per tile)
+            const unsigned long long dm = __ballot(active && r.nchild > 0);
+            if (dm != 0ull && __lane_id() == 0) fp.tile_deep[(i / fp.nsb) / (kTile * kTile)] = 1;
+        }
         if (fp.count) {  // profile == 2 only: one atomic pair per wave (the whole-frame roofline)
             const bool hit = active && cur_d.w >= 0.0f && __float_as_int(cur_h.w) >= 0;
             const unsigned long long hm = __ballot(hit), tm = __ballot(hit && r.kind == 2 && mats[r.mid].tex >= 0);
@@ -425,21 +429,29 @@ void launch_accumulate_frame(const float* frame, float* sum, float* mean, long l
 // last launch of a slot's frame: the frame counters go to pinned host memory and the device
 // copy is zeroed for the next frame (replaces a D2H copy + a memset: two fewer queue operations
 // per frame)
-__global__ void k_export_counters(uint4* dev, uint4* host, int n16, unsigned long long* __restrict__ stamps) {
+__global__ void k_export_counters(uint4* dev, uint4* host, int n16, int* __restrict__ deep_dev,
+                                  int* __restrict__ deep_host, int ndeep, unsigned long long* __restrict__ stamps) {
     PGRT_STAMP_BEGIN(stamps);
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += gridDim.x * blockDim.x) {
         host[i] = dev[i];
         dev[i] = make_uint4(0u, 0u, 0u, 0u);
     }
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ndeep; i += gridDim.x * blockDim.x) {
+        deep_host[i] = deep_dev[i];
+        deep_dev[i] = 0;
+    }
     PGRT_STAMP_END(stamps);
 }
 
-void launch_export_counters(FrameCounters* dev, FrameCounters* host, int n, hipStream_t stream) {
+void launch_export_counters(FrameCounters* dev, FrameCounters* host, int n, int* deep_dev, int* deep_host, int ndeep,
+                            hipStream_t stream) {
     static_assert(sizeof(FrameCounters) % 16 == 0, "FrameCounters must be a multiple of 16 bytes");
     const int n16 = (int)(sizeof(FrameCounters) / 16) * n;
-    const int grid = std::min(64, (n16 + kBlock - 1) / kBlock);
+    if (!deep_dev || !deep_host) ndeep = 0;
+    const int grid = std::min(64, (std::max(n16, ndeep) + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_export_counters, dim3((unsigned)grid), dim3(kBlock), 0, stream, reinterpret_cast<uint4*>(dev),
-                       reinterpret_cast<uint4*>(host), n16, stamp_next(kStampExport, -1, grid, kBlock));
+                       reinterpret_cast<uint4*>(host), n16, deep_dev, deep_host, ndeep,
+                       stamp_next(kStampExport, -1, grid, kBlock));
 }
 
 // ------------------------------------------------------------------ math self-test

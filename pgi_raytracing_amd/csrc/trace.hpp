@@ -68,6 +68,10 @@ struct FrameParams {
     int slots, slot, frame_tiles, frame_out_tiles;  // frame_out_tiles: tiles per frame in a tile-compact output
     long long frame_stride;
     int count;  // profile == 2: the shade kernels count hits / textured hits (FrameCounters::shade)
+    // synchronous frames: the level-0 shade sets tile_deep[q] = 1 for the slot's tile q when a
+    // primary ray there hit a dielectric (reflection / refraction children) -- the next frame's
+    // tile deal (context.cpp deal_tiles); NULL: not recorded
+    int* tile_deep;
 };
 
 __host__ __device__ inline int frame_of_tile(const FrameParams& fp, int tile) {
@@ -217,7 +221,10 @@ bool subtree_available(const SceneView& s);
 void launch_subtree(const SceneView& s, const FrameParams& fp, int level, Queue q, LevelNodes nodes,
                     FrameCounters* fc, int max_count, int expect, bool count, hipStream_t stream);
 // copy `n` FrameCounters to pinned host memory and zero them on the device
-void launch_export_counters(FrameCounters* dev, FrameCounters* host, int n, hipStream_t stream);
+// also copies the slot's per-tile deep flags (FrameParams::tile_deep, ndeep ints) to deep_host and
+// zeroes them on the device (deep_dev NULL: none)
+void launch_export_counters(FrameCounters* dev, FrameCounters* host, int n, int* deep_dev, int* deep_host, int ndeep,
+                            hipStream_t stream);
 // Distributed frames: rank r's tile-compact buffer (frame-major, count[r] tiles per frame in its
 // local deal order); prefix = exclusive prefix of the counts (prefix[world] = all tiles)
 constexpr int kMaxRanks = 16;
@@ -261,6 +268,8 @@ constexpr int kDefaultPacketBudget = 256;
 // on their bounce levels (context.cpp packet_budget)
 constexpr int kSmallPacketBatch = 1 << 22;
 constexpr int kSmallBatchPacketBudget = 64;
+// one-frame batches: levels >= this as whole ray trees in one launch (pgrt_config.subtree_level)
+constexpr int kSubtreeLevelSmall = 3;
 // "big" scenes (BVH + triangles far beyond the L2, fetches served by the MALL / HBM): the
 // level-0 packet kernel is built for 8 waves (trace.hip), level 0 of calls in flight is ordered
 // (context.cpp call_ordered)

@@ -138,12 +138,18 @@ def test_avenger_frame_parity(gpu_ctx, avenger_scene, cfg):
     cam = abi.default_camera(128, 96)
     gpu_ctx.set_camera(cam)
     p = abi.make_params(**cfg)
-    img, st = gpu_ctx.render(p)
     ref, sto = _oracle(avenger_scene).render(cam, p)
-    diff, exact = assert_frames_match(img, ref)
-    assert exact == 1.0, f"max diff {diff}, exact fraction {exact}"
-    assert (st.rays_primary, st.rays_shadow, st.rays_reflect, st.rays_refract) == \
-        (sto.rays_primary, sto.rays_shadow, sto.rays_reflect, sto.rays_refract)
+    # default (one-frame batches: levels >= 3 as whole ray trees) and one launch per level
+    for sub in (0, -1):
+        old = gpu_ctx.configure(subtree_level=sub)
+        try:
+            img, st = gpu_ctx.render(p)
+        finally:
+            gpu_ctx.set_config(old)
+        diff, exact = assert_frames_match(img, ref)
+        assert exact == 1.0, f"subtree_level {sub}: max diff {diff}, exact fraction {exact}"
+        assert (st.rays_primary, st.rays_shadow, st.rays_reflect, st.rays_refract) == \
+            (sto.rays_primary, sto.rays_shadow, sto.rays_reflect, sto.rays_refract)
 
 
 @pytest.mark.parametrize("cfg", CONFIGS[1:3] + CONFIGS[4:5], ids=["d5", "d7", "S3d7dof"])
@@ -495,6 +501,37 @@ def test_subtree_levels_bit_exact(gpu_ctx, avenger_scene, geosphere_scene, sub, 
     finally:
         gpu_ctx.set_config(old)
         gpu_ctx.set_scene(avenger_scene)
+
+
+@pytest.mark.parametrize("order", [0, -1])
+def test_tile_order_bit_exact(gpu_ctx, avenger_scene, order):
+    """Synchronous frames after the first of a size deal the tiles whose primary rays hit a
+    dielectric in the previous frame to the first pipeline slot (pgrt_config.tile_order 0) or
+    round-robin (-1); a different camera makes the recorded tiles stale -- every frame equals the
+    oracle bit for bit, with the same ray counts per kind."""
+    old = gpu_ctx.configure(tile_order=order)
+    try:
+        W, H = 448, 320  # 7 x 5 tiles: the canopy covers some of them
+        for k, (pos, c) in enumerate((((0.0, 0.0, 0.0), dict(spp_side=1, max_level=5)),
+                                      ((0.0, 0.0, 0.0), dict(spp_side=1, max_level=5, jitter=abi.PGRT_JITTER_HASH,
+                                                             frame=4)),
+                                      ((0.0, 0.0, 0.0), dict(spp_side=2, max_level=4)),
+                                      ((30.0, -20.0, 10.0), dict(spp_side=1, max_level=6)))):
+            cam = abi.default_camera(W, H)
+            if k == 3:  # moved camera: the deal follows the last frame's tiles (stale, speed only)
+                cam = abi.make_camera(W, H, abi.deg2rad(42.185), (-140.0 + pos[0], -175.0 + pos[1], 80.0 + pos[2]),
+                                      (0.0, 0.0, 0.0))
+            gpu_ctx.set_camera(cam)
+            p = abi.make_params(**c)
+            for rep in range(2):
+                img, st = gpu_ctx.render(p)
+                ref, sto = _oracle(avenger_scene).render(cam, p)
+                _, exact = assert_frames_match(img, ref)
+                assert exact == 1.0, f"{c} rep {rep}"
+                assert (st.rays_primary, st.rays_shadow, st.rays_reflect, st.rays_refract) == \
+                    (sto.rays_primary, sto.rays_shadow, sto.rays_reflect, sto.rays_refract), f"{c}"
+    finally:
+        gpu_ctx.set_config(old)
 
 
 def test_auto_probe_frames_unchanged(gpu_ctx, avenger_scene):
