@@ -62,8 +62,8 @@ CONFIGS = {
 }
 # PMC-measured HBM traffic per closest-hit launch of the bench's profiled configuration
 # (tools/profile.sh + tools/traffic.py, committed under profiles/)
-TRAFFIC = {"C2": "profiles/r3/traffic_C2.json", "C3": "profiles/r3/traffic_C3.json",
-           "C4": "profiles/r3/traffic_C4.json", "C5": "profiles/r3/traffic_C5.json",
+TRAFFIC = {"C2": "profiles/r4/traffic_C2_r4f.json", "C3": "profiles/r3/traffic_C3.json",
+           "C4": "profiles/r3/traffic_C4.json", "C5": "profiles/r4/traffic_C5_r4r.json",
            "C2-path": "profiles/r2/traffic_C2-path.json"}
 
 
@@ -403,12 +403,18 @@ def main():
     elapsed = time.perf_counter() - t0
     if dist:
         dist.barrier()
-    # frame latency (one synchronous frame at a time), reported beside the throughput
+    # frame latency (one synchronous frame at a time, the reference's Producer loop,
+    # simpleguidx11.cpp:95-124), reported beside the throughput: the context set up for it --
+    # one frame in flight, so a frame gets the two pipeline slots and the deep-tiles-first deal
+    # (pgrt_config.tile_order), which needs one earlier frame of the same size (2 warm-ups)
     lat = []
-    for _ in range(min(args.steps, 30)):
+    ctx.set_frames_in_flight(1)
+    for k in range(min(args.steps, 30) + 2):
         t1 = time.perf_counter()
         frame(params)
-        lat.append(time.perf_counter() - t1)
+        if k >= 2:
+            lat.append(time.perf_counter() - t1)
+    ctx.set_frames_in_flight(in_flight)
     latency_ms = sorted(lat)[len(lat) // 2] * 1e3 if lat else None
     total_rays = rays
     per_rank_ms = [elapsed / max(1, args.steps) * 1e3]
@@ -530,6 +536,7 @@ def main():
         # per frame) queued behind them and overlapped with the calls in flight
         fb_host = ctx.host_array((args.height, args.width, 4))
         try:
+            ctx.set_frames_in_flight(1)  # synchronous frames: as the latency above
             for _ in range(2):
                 ctx.render(params, out=fb_host)
             lat_h = []
@@ -538,6 +545,7 @@ def main():
                 ctx.render(params, out=fb_host)
                 lat_h.append(time.perf_counter() - t1)
         finally:
+            ctx.set_frames_in_flight(in_flight)
             ctx.host_free(fb_host)
         ring = min(in_flight, 4)
         bufs = [ctx.host_array((F, args.height, args.width, 4)) for _ in range(ring)]

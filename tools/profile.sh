@@ -29,4 +29,6 @@ run pmc_fetch 300 --kernel-trace --pmc FETCH_SIZE
 run pmc_write 300 --kernel-trace --pmc WRITE_SIZE
 run pmc_l2 300 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum
 run pmc_valu 300 --kernel-trace --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE
+# bench.py --roofline-only's frames per call and profile=1 calls for this config (traffic.py)
+if [ "$CFG" = C2 ]; then export FRAMES_PER_CALL=8 ROOF_CALLS=5; else export FRAMES_PER_CALL=1 ROOF_CALLS=2; fi
 python3 tools/traffic.py "$OUT" "$OUT/traffic_${CFG}.json" "$TAG" "$(grep -o '"workload": "[^"]*"' "$OUT/trace.log" | head -1 | sed 's/"workload": "//; s/"$//')"

@@ -123,8 +123,10 @@ def main():
         res["valu_issue_note"] = ("frac = SQ_INSTS_VALU x 2 cyc / (1024 SIMDs x GRBM_GUI_ACTIVE / 8): the fraction of "
                                   "the chip's VALU issue slots the launch used (1.0 = every SIMD issuing a wave64 "
                                   "VALU instruction every 2 cycles)")
+    # bench.py --roofline-only: F frames per call (8 for C2, 1 for C3-C5), 5 profile=1 calls for
+    # C2 and 2 for the others (its `reps`)
     fpc = int(os.environ.get("FRAMES_PER_CALL", "8"))
-    fr = frame_bytes(fetch, fn, write, wn, fpc)
+    fr = frame_bytes(fetch, fn, write, wn, fpc, int(os.environ.get("ROOF_CALLS", "5")))
     if fr:
         res["frame"] = fr
         res["frame_note"] = ("every kernel of the profile=1 roofline calls (FETCH_SIZE x2 + WRITE_SIZE), per frame; "
