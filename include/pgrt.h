@@ -468,6 +468,10 @@ int pgrt_timeline_read(pgrt_ctx* ctx, pgrt_timeline_rec* out, int max, int* n);
  *      pairs; out: n x 8 {sqrtf(a), a/b, powf(a,b), expf(a), atan2f(a,b), asinf(a),
  *      1/sqrtf(a), (float)pow((double)a,(double)b)} ---- */
 int pgrt_selftest_math(pgrt_ctx* ctx, const float* in_pairs, int n, float* out8);
+/* ---- test hook: the kernels' sRGB expand / compress (mix_srgb, utils.cpp:204-241) against their
+ *      exact pg_pow_d form on every float whose bit pattern is in [first_bits, first_bits + count):
+ *      mismatches[0] / [1] = inputs where expand / compress differ (bitwise) ---- */
+int pgrt_selftest_srgb(pgrt_ctx* ctx, uint32_t first_bits, uint32_t count, uint64_t* mismatches);
 
 #ifdef __cplusplus
 }

@@ -2729,4 +2729,21 @@ int pgrt_selftest_math(pgrt_ctx* ctx, const float* in_pairs, int n, float* out8)
     });
 }
 
+// test hook: the kernels' sRGB expand / compress against their exact form over a float range
+int pgrt_selftest_srgb(pgrt_ctx* ctx, uint32_t first_bits, uint32_t count, uint64_t* mismatches) {
+    if (!ctx || !mismatches) return PGRT_ERR_INVALID_ARGUMENT;
+    return guarded(ctx, [&] {
+        DevBuf<unsigned long long> m;
+        m.alloc(2);
+        PGRT_HIP(hipMemsetAsync(m.p, 0, 2 * sizeof(unsigned long long), ctx->stream));
+        launch_selftest_srgb(first_bits, count, m.p, ctx->stream);
+        PGRT_HIP(hipGetLastError());
+        unsigned long long h[2] = {0, 0};
+        PGRT_HIP(hipMemcpyAsync(h, m.p, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+        PGRT_HIP(hipStreamSynchronize(ctx->stream));
+        mismatches[0] = h[0];
+        mismatches[1] = h[1];
+    });
+}
+
 }  // extern "C"

@@ -471,6 +471,24 @@ __global__ void k_selftest(const float* in, int n, float* out) {
     o[7] = (float)pg_pow_d((double)a, (double)b);
 }
 
+// srgb_expand / srgb_compress (the kernels' form) vs their exact pg_pow_d form, bitwise, over a
+// range of float bit patterns (grid-stride); mismatches counted per function
+__global__ __launch_bounds__(256) void k_selftest_srgb(uint32_t first, uint32_t count, unsigned long long* mism) {
+    unsigned long long me = 0, mc = 0;
+    for (uint32_t k = blockIdx.x * 256u + threadIdx.x; k < count; k += gridDim.x * 256u) {
+        const float u = __uint_as_float(first + k);
+        me += __float_as_uint(srgb_expand(u)) != __float_as_uint(srgb_expand_exact(u)) ? 1ull : 0ull;
+        mc += __float_as_uint(srgb_compress(u)) != __float_as_uint(srgb_compress_exact(u)) ? 1ull : 0ull;
+    }
+    if (me) atomicAdd(&mism[0], me);
+    if (mc) atomicAdd(&mism[1], mc);
+}
+
+void launch_selftest_srgb(uint32_t first_bits, uint32_t count, unsigned long long* mismatches, hipStream_t stream) {
+    if (count == 0) return;
+    hipLaunchKernelGGL(k_selftest_srgb, dim3(16384), dim3(256), 0, stream, first_bits, count, mismatches);
+}
+
 void launch_selftest_math(const float* in, int n, float* out, hipStream_t stream) {
     if (n <= 0) return;
     hipLaunchKernelGGL(k_selftest, dim3(ceil_div(n, 256)), dim3(256), 0, stream, in, n, out);

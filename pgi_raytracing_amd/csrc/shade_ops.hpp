@@ -239,18 +239,59 @@ __device__ inline float4 env_texel(const SceneView& s, const float* lut, V3 d) {
     return env_finish(s, lut, env_fetch(s, d));
 }
 
-// utils.cpp:204-241
-__device__ inline float srgb_compress(float u) {
+// utils.cpp:204-241, exactly as the restatement evaluates it (pg_pow_d: double exp(y log x))
+__device__ __noinline__ float srgb_compress_exact(float u) {
     if (u <= 0) return 0.0f;
     if (u >= 1) return 1.0f;
     if ((double)u <= 0.00313080) return (float)(12.92 * (double)u);
     return (float)(1.00 * pg_pow_d((double)u, 1 / 2.4) - 0.055);
 }
-__device__ inline float srgb_expand(float u) {
+__device__ __noinline__ float srgb_expand_exact(float u) {
     if (u <= 0) return 0.0f;
     if (u >= 1) return 1.0f;
     if ((double)u <= 0.04045) return (float)((double)u / 12.92);
     return (float)pg_pow_d(((double)u + 0.055) / 1.055, 2.4);
+}
+
+// The same floats, faster (mix_srgb's six powers are most of a dielectric node's combine).  y =
+// x^(p/q) as the root of y^q = x^p: a float exp2(log2) estimate (~2^-20 relative), then two Newton
+// steps in double with a float reciprocal of the derivative (-> ~2^-50), then Ziv's rounding test:
+// when y widened by 2^-40 either way rounds to one float, that float is also the rounding of the
+// restatement's pg_pow_d (both are within ~2^-50 of the true power; the double exponents 2.4 and
+// 1/2.4 differ from 12/5 and 5/12 by < 2^-51 relative in the result), otherwise the exact function
+// decides (probability ~2^-16).  tests/test_gpu_parity.py compares both on EVERY float in [0, 1].
+__device__ __forceinline__ double pow_root_newton(double y, double xp, int q) {
+    // one Newton step for y^q = xp (q = 5 or 12): y -= (y^q - xp) / (q y^(q-1))
+    const double y2 = y * y, y4 = y2 * y2;
+    const double yq = q == 5 ? y4 * y : y4 * y4 * y4;
+    const float r = __builtin_amdgcn_rcpf((float)((double)q * yq)) * (float)y;  // 1 / (q y^(q-1))
+    return fma(-(yq - xp), (double)r, y);
+}
+__device__ inline float srgb_compress(float u) {
+    if (u <= 0) return 0.0f;
+    if (u >= 1) return 1.0f;
+    if ((double)u <= 0.00313080) return (float)(12.92 * (double)u);
+    const double x = (double)u;
+    const double x2 = x * x, x5 = x2 * x2 * x;  // y = x^(5/12): y^12 = x^5
+    double y = (double)__builtin_amdgcn_exp2f((5.0f / 12.0f) * __builtin_amdgcn_logf(u));
+    y = pow_root_newton(y, x5, 12);
+    y = pow_root_newton(y, x5, 12);
+    const double v = y - 0.055, tol = y * 0x1p-40;
+    const float lo = (float)(v - tol), hi = (float)(v + tol);
+    return lo == hi ? lo : srgb_compress_exact(u);
+}
+__device__ inline float srgb_expand(float u) {
+    if (u <= 0) return 0.0f;
+    if (u >= 1) return 1.0f;
+    if ((double)u <= 0.04045) return (float)((double)u / 12.92);
+    const double x = ((double)u + 0.055) / 1.055;
+    const double x4 = (x * x) * (x * x), x12 = x4 * x4 * x4;  // y = x^(12/5): y^5 = x^12
+    double y = (double)__builtin_amdgcn_exp2f(2.4f * __builtin_amdgcn_logf((float)x));
+    y = pow_root_newton(y, x12, 5);
+    y = pow_root_newton(y, x12, 5);
+    const double tol = y * 0x1p-40;
+    const float lo = (float)(y - tol), hi = (float)(y + tol);
+    return lo == hi ? lo : srgb_expand_exact(u);
 }
 // mix_srgb = compress(mix_linear(expand(c0), expand(c1), a)); each of the three swaps r<->b.
 __device__ inline float4 mix_srgb(float4 c0, float4 c1, float a) {

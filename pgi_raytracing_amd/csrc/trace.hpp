@@ -304,5 +304,6 @@ void launch_pack_attributes(const float* nrm, const float* uv, const int* mat, i
 
 // math self-test hook (tests/test_gpu_*): evaluates the shared math on the device
 void launch_selftest_math(const float* in, int n, float* out, hipStream_t stream);
+void launch_selftest_srgb(uint32_t first_bits, uint32_t count, unsigned long long* mismatches, hipStream_t stream);
 
 }  // namespace pgrt

@@ -100,6 +100,7 @@ def lib():
         "pgrt_obj_material_name": (C.c_char_p, [vp, ip]),
         "pgrt_obj_surface_range": (ip, [vp, ip, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "pgrt_selftest_math": (ip, [vp, fp, ip, fp]),
+        "pgrt_selftest_srgb": (ip, [vp, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64)]),
         "pgrt_frame_diag": (ip, [vp, C.POINTER(abi.LevelDiag), ip]),
         "pgrt_timeline_enable": (ip, [vp, ip]),
         "pgrt_timeline_read": (ip, [vp, C.POINTER(abi.TimelineRec), ip, C.POINTER(C.c_int)]),
@@ -309,6 +310,13 @@ class Context:
         out = np.zeros((pairs.shape[0], 8), np.float32)
         _check(self.h, self.L.pgrt_selftest_math(self.h, abi.fptr(pairs), pairs.shape[0], abi.fptr(out)))
         return out
+
+    def selftest_srgb(self, first_bits: int, count: int):
+        """(expand, compress) mismatches of the kernels' sRGB functions vs their exact form over the
+        floats with bit patterns [first_bits, first_bits + count)."""
+        m = (C.c_uint64 * 2)()
+        _check(self.h, self.L.pgrt_selftest_srgb(self.h, first_bits, count, m))
+        return int(m[0]), int(m[1])
 
     # ---- frames in flight ----
     def set_frames_in_flight(self, n: int):

@@ -69,6 +69,20 @@ def test_env_angles_fast_path_bit_exact(gpu_ctx):
     assert same.all(), f"{len(bad)} mismatches, first {bad[:5]}: pairs {pairs[bad[:5, 0]]}"
 
 
+def test_srgb_fast_path_exhaustive(gpu_ctx):
+    """The kernels' sRGB expand / compress (mix_srgb: a float exp2(log2) estimate, two Newton steps
+    in double, Ziv's rounding test with the exact pg_pow_d form as fallback) equal the exact form
+    bit for bit on EVERY float in [0, 1] (bit patterns 0 .. 0x3f800000, ~1.07e9 inputs each) and
+    on a band above 1 -- the proof that the fast path cannot change a pixel."""
+    end = 0x3F800000 + (1 << 20)
+    first = 0
+    while first < end:
+        n = min(1 << 28, end - first)
+        me, mc = gpu_ctx.selftest_srgb(first, n)
+        assert (me, mc) == (0, 0), f"bits [{first:#x}, {first + n:#x}): {me} expand, {mc} compress mismatches"
+        first += n
+
+
 def test_tutorial1_kat_on_gpu(gpu_ctx):
     gpu_ctx.set_scene(single_triangle_scene())
     ray = np.array([0.1, 0.2, 2.0, FLT_MIN, 0.0, 0.0, -1.0, FLT_MAX], np.float32)
