@@ -524,6 +524,7 @@ def test_tile_order_bit_exact(gpu_ctx, avenger_scene, order):
     round-robin (-1); a different camera makes the recorded tiles stale -- every frame equals the
     oracle bit for bit, with the same ray counts per kind."""
     old = gpu_ctx.configure(tile_order=order)
+    gpu_ctx.set_scene(avenger_scene)
     try:
         W, H = 448, 320  # 7 x 5 tiles: the canopy covers some of them
         for k, (pos, c) in enumerate((((0.0, 0.0, 0.0), dict(spp_side=1, max_level=5)),
