@@ -19,7 +19,7 @@ __device__ __forceinline__ void tile_pixel(int slot_pix, const int4* tiles, int&
     const int lx = ((blk & 7) << 3) + (w & 7);
     const int ly = ((blk >> 3) << 3) + (w >> 3);
     const int4 tr = tiles[tile];
-    valid = lx < tr.z && ly < tr.w;
+    valid = lx < tile_width(tr) && ly < tr.w;
     px = tr.x + lx;
     py = tr.y + ly;
 }
@@ -28,7 +28,7 @@ __device__ __forceinline__ void tile_pixel(int slot_pix, const int4* tiles, int&
 __device__ __forceinline__ void store_pixel(const FrameParams& fp, const int4* tiles, const FrameOut& fo, int p,
                                             int px, int py, float4 o) {
     if (fo.mode == 0) {
-        float* dst = fo.out + (size_t)frame_of_tile(fp, p / (kTile * kTile)) * fp.frame_stride +
+        float* dst = fo.out + (size_t)frame_of_tile(tiles[p / (kTile * kTile)]) * fp.frame_stride +
                      ((size_t)(py - fo.oy) * (size_t)fo.pitch + (size_t)(px - fo.ox)) * 4;
         st_stream(reinterpret_cast<float4*>(dst), o);
         return;
@@ -56,7 +56,8 @@ __device__ __forceinline__ void store_pixel(const FrameParams& fp, const int4* t
 // of a partial tile: ro = 0, rd = (0, 0, 0, -1) (tfar < 0 never hits).
 __device__ __forceinline__ bool primary_ray(const CameraView& cam, const FrameParams& fp, const int4* tiles, int i,
                                             float4& ro, float4& rd) {
-    const int slot_pix = i / fp.nsb;
+    // one sample per pixel per batch (1 spp, the C2 frames): no integer divisions by run-time values
+    const int slot_pix = fp.nsb == 1 ? i : i / fp.nsb;
     const int s = fp.s0 + (i - slot_pix * fp.nsb);
     int px, py;
     bool valid;
@@ -66,28 +67,30 @@ __device__ __forceinline__ bool primary_ray(const CameraView& cam, const FramePa
         rd = make_float4(0, 0, 0, -1.0f);
         return false;
     }
-    const uint32_t frame = fp.frame + (uint32_t)frame_of_tile(fp, slot_pix / (kTile * kTile));
+    const uint32_t frame = fp.frame + (uint32_t)frame_of_tile(tiles[slot_pix / (kTile * kTile)]);
     const int S = fp.spp_side;
-    const int sx = s / S, sy = s - (s / S) * S;
+    const int sq = S == 1 ? 0 : s / S;
+    const int sx = sq, sy = s - sq * S;
     const uint32_t pixel = (uint32_t)py * (uint32_t)cam.width + (uint32_t)px;
     float j0 = 0.0f, j1 = 0.0f, j2 = 0.0f, j3 = 0.0f;
     if (fp.jitter != PGRT_JITTER_NONE) {
-        const float Sf = (float)S;
-        const float ja = -0.5f / Sf, jb = 0.5f / Sf;
-        const float la = -fp.aperture / 2.0f, lb = fp.aperture / 2.0f;
+        const float ja = fp.jit_a, jb = fp.jit_b;  // -0.5f / S, 0.5f / S
         const float u0 = pg_jitter_u01(fp.seed, frame, pixel, (uint32_t)s, 0);
         const float u1 = pg_jitter_u01(fp.seed, frame, pixel, (uint32_t)s, 1);
-        const bool corr = fp.jitter == PGRT_JITTER_HASH_CORRELATED;
-        const float u2 = corr ? u0 : pg_jitter_u01(fp.seed, frame, pixel, (uint32_t)s, 2);
-        const float u3 = corr ? u1 : pg_jitter_u01(fp.seed, frame, pixel, (uint32_t)s, 3);
         j0 = u0 * (jb - ja) + ja;
         j1 = u1 * (jb - ja) + ja;
-        j2 = u2 * (lb - la) + la;
-        j3 = u3 * (lb - la) + la;
+        if (fp.dof) {  // the lens sample (streams 2, 3) only where the thin lens uses it
+            const float la = -fp.aperture / 2.0f, lb = fp.aperture / 2.0f;
+            const bool corr = fp.jitter == PGRT_JITTER_HASH_CORRELATED;
+            const float u2 = corr ? u0 : pg_jitter_u01(fp.seed, frame, pixel, (uint32_t)s, 2);
+            const float u3 = corr ? u1 : pg_jitter_u01(fp.seed, frame, pixel, (uint32_t)s, 3);
+            j2 = u2 * (lb - la) + la;
+            j3 = u3 * (lb - la) + la;
+        }
     }
     // get_pixel sample position (raytracer.cpp:412-413)
-    const float nx = (float)px + ((float)sx * (1.0f / (float)S)) + j0;
-    const float ny = (float)py + ((float)sy * (1.0f / (float)S)) + j1;
+    const float nx = (float)px + ((float)sx * fp.inv_s) + j0;  // fp.inv_s = 1.0f / S
+    const float ny = (float)py + ((float)sy * fp.inv_s) + j1;
     // camera-space direction with integer W/2, H/2 (PinHoleCamera.cpp:41-42, :67)
     V3 crd = v3(nx - (float)(cam.width / 2), (float)(cam.height / 2) - ny, -cam.fy);
     crd = normalize(crd);

@@ -1033,6 +1033,9 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
     fp0.frame_out_tiles = fs->frame_out_tiles;
     fp0.frame_stride = fs->frame_stride;
     fp0.spp_side = p->spp_side;
+    fp0.inv_s = 1.0f / (float)p->spp_side;
+    fp0.jit_a = -0.5f / (float)p->spp_side;
+    fp0.jit_b = 0.5f / (float)p->spp_side;
     fp0.max_level = p->max_level;
     fp0.dof = p->dof;
     fp0.focal = p->focal_distance;
@@ -1338,7 +1341,7 @@ void frame_stats(pgrt_ctx* ctx, FrameSet* fs, int retries) {
     const int launches = st->trace_launches;
     *st = pgrt_stats{};
     long long real_pix = 0;
-    for (auto& t : fs->tiles) real_pix += (long long)t.z * t.w;
+    for (auto& t : fs->tiles) real_pix += (long long)tile_width(t) * t.w;
     st->rays_primary = (uint64_t)(real_pix * spp);
     st->rays_shadow = rays_shadow;
     st->rays_reflect = rays_reflect;
@@ -1632,7 +1635,8 @@ void start_frame(pgrt_ctx* ctx, FrameSet* fs, const pgrt_render_params* p, std::
     fs->frame_out_tiles = (int)tiles.size();
     fs->frame_stride = frame_stride;
     fs->tiles.clear();
-    for (int f = 0; f < nframes; ++f) fs->tiles.insert(fs->tiles.end(), tiles.begin(), tiles.end());
+    for (int f = 0; f < nframes; ++f)  // each record carries its frame (frame_of_tile)
+        for (const int4& t : tiles) fs->tiles.push_back(make_int4(t.x, t.y, t.z | (f << kTileFrameShift), t.w));
     fs->distributed = distributed;
     fs->dist_fb = fb;
     fs->cam_w = ctx->cam.width;

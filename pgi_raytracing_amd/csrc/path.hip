@@ -60,7 +60,7 @@ __device__ __forceinline__ uint32_t path_key(const FrameParams& fp, const int4* 
     int px, py;
     bool valid;
     tile_pixel(slot_pix, tiles, px, py, valid);
-    const uint32_t frame = fp.frame + (uint32_t)frame_of_tile(fp, slot_pix / (kTile * kTile));
+    const uint32_t frame = fp.frame + (uint32_t)frame_of_tile(tiles[slot_pix / (kTile * kTile)]);
     return pg_path_key(fp.seed, frame, (uint32_t)py * (uint32_t)width + (uint32_t)px, (uint32_t)sample);
 }
 

@@ -68,15 +68,20 @@ struct FrameParams {
     int slots, slot, frame_tiles, frame_out_tiles;  // frame_out_tiles: tiles per frame in a tile-compact output
     long long frame_stride;
     int count;  // profile == 2: the shade kernels count hits / textured hits (FrameCounters::shade)
+    // get_pixel's per-frame constants (host IEEE float divisions = the device's correctly rounded
+    // ones): 1 / S and the sub-pixel jitter interval [-0.5 / S, 0.5 / S] (raytracer.cpp:407-413)
+    float inv_s, jit_a, jit_b;
     // synchronous frames: the level-0 shade sets tile_deep[q] = 1 for the slot's tile q when a
     // primary ray there hit a dielectric (reflection / refraction children) -- the next frame's
     // tile deal (context.cpp deal_tiles); NULL: not recorded
     int* tile_deep;
 };
 
-__host__ __device__ inline int frame_of_tile(const FrameParams& fp, int tile) {
-    return fp.frame_tiles > 0 ? (tile * fp.slots + fp.slot) / fp.frame_tiles : 0;
-}
+// A tile record is (x, y, width | frame << 8, height): the frame of a multi-frame call the tile
+// belongs to rides in the record (set by start_frame), so no ray divides by the call's tile count
+constexpr int kTileFrameShift = 8;
+__host__ __device__ inline int tile_width(const int4& tr) { return tr.z & ((1 << kTileFrameShift) - 1); }
+__host__ __device__ inline int frame_of_tile(const int4& tr) { return tr.z >> kTileFrameShift; }
 
 // level-L queue view
 struct Queue {
