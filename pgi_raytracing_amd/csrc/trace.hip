@@ -662,7 +662,8 @@ __device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __re
 // MINW: minimum waves per SIMD the register allocation must allow (launch bound).  The level-0
 // kernel (GEN) uses 67 VGPRs -> 7 waves; big scenes (BVH + triangles far beyond the L2, fetches
 // that wait on the MALL / HBM) take the 8-wave build (59 VGPRs, more SGPR spills): C5 19.6 ->
-// 19.1 ms/frame, while the avenger proxy's issue-bound level 0 runs better at 7 (r2j A/B)
+// 19.1 ms/frame; since the lighter r4 ray generation the avenger proxy's level 0 gains too (r4z A/B,
+// profiles/r4/ab_r4z_shade_block_l0_waves.txt: C2 400 frames 0.1525 -> 0.1496 ms/frame)
 template <bool COUNT, bool GEN, int MINW, bool BUDGET = false>
 __global__ __launch_bounds__(kTraceBlock, MINW) void k_trace_pkt(SceneView s, const float4* __restrict__ ro,
                                                            const float4* __restrict__ rd, float4* __restrict__ hits,
@@ -741,14 +742,13 @@ bool launch_trace(const SceneView& s_in, const TraceLaunch& t, hipStream_t strea
     hipExtLaunchKernelGGL((k_trace_pkt<C, G, W, B>), dim3(grid), dim3(kTraceBlock), 0, stream, t_ev_start, ev_stop, \
                           0, s, t.ro, t.rd, t.hits, t.count_dev, t.count_terms, t.count_host, max_count, t.counters, \
                           g, t.pkt_util, t.budget, t.defer_list, t.defer_count)
-        const bool big = s.ntri > kPacketBigScene;
         s.stamps = stamp_next(kStampTracePkt, t.level, grid, kTraceBlock);
         if (t.count) {
             if (t.gen) PGRT_LAUNCH_P(true, true, 1, false);
             else if (budget) PGRT_LAUNCH_P(true, false, 1, true);
             else PGRT_LAUNCH_P(true, false, 1, false);
         } else if (t.gen) {
-            if (big) PGRT_LAUNCH_P(false, true, 8, false); else PGRT_LAUNCH_P(false, true, 1, false);
+            PGRT_LAUNCH_P(false, true, 8, false);  // every scene (r4z: the avenger too)
         } else if (budget) {
             PGRT_LAUNCH_P(false, false, 1, true);
         } else {
