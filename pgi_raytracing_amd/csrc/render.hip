@@ -63,8 +63,9 @@ void launch_raygen(const CameraView& cam, const FrameParams& fp, const int4* til
 // unconstrained 98 VGPRs allow -- r2c C2 A/B: 0.1938 -> 0.1901 ms/frame (5 waves 0.1907)
 constexpr int kShadeBlock = 256;
 static_assert(kShadeBlock % kBlock == 0, "k_shade blocks are whole multiples of kBlock");
+// level 0 of a 1-spp batch at 6 waves per SIMD (80 VGPRs; r4aa: driver line 0.177 -> 0.173 ms/frame)
 #ifndef PGRT_SHADE_L0F_WAVES
-#define PGRT_SHADE_L0F_WAVES 5
+#define PGRT_SHADE_L0F_WAVES 6
 #endif
 constexpr int kShadeL0fWaves = PGRT_SHADE_L0F_WAVES;
 
