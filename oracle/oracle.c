@@ -216,7 +216,12 @@ static inline float xorsign(float a, float s_signbit_src)
     return a;
 }
 
-/* Embree's Moeller-Trumbore triangle test (restated); returns 1 on a hit in (tnear, tfar]. */
+/* Embree's Moeller-Trumbore triangle test (restated; Embree 3.11 kernels/geometry/
+ * triangle_intersector_moeller.h, not vendored): edge tests on the scaled U, V, then the depth
+ * test on the SCALED distance, absDen*tnear < T <= absDen*tfar, and only then t = T / absDen
+ * (Embree: T * rcp(absDen); here the IEEE division -- the one remaining difference).  The
+ * interval is the ray's own (tnear, tfar], so the accepted set does not depend on the order in
+ * which triangles are tested; the closest of them wins, ties to the smaller index. */
 static inline int tri_hit(const float* q, const Ray* r, float* tt, float* uu, float* vv)
 {
     V3 v0 = v3(q[0], q[1], q[2]), e1 = v3(q[3], q[4], q[5]), e2 = v3(q[6], q[7], q[8]);
@@ -229,9 +234,8 @@ static inline int tri_hit(const float* q, const Ray* r, float* tt, float* uu, fl
     float V = xorsign(v_dot(R, e1), den);
     if (!(den != 0.0f && U >= 0.0f && V >= 0.0f && U + V <= absden)) return 0;
     float T = xorsign(v_dot(ng, C), den);
-    float t = T / absden;
-    if (!(t > r->tnear && t <= r->tfar)) return 0;
-    *tt = t;
+    if (!(absden * r->tnear < T && T <= absden * r->tfar)) return 0;
+    *tt = T / absden;
     *uu = U / absden;
     *vv = V / absden;
     return 1;

@@ -24,7 +24,8 @@ _LIBS = {}
 def lib(libm: bool = False):
     name = "liboracle_libm.so" if libm else "liboracle.so"
     if name not in _LIBS:
-        path = os.path.join(HERE, "_build", name)
+        # ORACLE_LIB_DIR: the sanitizer build of the restatement (make asan -> build/asan)
+        path = os.path.join(os.environ.get("ORACLE_LIB_DIR") or os.path.join(HERE, "_build"), name)
         if not os.path.exists(path):
             raise RuntimeError(f"{path} missing: run `make -C oracle` (or __graft_entry__.build())")
         L = C.CDLL(path)

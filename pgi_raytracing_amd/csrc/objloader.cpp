@@ -298,10 +298,15 @@ int pgrt_obj_load(const char* obj_path, int flip_yz, pgrt_obj** out) {
         };
         auto vertex = [&](const std::string& tok) -> FaceVertex {
             parse_indices(tok, buf);
-            FaceVertex fv{std::atoi(buf[0].c_str()) - 1, std::atoi(buf[1].c_str()) - 1, std::atoi(buf[2].c_str()) - 1};
-            if (fv.v < 0 || fv.v >= nv || fv.t < 0 || fv.t >= nt || fv.n < 0 || fv.n >= nn)
+            // atoi(b) - 1 in the reference (objloader.cpp:443-452), range-checked here in 64 bits:
+            // an index past INT_MAX (atoi's overflow, then INT_MIN - 1) is undefined there
+            // (make asan: UBSan caught it); strtoll saturates instead
+            const long long iv = std::strtoll(buf[0].c_str(), nullptr, 10) - 1;
+            const long long it = std::strtoll(buf[1].c_str(), nullptr, 10) - 1;
+            const long long in = std::strtoll(buf[2].c_str(), nullptr, 10) - 1;
+            if (iv < 0 || iv >= nv || it < 0 || it >= nt || in < 0 || in >= nn)
                 throw std::runtime_error("face index out of range in '" + tok + "'");
-            return fv;
+            return FaceVertex{(int)iv, (int)it, (int)in};
         };
         for (const auto& line : lines) {  // pass 3: groups, materials, faces
             const char c = line[0];

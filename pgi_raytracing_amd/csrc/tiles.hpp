@@ -15,6 +15,13 @@
 #include <cstdlib>
 #include <cstdio>
 
+// host + device helpers; a host-only compile (tiles_abi.cpp under g++, make asan) sees plain inline
+#if defined(__HIP__)
+#define PGRT_TILE_HD __host__ __device__
+#else
+#define PGRT_TILE_HD
+#endif
+
 namespace pgrt {
 
 struct TileDeal {
@@ -54,10 +61,10 @@ inline TileDeal tile_deal(int world, int a, int b) {
     return TileDeal{world, a, b};
 }
 
-__host__ __device__ inline int deal_round(const TileDeal& d) { return d.a + d.b * (d.world - 1); }
+PGRT_TILE_HD inline int deal_round(const TileDeal& d) { return d.a + d.b * (d.world - 1); }
 
 // tile t -> (rank, local index j on that rank)
-__host__ __device__ inline void deal_owner(const TileDeal& d, int t, int& rank, int& j) {
+PGRT_TILE_HD inline void deal_owner(const TileDeal& d, int t, int& rank, int& j) {
     if (d.world <= 1) {
         rank = 0;
         j = t;
@@ -80,7 +87,7 @@ __host__ __device__ inline void deal_owner(const TileDeal& d, int t, int& rank, 
 }
 
 // (rank, local index j) -> tile t (may be >= the tile count: padding of the rank's list)
-__host__ __device__ inline int deal_tile(const TileDeal& d, int rank, int j) {
+PGRT_TILE_HD inline int deal_tile(const TileDeal& d, int rank, int j) {
     if (d.world <= 1) return j;
     const int R = deal_round(d);
     const int m = d.a < d.b ? d.a : d.b;

@@ -36,9 +36,11 @@ __device__ __forceinline__ bool box_hit_nf(float nx, float fx, float ny, float f
     return t0 <= t1 * 1.000001f;
 }
 
-// Moeller-Trumbore as Embree's closest-hit path evaluates it (see oracle/oracle.c): e1 = v0 - v1,
-// e2 = v2 - v0 (precomputed), Ng = e2 x e1, scaled edge tests, IEEE divisions.  Closest hit in
-// (tnear, tfar]; ties in t go to the smaller original triangle index.
+// Moeller-Trumbore as Embree's closest-hit path evaluates it (see oracle/oracle.c tri_hit): e1 =
+// v0 - v1, e2 = v2 - v0 (precomputed), Ng = e2 x e1, scaled edge tests, the depth test on the
+// scaled distance (absDen * tnear < T <= absDen * tfar, Embree 3.11 triangle_intersector_moeller.h)
+// before t = T / absDen (IEEE division; Embree: rcp).  Closest hit in the ray's (tnear, tfar];
+// ties in t go to the smaller original triangle index.
 // ng: the triangle's Ng = e2 x e1 (tri_normal, precomputed per reference with the same float ops)
 __device__ __forceinline__ void tri_test_ng(float4 q0, float4 q1, float4 q2, float4 ng, float ox, float oy, float oz,
                                             float dx, float dy, float dz, float tnear, float tfar, float& best_t,
@@ -56,8 +58,8 @@ __device__ __forceinline__ void tri_test_ng(float4 q0, float4 q1, float4 q2, flo
     const float V = xorsign(rx * e1x + ry * e1y + rz * e1z, den);
     if (den != 0.0f && U >= 0.0f && V >= 0.0f && U + V <= absden) {
         const float T = xorsign(ngx * cx + ngy * cy + ngz * cz, den);
-        const float t = T / absden;
-        if (t > tnear && t <= tfar) {
+        if (absden * tnear < T && T <= absden * tfar) {
+            const float t = T / absden;
             const int prim = __float_as_int(q0.w);
             if (best_prim < 0 || t < best_t || (t == best_t && prim < best_prim)) {
                 best_t = t;

@@ -432,10 +432,14 @@ def load_obj(obj_path: str, flip_yz: bool = False) -> Scene:
         d = abi.SceneDesc()
         L.pgrt_obj_scene(h, C.byref(d))
         n = d.num_triangles
-        pos = np.ctypeslib.as_array(d.positions, shape=(9 * n,)).copy()
-        nrm = np.ctypeslib.as_array(d.normals, shape=(9 * n,)).copy()
-        uv = np.ctypeslib.as_array(d.uvs, shape=(6 * n,)).copy()
-        mid = np.ctypeslib.as_array(d.material_ids, shape=(n,)).copy()
+
+        def arr(ptr, size, dtype):  # an OBJ without faces has no arrays at all (NULL pointers)
+            return np.ctypeslib.as_array(ptr, shape=(size,)).copy() if size else np.zeros(0, dtype)
+
+        pos = arr(d.positions, 9 * n, np.float32)
+        nrm = arr(d.normals, 9 * n, np.float32)
+        uv = arr(d.uvs, 6 * n, np.float32)
+        mid = arr(d.material_ids, n, np.int32)
         ns, nm, nt = C.c_int(), C.c_int(), C.c_int()
         L.pgrt_obj_counts(h, C.byref(ns), C.byref(nm), C.byref(nt))
         mats = []
@@ -443,7 +447,13 @@ def load_obj(obj_path: str, flip_yz: bool = False) -> Scene:
             m = d.materials[i]
             mats.append(MaterialData(L.pgrt_obj_material_name(h, i).decode(), tuple(m.diffuse), tuple(m.specular),
                                      m.shininess, m.ior, m.type, m.diffuse_tex))
-        textures = [TextureData.from_file(L.pgrt_obj_texture_path(h, i).decode()) for i in range(nt.value)]
+        textures = []
+        for i in range(nt.value):  # a map_Kd that does not decode fails the load (the reference reads garbage)
+            path = L.pgrt_obj_texture_path(h, i).decode()
+            try:
+                textures.append(TextureData.from_file(path))
+            except (OSError, ValueError, RuntimeError) as e:
+                raise PgrtError(-7, f"texture {path}: {e}") from e
         surfaces = []
         for i in range(ns.value):
             f, c = C.c_int(), C.c_int()

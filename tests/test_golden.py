@@ -110,3 +110,45 @@ def test_gpu_frames_equal_golden(gpu_ctx, vec, avenger_scene):
     p, _ = gpu_ctx.render(abi.make_params(max_level=5, spp_side=2, mode=abi.PGRT_MODE_PATH,
                                           jitter=abi.PGRT_JITTER_HASH, seed=7))
     assert bits_equal(w, vec["frame_whitted_d5"]) and bits_equal(p, vec["frame_path_d5_s2"])
+
+
+# ---- Embree's depth test on the scaled distance (tests/golden/make_depth_vectors.py) ----
+
+@pytest.fixture(scope="module")
+def depth():
+    return np.load(os.path.join(GOLDEN, "depth_test_vectors.npz"))  # allow_pickle=False (default)
+
+
+def _depth_scene(d):
+    from pgi_raytracing_amd.scene import LightData, MaterialData, Scene
+
+    pos = np.asarray(d["pos"], np.float32)
+    n = pos.size // 9
+    nrm = np.tile(np.array([0, 0, 1], np.float32), 3 * n)
+    return Scene(pos, nrm, np.zeros(6 * n, np.float32), np.zeros(n, np.int32), [MaterialData()], [], -1, [LightData()])
+
+
+def test_depth_vectors_separate_the_two_forms(depth):
+    """The vectors sit on the interval ends: the divide-first form classifies some differently."""
+    kinds = set(depth["kinds"][depth["divide_first_differs"]])
+    assert depth["divide_first_differs"].sum() >= 20
+    assert {"near", "far", "shadow-near", "shadow-far"} <= kinds
+
+
+@pytest.mark.parametrize("accel", [0, 1])
+def test_oracle_depth_test_is_embree_scaled_form(depth, accel):
+    """oracle tri_hit: absDen*tnear < T <= absDen*tfar before t = T/absDen (Embree 3.11
+    triangle_intersector_moeller.h), brute force and through the oracle's BVH."""
+    got = pyoracle.OracleScene(_depth_scene(depth), accel=accel).intersect(depth["rays"])
+    assert bits_equal(got, depth["hits"])
+
+
+@pytest.mark.gpu
+def test_gpu_depth_test_is_embree_scaled_form(gpu_ctx, depth):
+    """pgrt_intersect_closest (AoS and SoA) and pgrt_occluded on the boundary vectors, bit for bit."""
+    gpu_ctx.set_scene(_depth_scene(depth))
+    rays = np.asarray(depth["rays"], np.float32)
+    assert bits_equal(gpu_ctx.intersect(rays), depth["hits"])
+    assert bits_equal(gpu_ctx.intersect_soa(np.ascontiguousarray(rays.T)).T, depth["hits"])
+    occ = gpu_ctx.occluded(rays)
+    assert (occ.astype(bool) == (depth["hits"][:, 3].view(np.int32) >= 0)).all()
