@@ -46,6 +46,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # node visited, 80 B per 8-wide node visited (small queues), 48 B per triangle tested (our
 # triangle record: v0|id, e1, e2)
 RAY_BYTES, NODE_BYTES, WIDE_NODE_BYTES, TRI_BYTES = 48, 64, 80, 48
+# level-0 rays of the packet traversal are generated in registers (k_trace_pkt<GEN>): no 32-B ray
+# read; it stores what the level-0 shade reads back -- the 16-B direction (pinhole: origin, tnear
+# and medium come from the camera) or origin + direction + medium (36 B, DoF) -- and the 16-B hit
+L0_PINHOLE_BYTES, L0_DOF_BYTES = 16 + 16, 36 + 16
+# closest-hit launches in the device timeline (pgrt_timeline_enable; abi.TIMELINE_KINDS)
+TRACE_KINDS = ("trace_pkt", "trace", "trace_8g", "trace_resume", "trace_shadow", "subtree")
 # B_shade per shaded ray / hit / textured hit or env lookup / emitted ray
 SHADE_RAY_BYTES, SHADE_HIT_BYTES, SHADE_COLOUR_BYTES = 48, 16, 16
 SHADE_ATTR_BYTES, SHADE_TEXEL_BYTES, SHADE_EMIT_BYTES = 64, 12, 48
@@ -447,8 +453,12 @@ def main():
         p1.profile = 2
         s2 = prof_call(p1)
         frame_rays = s2.rays()
-        alg_bytes = (RAY_BYTES * frame_rays + NODE_BYTES * s2.node_visits + WIDE_NODE_BYTES * s2.wide_node_visits
-                     + TRI_BYTES * s2.tri_tests)
+        # level 0 on packets (AUTO always, unless --packet-levels turns them off): rays generated
+        # in registers, not read from a queue
+        fused_l0 = args.packet_levels is None or args.packet_levels != abi.PGRT_PACKETS_OFF
+        l0_bytes = (L0_DOF_BYTES if args.dof else L0_PINHOLE_BYTES) if fused_l0 else RAY_BYTES
+        alg_bytes = (RAY_BYTES * (frame_rays - s2.rays_primary) + l0_bytes * s2.rays_primary
+                     + NODE_BYTES * s2.node_visits + WIDE_NODE_BYTES * s2.wide_node_visits + TRI_BYTES * s2.tri_tests)
         avg_launch_ms = ms_trace / max(1, launches)
         per_launch_bytes = alg_bytes / max(1, launches / reps)
         achieved = per_launch_bytes / (avg_launch_ms * 1e-3) / 1e9
@@ -469,7 +479,47 @@ def main():
             "wide_node_visits_per_ray": round(s2.wide_node_visits / max(1, frame_rays), 2),
             "tri_tests_per_ray": round(s2.tri_tests / max(1, frame_rays), 2),
             "bytes_per_ray": round(alg_bytes / max(1, frame_rays), 1),
+            "level0_bytes_per_ray": l0_bytes,
+            "timing": "HIP events around every closest-hit launch of " + str(reps) + " profile=1 calls of "
+                      + str(frames_per_prof) + " frame(s), synchronous (rocprofv3 trace of exactly these calls: "
+                      "tools/profile.sh + tools/traffic.py)",
         }
+        if world == 1 and args.steps:
+            # the closest-hit launches in the TIMED configuration (calls of F frames, `in_flight` of
+            # them in flight): the device-stamped launch timeline of a separate run of such calls;
+            # the union of the closest-hit launches' wave spans is the time closest-hit kernels
+            # occupy the device per frame (<= the frame time by construction)
+            ncalls = max(2 * in_flight, min(max(1, args.steps // F), 4 * in_flight))
+            ctx.timeline_enable(True)
+            try:
+                run_frames(ncalls * F)
+                recs = ctx.timeline_read()
+            finally:
+                ctx.timeline_enable(False)
+            iv = sorted((r["us_start"], r["us_end"]) for r in recs if r["kind"] in TRACE_KINDS)
+            busy, cur = 0.0, None
+            for a, b in iv:
+                if cur is None or a > cur[1]:
+                    if cur:
+                        busy += cur[1] - cur[0]
+                    cur = [a, b]
+                else:
+                    cur[1] = max(cur[1], b)
+            if cur:
+                busy += cur[1] - cur[0]
+            span = (max(r["us_end"] for r in recs) - min(r["us_start"] for r in recs)) if recs else 0.0
+            nfr = ncalls * F
+            if busy > 0:
+                busy_ms = busy / 1e3 / nfr
+                ta = alg_bytes / frames_per_prof / (busy_ms * 1e-3) / 1e9
+                roof["timed"] = {
+                    "achieved": round(ta, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ta / HBM_PEAK_GBS, 4),
+                    "trace_busy_ms_per_frame": round(busy_ms, 4), "span_ms_per_frame": round(span / 1e3 / nfr, 4),
+                    "frames": nfr, "calls": ncalls, "frames_per_call": F, "in_flight": in_flight,
+                    "note": "closest-hit bytes per frame over the union of the closest-hit launches' wave spans "
+                            "(device timeline, pgrt_timeline_enable) while calls of the timed configuration run "
+                            "in flight -- a separate run with the stamps on; <= ms_per_step by construction",
+                }
         if args.mode == "whitted":
             # whole-frame algorithmic bytes (B = 32 + 16 + 64 N_node + 36 N_tri + B_shade)
             # over the timed region's ms per frame: the closest-hit bytes above (every level and the

@@ -451,6 +451,7 @@ int pgrt_frame_diag(const pgrt_ctx* ctx, pgrt_level_diag* out, int max_levels);
 #define PGRT_TL_PATH_SHADE 11
 #define PGRT_TL_PATH_RESOLVE 12
 #define PGRT_TL_SUBTREE 13      /* the deep levels as one launch (pgrt_config.subtree_level) */
+#define PGRT_TL_HOST_EXPORT 14  /* a slot's finished tiles to a page-locked host framebuffer */
 typedef struct pgrt_timeline_rec {
     uint64_t ticket;     /* the call (the ticket an asynchronous call returned; synchronous calls count too) */
     int slot;            /* pipeline slot (stream) of the call */

@@ -208,12 +208,15 @@ int pgrt_render(pgrt_ctx* ctx, const pgrt_render_params* p, float* rgba_host, pg
         int x, y, w, h;
         frame_rect(ctx, p, x, y, w, h);
         ctx->out_tmp.alloc((size_t)w * h * 4);
-        if (ctx->group)
+        const size_t bytes = (size_t)w * h * 4 * sizeof(float);
+        if (ctx->group) {
             group_render(ctx, p, 1, ctx->out_tmp.p, st);
-        else
-            render_tiles(ctx, p, rect_tiles(x, y, w, h), ctx->out_tmp.p, 0, x, y, w, st);
-        PGRT_HIP(hipMemcpyAsync(rgba_host, ctx->out_tmp.p, (size_t)w * h * 4 * sizeof(float), hipMemcpyDeviceToHost,
-                                ctx->stream));
+            PGRT_HIP(hipMemcpyAsync(rgba_host, ctx->out_tmp.p, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        } else {
+            // the frame's slots move their finished tiles to rgba_host themselves (set_host_output:
+            // export kernels into page-locked memory, else one copy after the frame)
+            render_tiles(ctx, p, rect_tiles(x, y, w, h), ctx->out_tmp.p, 0, x, y, w, st, 1, 0, rgba_host, bytes);
+        }
         PGRT_HIP(hipStreamSynchronize(ctx->stream));
         if (st) st->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     });
@@ -416,7 +419,7 @@ int submit_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device, 
         }
         FrameSet* fs = frame_set(ctx, (int)(ctx->next_ticket % (unsigned long long)ctx->frames_in_flight));
         if (fs->pending) finish_through(ctx, fs->ticket);  // the set's previous frame completes first
-        fs->host_dst = nullptr;
+        set_host_output(fs, nullptr, nullptr, 0);
         // pgrt_config.max_batches_in_flight: bound the sample batches queued across frames in
         // flight (this frame's own count estimated with one slot per frame, as enqueue_frame deals
         // them when frames are in flight)
@@ -452,11 +455,10 @@ int submit_async(pgrt_ctx* ctx, const pgrt_render_params* p, void* rgba_device, 
         } else {
             int x, y, w, h;
             frame_rect(ctx, p, x, y, w, h);
-            fs->host_dst = rgba_host;
-            fs->host_bytes = (size_t)nframes * w * h * 4 * sizeof(float);
             if (rgba_host) {
                 fs->host_stage.alloc((size_t)nframes * w * h * 4);
                 rgba_device = fs->host_stage.p;
+                set_host_output(fs, rgba_host, fs->host_stage.p, (size_t)nframes * w * h * 4 * sizeof(float));
             }
             start_frame(ctx, fs, p, rect_tiles(x, y, w, h), static_cast<float*>(rgba_device), 0, x, y, w, false,
                         nullptr, nframes, (long long)w * h * 4);

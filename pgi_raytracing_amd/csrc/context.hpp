@@ -220,11 +220,16 @@ struct FrameSet {
     TileDeal deal{1, 1, 1};  // distributed: the tile deal this frame was rendered with
     float* dist_fb = nullptr;
     DevBuf<float> tilebuf;  // distributed: this rank's tiles, tile-compact
-    // host-output frames (pgrt_render_frames_host_async): rendered into host_stage, then ONE
-    // device-to-host copy of host_bytes into host_dst on the set's first slot stream, overlapped
-    // with the frames in flight behind it
+    // host-output frames (pgrt_render, pgrt_render_frames_host_async; set_host_output): rendered
+    // into a device framebuffer (host_src: host_stage, or the context's out_tmp), then moved to
+    // host_dst.  A page-locked destination (host_map: its device-visible address) is written by one
+    // export kernel per pipeline slot as soon as that slot's tiles are final (k_export_tiles), so
+    // the bulk slot's pixels cross PCIe while the deep-tile slot still renders; a pageable one gets
+    // ONE device-to-host copy of host_bytes after every slot, on slot 0's stream
     DevBuf<float> host_stage;
+    float* host_src = nullptr;
     float* host_dst = nullptr;
+    float* host_map = nullptr;
     size_t host_bytes = 0;
     int cam_w = 0, cam_h = 0;  // image size at submission (the gather's layout)
     bool deep_rec = false;     // the level-0 shades record deep tiles (FrameParams::tile_deep)
@@ -418,8 +423,9 @@ void start_frame(pgrt_ctx* ctx, FrameSet* fs, const pgrt_render_params* p, std::
                  long long frame_stride = 0, TileDeal deal = TileDeal{1, 1, 1}, bool defer_gather = false);
 void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<int4>& tiles, float* out,
                   int out_mode, int ox, int oy, int pitch, pgrt_stats* st, int nframes = 1,
-                  long long frame_stride = 0);
+                  long long frame_stride = 0, float* host_out = nullptr, size_t host_bytes = 0);
 std::vector<int4> rect_tiles(int x0, int y0, int w, int h);
+void set_host_output(FrameSet* fs, float* dst, float* src, size_t bytes);
 void frame_rect(const pgrt_ctx* ctx, const pgrt_render_params* p, int& x, int& y, int& w, int& h);
 
 // ---- distributed.cpp

@@ -359,7 +359,7 @@ unsigned long long group_submit(pgrt_ctx* head, const pgrt_render_params* p, int
     for (pgrt_ctx* m : R) {
         on_device(m);
         FrameSet* fs = frame_set(m, si);
-        fs->host_dst = nullptr;
+        set_host_output(fs, nullptr, nullptr, 0);
         m->next_ticket = ticket;  // every rank's frame carries rank 0's ticket
         start_frame(m, fs, p, rank_tiles(head->cam.width, head->cam.height, m->rank, deal), nullptr, 1, 0, 0, 0,
                     true, m == head ? fb : nullptr, nframes, 0, deal, true);
@@ -439,7 +439,7 @@ int pgrt_render_distributed_device(pgrt_ctx* ctx, const pgrt_render_params* p, v
         FrameSet* fs = frame_set(ctx, 0);
         // set 0 may last have served pgrt_render_frames_host_async: its host destination belongs
         // to that call (the caller may have freed it), never to this frame
-        fs->host_dst = nullptr;
+        set_host_output(fs, nullptr, nullptr, 0);
         PGRT_HIP(hipEventRecord(fs->ev_ready, ctx->stream));
         const TileDeal deal = ctx_deal(ctx, ctx->world);
         start_frame(ctx, fs, p, rank_tiles(ctx->cam.width, ctx->cam.height, ctx->rank, deal), nullptr, 1, 0, 0, 0,

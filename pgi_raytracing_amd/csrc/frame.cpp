@@ -584,6 +584,13 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             debug_sync(s, "finish", 0, bi);
             ctx->timer.end(s, id);
         }
+        if (fs->host_map) {  // this slot's final pixels -> the page-locked host framebuffer, now
+            PGRT_REQUIRE(fs->out_mode == 0 && fs->out == fs->host_src, PGRT_ERR_INVALID_ARGUMENT,
+                         "internal: host export of a frame that is not rendered into its staging framebuffer");
+            launch_export_tiles(sl->tiles.p, nt, fs->host_src, fs->host_map, fs->ox, fs->oy, fs->pitch,
+                                fs->frame_stride, s);
+            debug_sync(s, "host export", 0, 0);
+        }
         sl->host_fc.resize(batches);
         // the frame's counters to pinned host memory, zeroed on the device for the next frame
         launch_export_counters(sl->fc.p, sl->pinned_fc, batches, fs->deep_rec ? sl->tile_deep.p : nullptr,
@@ -591,10 +598,10 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
         debug_sync(s, "export", 0, 0);
         PGRT_HIP(hipEventRecord(sl->ev_done, s));
     }
-    if (fs->host_dst && K > 0) {  // host output: after every slot, on slot 0's stream
+    if (fs->host_dst && !fs->host_map && K > 0) {  // pageable host output: after every slot, on slot 0's stream
         FrameSlot* s0 = fs->slots[0].get();
         for (int j = 1; j < K; ++j) PGRT_HIP(hipStreamWaitEvent(s0->stream, fs->slots[j]->ev_done, 0));
-        PGRT_HIP(hipMemcpyAsync(fs->host_dst, fs->host_stage.p, fs->host_bytes, hipMemcpyDeviceToHost, s0->stream));
+        PGRT_HIP(hipMemcpyAsync(fs->host_dst, fs->host_src, fs->host_bytes, hipMemcpyDeviceToHost, s0->stream));
         PGRT_HIP(hipEventRecord(s0->ev_done, s0->stream));
     }
     PGRT_HIP(hipGetLastError());
@@ -782,7 +789,7 @@ void start_frame(pgrt_ctx* ctx, FrameSet* fs, const pgrt_render_params* p, std::
     check_frame(ctx, p);
     PGRT_REQUIRE(nframes >= 1 && nframes <= kMaxFramesPerCall, PGRT_ERR_INVALID_ARGUMENT,
                  "frames per call must be in [1, 64]");
-    PGRT_REQUIRE(!fs->host_dst || (!distributed && out == fs->host_stage.p), PGRT_ERR_INVALID_ARGUMENT,
+    PGRT_REQUIRE(!fs->host_dst || (!distributed && out == fs->host_src && out_mode == 0), PGRT_ERR_INVALID_ARGUMENT,
                  "internal: a host destination is set for a frame that does not render into the staging buffer");
     fs->t0 = std::chrono::steady_clock::now();
     fs->params = *p;
@@ -825,14 +832,31 @@ void start_frame(pgrt_ctx* ctx, FrameSet* fs, const pgrt_render_params* p, std::
 // Synchronous render of `tiles` (pending asynchronous frames complete first).
 void render_tiles(pgrt_ctx* ctx, const pgrt_render_params* p, const std::vector<int4>& tiles, float* out,
                   int out_mode, int ox, int oy, int pitch, pgrt_stats* st, int nframes,
-                  long long frame_stride) {
+                  long long frame_stride, float* host_out, size_t host_bytes) {
     drain_frames(ctx);
     FrameSet* fs = frame_set(ctx, 0);
-    fs->host_dst = nullptr;
+    // host_out: the framebuffer `out` (device) also lands in host memory of the same layout
+    set_host_output(fs, host_out, out, host_bytes);
     PGRT_HIP(hipEventRecord(fs->ev_ready, ctx->stream));  // prior context-stream work first
     start_frame(ctx, fs, p, tiles, out, out_mode, ox, oy, pitch, false, nullptr, nframes, frame_stride);
     finish_frame(ctx, fs);
     if (st) *st = fs->stats;
+}
+
+// The host destination of fs's frames (NULL: none).  Page-locked memory (hipHostMalloc /
+// hipHostRegister: it has a device-visible address) is written by the per-slot export kernels;
+// pageable memory by one SDMA copy of `bytes` after the frame.
+void set_host_output(FrameSet* fs, float* dst, float* src, size_t bytes) {
+    fs->host_dst = dst;
+    fs->host_src = dst ? src : nullptr;
+    fs->host_bytes = dst ? bytes : 0;
+    fs->host_map = nullptr;
+    if (!dst) return;
+    void* dev = nullptr;
+    if (hipHostGetDevicePointer(&dev, dst, 0) == hipSuccess && dev)
+        fs->host_map = static_cast<float*>(dev);
+    else
+        (void)hipGetLastError();  // not page-locked: the copy path
 }
 
 std::vector<int4> rect_tiles(int x0, int y0, int w, int h) {

@@ -425,6 +425,43 @@ void launch_accumulate_frame(const float* frame, float* sum, float* mean, long l
                        reinterpret_cast<float4*>(mean), pixels, count);
 }
 
+// ------------------------------------------------------------------ host framebuffer export
+//
+// SURVEY.md §8(d) times a frame to the framebuffer on the host (the reference's Producer copies
+// it under the mutex, simpleguidx11.cpp:120-124).  A blit kernel storing into page-locked host
+// memory moves 53 GB/s over PCIe where an SDMA copy of the same 33 MB moved 28-44
+// (profiles/r5/r5a/d2h_probe.txt), and one is launched per pipeline slot right after that slot's
+// finish: the bulk slot's pixels cross PCIe while the deep-tile slot is still rendering.  One wave
+// per tile row: 64 consecutive 16-B pixels, full lines on the link.
+__global__ __launch_bounds__(kBlock) void k_export_tiles(const int4* __restrict__ tiles, int rows,
+                                                         const float4* __restrict__ src, float4* __restrict__ dst,
+                                                         int ox, int oy, int pitch, long long frame_stride4,
+                                                         unsigned long long* __restrict__ stamps) {
+    PGRT_STAMP_BEGIN(stamps);
+    const int x = threadIdx.x & 63;
+    for (int r = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); r < rows; r += gridDim.x * (kBlock / 64)) {
+        const int4 tr = tiles[r >> 6];  // 64 rows per tile
+        const int ly = r & 63;
+        if (ly >= tr.w || x >= tile_width(tr)) continue;
+        const size_t o = (size_t)frame_of_tile(tr) * (size_t)frame_stride4 + (size_t)(tr.y + ly - oy) * (size_t)pitch +
+                         (size_t)(tr.x + x - ox);
+        dst[o] = ld_stream(src + o);
+    }
+    PGRT_STAMP_END(stamps);
+}
+
+void launch_export_tiles(const int4* tiles, int ntiles, const float* src, float* dst_host, int ox, int oy, int pitch,
+                         long long frame_stride, hipStream_t stream) {
+    if (ntiles <= 0) return;
+    const int rows = ntiles * kTile;
+    // 256 workgroups saturate the link (d2h_probe: 53 GB/s from 256 to 4096) and leave the CUs to
+    // the frame's other slot
+    const int grid = std::min(256, ceil_div(rows, kBlock / 64));
+    hipLaunchKernelGGL(k_export_tiles, dim3(grid), dim3(kBlock), 0, stream, tiles, rows,
+                       reinterpret_cast<const float4*>(src), reinterpret_cast<float4*>(dst_host), ox, oy, pitch,
+                       frame_stride / 4, stamp_next(kStampExportTiles, -1, grid, kBlock));
+}
+
 // ------------------------------------------------------------------ counter export
 
 // last launch of a slot's frame: the frame counters go to pinned host memory and the device

@@ -31,6 +31,7 @@ enum StampKind : int {
     kStampPathShade,
     kStampPathResolve,
     kStampSubtree,
+    kStampExportTiles,
     kStampKinds
 };
 

@@ -228,6 +228,11 @@ void launch_subtree(const SceneView& s, const FrameParams& fp, int level, Queue 
 // copy `n` FrameCounters to pinned host memory and zero them on the device
 // also copies the slot's per-tile deep flags (FrameParams::tile_deep, ndeep ints) to deep_host and
 // zeroes them on the device (deep_dev NULL: none)
+// host-output frames: a pipeline slot's finished tiles (ntiles records, frame index in each) from
+// the device framebuffer src to the same place in the page-locked host framebuffer dst_host
+// (device-visible address); framebuffer origin ox, oy, pitch in pixels, frame_stride in floats
+void launch_export_tiles(const int4* tiles, int ntiles, const float* src, float* dst_host, int ox, int oy, int pitch,
+                         long long frame_stride, hipStream_t stream);
 void launch_export_counters(FrameCounters* dev, FrameCounters* host, int n, int* deep_dev, int* deep_host, int ndeep,
                             hipStream_t stream);
 // Distributed frames: rank r's tile-compact buffer (frame-major, count[r] tiles per frame in its

@@ -873,3 +873,32 @@ def test_frames_in_flight_match_synchronous(gpu_ctx, avenger_scene):
         gpu_ctx.set_frames_in_flight(1)
         for b in bufs:
             gpu_ctx.free(b)
+
+
+def test_host_framebuffer_pinned_sync_equals_device(gpu_ctx, avenger_scene):
+    """pgrt_render into page-locked host memory: every pipeline slot exports its finished tiles
+    itself (k_export_tiles, the bulk slot while the deep-tile slot still renders) -- the host frame
+    equals the device-resident frame and the pageable-memory path bit for bit, at C2's full size
+    (the second frame takes the deep-tiles-first deal) and for a render rect."""
+    gpu_ctx.set_scene(avenger_scene)
+    W, H = 1920, 1080
+    gpu_ctx.set_camera(abi.default_camera(W, H))
+    gpu_ctx.set_frames_in_flight(1)
+    for p, (w, h) in ((abi.make_params(max_level=5), (W, H)),
+                      (abi.make_params(max_level=5, jitter=abi.PGRT_JITTER_HASH, frame=3), (W, H)),
+                      (abi.make_params(max_level=5, rect=(101, 37, 333, 190)), (333, 190))):
+        fb = gpu_ctx.alloc(w * h * 16)
+        hb = gpu_ctx.host_array((h, w, 4))
+        try:
+            for _ in range(2):  # the second synchronous frame deals the deep tiles to slot 0
+                hb.fill(-7.0)
+                gpu_ctx.render(p, out=hb)
+            gpu_ctx.render_device(p, fb)
+            dev = gpu_ctx.to_host(fb, (h, w, 4))
+            pageable, _ = gpu_ctx.render(p)
+            for name, o in (("pinned", hb), ("pageable", pageable)):
+                same = (o == dev) | (np.isnan(o) & np.isnan(dev))
+                assert same.all(), f"{name} {w}x{h}: {(~same).sum()} pixels differ"
+        finally:
+            gpu_ctx.host_free(hb)
+            gpu_ctx.free(fb)

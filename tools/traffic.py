@@ -72,6 +72,57 @@ def frame_bytes(fetch, fn, write, wn, frames_per_call, calls=5):
     }
 
 
+def roofline_kernel_trace(root, calls, out):
+    """The trace pass's closest-hit launches of exactly the profile=1 roofline calls: written to
+    <out>_kernel_trace.csv (one row per launch as bench.py times it -- a budgeted packet launch and
+    its k_trace8g<RESUME> deferral launch are one row, from the first's start to the second's
+    end), their average duration beside the bench's own avg_launch_ms (HIP events, same run)."""
+    files = glob.glob(os.path.join(root, "trace", "**", "*kernel_trace.csv"), recursive=True)
+    if not files:
+        return None
+    rows = {}
+    with open(files[0]) as fh:
+        for r in csv.DictReader(fh):
+            rows[r["Dispatch_Id"]] = r
+    names = {d: r["Kernel_Name"] for d, r in rows.items()}
+    segs = frame_calls(names, calls)
+    if not segs:
+        return None
+    is_trace = lambda n: ("k_trace" in n and "<true" not in n) or (
+        "k_subtree" in n and n.split("(")[0].rstrip().endswith("false>"))
+    is_resume = lambda n: "k_trace8g" in n and ", true>" in n.split("(")[0]
+    launches = []
+    for seg in segs:
+        for d in sorted(seg, key=int):
+            n = names[d]
+            if not is_trace(n):
+                continue
+            t0, t1 = int(rows[d]["Start_Timestamp"]), int(rows[d]["End_Timestamp"])
+            if is_resume(n) and launches:
+                launches[-1]["end"] = t1  # the deferral launch of the packet launch before it
+                launches[-1]["kernels"] += " + " + n.split("(")[0]
+                continue
+            launches.append({"dispatch": d, "kernels": n.split("(")[0], "start": t0, "end": t1})
+    path = os.path.splitext(out)[0] + "_kernel_trace.csv"
+    with open(path, "w", newline="") as fh:
+        w = csv.writer(fh)
+        w.writerow(["dispatch", "kernels", "start_ns", "end_ns", "duration_us"])
+        for l in launches:
+            w.writerow([l["dispatch"], l["kernels"], l["start"], l["end"], round((l["end"] - l["start"]) / 1e3, 3)])
+    avg_ms = sum(l["end"] - l["start"] for l in launches) / len(launches) / 1e6
+    res = {"csv": os.path.basename(path), "calls": len(segs), "launches": len(launches),
+           "launches_per_call": round(len(launches) / len(segs), 2), "avg_launch_ms": round(avg_ms, 4)}
+    logp = os.path.join(root, "trace.log")
+    if os.path.exists(logp):  # bench.py --roofline-only's own line in the same (traced) run
+        for line in open(logp):
+            if line.startswith('{"metric'):
+                b = json.loads(line).get("roofline") or {}
+                if b.get("avg_launch_ms"):
+                    res["bench_avg_launch_ms_same_run"] = b["avg_launch_ms"]
+                    res["rocprof_vs_bench"] = round(avg_ms / b["avg_launch_ms"], 4)
+    return res
+
+
 def main():
     root, out, rnd = sys.argv[1], sys.argv[2], sys.argv[3]
     workload = sys.argv[4] if len(sys.argv) > 4 else "C2 avenger-proxy 1920x1080 Whitted d=5 (bench.py default)"
@@ -90,7 +141,13 @@ def main():
     def is_resume(n):
         return "k_trace8g" in n and ", true>" in n.split("(")[0]
 
-    fids, wids = trace_ids(fn), trace_ids(wn)
+    # only the bench's profile=1 roofline calls (the segments frame_calls picks), so the bytes
+    # per launch describe exactly the launches bench.py's avg_launch_ms times
+    calls = int(os.environ.get("ROOF_CALLS", "5"))
+    in_calls = lambda names: {d for seg in frame_calls(names, calls) for d in seg}
+    fsel, wsel = in_calls(fn), in_calls(wn)
+    fids = [d for d in trace_ids(fn) if d in fsel]
+    wids = [d for d in trace_ids(wn) if d in wsel]
     f_n = max(1, sum(1 for d in fids if not is_resume(fn[d])))
     w_n = max(1, sum(1 for d in wids if not is_resume(wn[d])))
     f_kb = sum(fetch[d] for d in fids) / f_n
@@ -112,7 +169,8 @@ def main():
     gui, _ = per_dispatch(os.path.join(root, "pmc_valu"), "GRBM_GUI_ACTIVE")
     if valu:
         by = collections.defaultdict(lambda: [0.0, 0.0, 0])
-        for d in trace_ids(vn):
+        vsel = in_calls(vn)
+        for d in [d for d in trace_ids(vn) if d in vsel]:
             k = vn[d].split("(")[0].split("<")[0].strip()
             by[k][0] += valu[d]
             by[k][1] += gui.get(d, 0.0)
@@ -131,6 +189,9 @@ def main():
         res["frame"] = fr
         res["frame_note"] = ("every kernel of the profile=1 roofline calls (FETCH_SIZE x2 + WRITE_SIZE), per frame; "
                              "calls delimited by their k_export_counters dispatch")
+    kt = roofline_kernel_trace(root, calls, out)
+    if kt:
+        res["kernel_trace"] = kt
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))
