@@ -109,7 +109,7 @@ int main() {
                 return 0;
             }))
             return 1;
-        for (int grid : {256, 1024, 4096}) {
+        for (int grid : {32, 64, 128, 256, 1024}) {
             for (int nc = 0; nc < 2; ++nc) {
                 float4* hp;
                 CK(hipHostGetDevicePointer((void**)&hp, nc ? (void*)host_nc : (void*)host_def, 0));

@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--cfg", action="append", default=[])
+    ap.add_argument("--host", action="store_true", help="also frames to page-locked host memory (sync and async)")
     a = ap.parse_args()
     sc = load_obj(scenes.AVENGER_OBJ)
     sc.set_environment(os.path.join(ROOT, "assets", "spherical_map_windows.jpg"))
@@ -92,6 +93,77 @@ def main():
         "frames": len(spans),
         "launches": rel(by_ticket[med_t], t0),
     }
+
+    # ---- sync_host / async_host: frames to page-locked host memory (SURVEY §8(d)'s ms/frame) ----
+    if a.host:
+        hb = ctx.host_array((H, W, 4))
+
+        def sync_host(n, on):
+            ctx.set_frames_in_flight(1)
+            ctx.timeline_enable(on)
+            lat = []
+            for k in range(n):
+                p = abi.RenderParams.from_buffer_copy(base)
+                p.frame = 2000 + k
+                t = time.perf_counter()
+                ctx.render(p, out=hb)
+                lat.append((time.perf_counter() - t) * 1e3)
+            return lat
+
+        sync_host(3, False)
+        h_off = sync_host(a.reps, False)
+        ctx.timeline_read()
+        h_on = sync_host(a.reps, True)
+        recs = ctx.timeline_read()
+        ctx.timeline_enable(False)
+        ctx.host_free(hb)
+        by_ticket = {}
+        for r in recs:
+            by_ticket.setdefault(r["ticket"], []).append(r)
+        spans = {t: (max(r["us_end"] for r in rs) - min(r["us_start"] for r in rs)) for t, rs in by_ticket.items()}
+        med_t = sorted(spans, key=lambda t: spans[t])[len(spans) // 2]
+        t0 = min(r["us_start"] for r in by_ticket[med_t])
+        results["sync_host"] = {
+            "workload": "C2, one synchronous frame at a time into a page-locked host framebuffer (pgrt_render)",
+            "host_ms_median_timeline_off": round(statistics.median(h_off), 4),
+            "host_ms_median_timeline_on": round(statistics.median(h_on), 4),
+            "device_span_ms_median": round(spans[med_t] / 1e3, 4),
+            "frames": len(spans),
+            "launches": rel(by_ticket[med_t], t0),
+        }
+        ring = 4
+        bufs = [ctx.host_array((F, H, W, 4)) for _ in range(ring)]
+        ctx.set_frames_in_flight(ring)
+
+        def host_calls(n, on):
+            ctx.timeline_enable(on)
+            pend = deque()
+            t = time.perf_counter()
+            for k in range(n):
+                p = abi.RenderParams.from_buffer_copy(base)
+                p.frame = 3000 + k * F
+                pend.append(ctx.render_frames_host_async(p, F, bufs[k % ring]))
+                if len(pend) >= ring:
+                    ctx.render_wait(pend.popleft())
+            while pend:
+                ctx.render_wait(pend.popleft())
+            return (time.perf_counter() - t) * 1e3
+
+        host_calls(ring, False)
+        dt_off = host_calls(12, False)
+        ctx.timeline_read()
+        dt_on = host_calls(12, True)
+        recs = ctx.timeline_read()
+        ctx.timeline_enable(False)
+        for b in bufs:
+            ctx.host_free(b)
+        t0 = min(r["us_start"] for r in recs)
+        results["async_host"] = {
+            "workload": f"C2, 12 calls of {F} frames to page-locked host memory, {ring} in flight (pgrt_render_frames_host_async)",
+            "ms_per_frame_timeline_off": round(dt_off / (12 * F), 4),
+            "ms_per_frame_timeline_on": round(dt_on / (12 * F), 4),
+            "launches": [r for r in rel(recs, t0) if r["kind"] in ("host_export", "finish", "trace_pkt", "export")],
+        }
 
     # ---- r20: the driver's timed region ----
     ctx.set_frames_in_flight(IN_FLIGHT)
