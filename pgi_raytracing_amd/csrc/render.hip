@@ -454,9 +454,11 @@ void launch_export_tiles(const int4* tiles, int ntiles, const float* src, float*
                          long long frame_stride, hipStream_t stream) {
     if (ntiles <= 0) return;
     const int rows = ntiles * kTile;
-    // 256 workgroups saturate the link (d2h_probe: 53 GB/s from 256 to 4096) and leave the CUs to
-    // the frame's other slot
-    const int grid = std::min(256, ceil_div(rows, kBlock / 64));
+    // 256 workgroups saturate the link (d2h_probe: 53 GB/s from 64 to 1024 workgroups)
+#ifndef PGRT_EXPORT_GRID
+#define PGRT_EXPORT_GRID 256
+#endif
+    const int grid = std::min(PGRT_EXPORT_GRID, ceil_div(rows, kBlock / 64));
     hipLaunchKernelGGL(k_export_tiles, dim3(grid), dim3(kBlock), 0, stream, tiles, rows,
                        reinterpret_cast<const float4*>(src), reinterpret_cast<float4*>(dst_host), ox, oy, pitch,
                        frame_stride / 4, stamp_next(kStampExportTiles, -1, grid, kBlock));
