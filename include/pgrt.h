@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PGRT_ABI_VERSION 1
+#define PGRT_ABI_VERSION 2 /* 2 (round 5): pgrt_config carries its size (checked) and host_export */
 
 #define PGRT_OK 0
 #define PGRT_ERR_INVALID_ARGUMENT (-1)
@@ -176,7 +176,12 @@ typedef struct pgrt_bvh_info {
 #define PGRT_BVH_PLOC 2           /* PLOC clustering over the Morton order + SAH leaf collapse */
 #define PGRT_PACKETS_AUTO 0       /* per level, from the measured packet efficiency (default) */
 #define PGRT_PACKETS_OFF (-1)     /* every level one lane per ray */
+#define PGRT_HOST_EXPORT_KERNEL 1 /* host frames: per-slot export kernels into page-locked memory */
+#define PGRT_HOST_EXPORT_COPY (-1) /* host frames: one device-to-host copy after the frame */
 typedef struct pgrt_config {
+    unsigned size;        /* sizeof(pgrt_config) of the caller's pgrt.h: pgrt_get_config fills it, and
+                             pgrt_set_config rejects any other value (a caller built against another
+                             layout fails loudly instead of writing fields into the wrong places) */
     int bvh_builder;      /* 0 = PGRT_BVH_PLOC (default), PGRT_BVH_LBVH; applied by pgrt_set_scene */
     int bvh_width;        /* 0 or 2: binary traversal layout (default); 8: quantized 8-wide for
                              every queue.  The 8-wide layout is always built for small queues. */
@@ -212,6 +217,14 @@ typedef struct pgrt_config {
                              size form the first slot, so the deep reflection / refraction levels
                              (the frame's critical path) start after a short level 0 while the
                              other slot's level 0 still runs; -1 = tiles dealt round-robin */
+    int host_export;    /* frames into page-locked host memory (pgrt_render,
+                             pgrt_render_frames_host_async): 0 = default -- a synchronous two-slot
+                             frame exports each slot's finished tiles with a small blit kernel as
+                             soon as that slot is done (the bulk slot's pixels cross PCIe while the
+                             deep-tile slot still renders), frames in flight take one DMA copy per
+                             call; PGRT_HOST_EXPORT_KERNEL = export kernels always;
+                             PGRT_HOST_EXPORT_COPY = one DMA copy after every frame; 2 = per-slot
+                             DMA copies of the slot's tile runs (A/B) */
 } pgrt_config;
 
 /* ---- context ---- */

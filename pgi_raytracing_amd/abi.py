@@ -117,6 +117,7 @@ PGRT_PACKETS_AUTO, PGRT_PACKETS_OFF = 0, -1
 class Config(C.Structure):
     """pgrt_config: speed-only choices (frames are bit-identical for every value)."""
     _fields_ = [
+        ("size", C.c_uint),
         ("bvh_builder", C.c_int),
         ("bvh_width", C.c_int),
         ("split_beta", C.c_float),
@@ -130,6 +131,7 @@ class Config(C.Structure):
         ("subtree_level", C.c_int),
         ("call_order", C.c_int),
         ("tile_order", C.c_int),
+        ("host_export", C.c_int),
     ]
 
 

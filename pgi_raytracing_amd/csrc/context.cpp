@@ -10,7 +10,7 @@ using namespace pgrt;
 
 extern "C" {
 
-const char* pgrt_version(void) { return "pgrt 0.1.0 (gfx950, abi 1)"; }
+const char* pgrt_version(void) { return "pgrt 0.2.0 (gfx950, abi 2)"; }
 
 int pgrt_device_count(int* count) {
     if (!count) return PGRT_ERR_INVALID_ARGUMENT;
@@ -29,6 +29,7 @@ int pgrt_create(int hip_device, pgrt_ctx** out) {
     pgrt_ctx* ctx = new (std::nothrow) pgrt_ctx();
     if (!ctx) return PGRT_ERR_OUT_OF_MEMORY;
     ctx->device = hip_device;
+    ctx->cfg.size = sizeof(pgrt_config);
     if (const char* e = getenv("PGRT_EMULATE_RANK")) {
         int r = 0, w = 1;
         if (sscanf(e, "%d/%d", &r, &w) == 2 && w >= 1 && w <= kMaxRanks && r >= 0 && r < w) {
@@ -101,12 +102,19 @@ const char* pgrt_last_error(const pgrt_ctx* ctx) { return ctx ? ctx->err.c_str()
 int pgrt_get_config(const pgrt_ctx* ctx, pgrt_config* cfg) {
     if (!ctx || !cfg) return PGRT_ERR_INVALID_ARGUMENT;
     *cfg = ctx->cfg;
+    cfg->size = sizeof(pgrt_config);
     return PGRT_OK;
 }
 
 int pgrt_set_config(pgrt_ctx* ctx, const pgrt_config* cfg) {
     if (!ctx || !cfg) return PGRT_ERR_INVALID_ARGUMENT;
     return guarded(ctx, [&] {
+        PGRT_REQUIRE(cfg->size == sizeof(pgrt_config), PGRT_ERR_INVALID_ARGUMENT,
+                     "pgrt_config.size is " + std::to_string(cfg->size) + ", this library's pgrt_config has " +
+                         std::to_string(sizeof(pgrt_config)) + " bytes (abi " + std::to_string(PGRT_ABI_VERSION) +
+                         "): start from pgrt_get_config");
+        PGRT_REQUIRE(cfg->host_export >= -1 && cfg->host_export <= 2, PGRT_ERR_INVALID_ARGUMENT,
+                     "host_export must be 0, PGRT_HOST_EXPORT_KERNEL, PGRT_HOST_EXPORT_COPY or 2");
         PGRT_REQUIRE(cfg->bvh_builder == 0 || cfg->bvh_builder == PGRT_BVH_LBVH || cfg->bvh_builder == PGRT_BVH_PLOC,
                      PGRT_ERR_INVALID_ARGUMENT, "bvh_builder must be 0, PGRT_BVH_LBVH or PGRT_BVH_PLOC");
         PGRT_REQUIRE(cfg->bvh_width == 0 || cfg->bvh_width == 2 || cfg->bvh_width == 8, PGRT_ERR_INVALID_ARGUMENT,

@@ -269,6 +269,46 @@ void probe_side_launch(pgrt_ctx* ctx, const SceneView& view, FrameSlot* sl, Fram
     launch_trace(view, pr, s);
 }
 
+// How a host-output frame's pixels reach host memory (pgrt_config.host_export).  Per slot -- right
+// after the slot's finish, so the bulk slot's pixels cross PCIe while the deep-tile slot of a
+// synchronous frame still renders -- by the export kernel (page-locked destinations only) or by
+// DMA copies of the slot's tile runs; otherwise one DMA copy after every slot.  r5d A/B (same box,
+// profiles/r5): one synchronous C2 frame into page-locked memory 1.69 ms with one copy after the
+// frame, 1.02 with per-slot export kernels of 32 workgroups (1.14 with 256: the kernel's PCIe stores
+// stall the memory pipelines of the CUs the deep-tile slot also runs on); calls in flight 0.60-0.64
+// ms/frame with one DMA copy per call, 0.75 with export kernels (their stores slow the other calls'
+// rendering), so frames in flight keep the copy.
+enum { kHostNone = 0, kHostKernel = 1, kHostRuns = 2, kHostOnce = 3 };
+int host_export_mode(const pgrt_ctx* ctx, const FrameSet* fs, int K) {
+    if (!fs->host_dst || K == 0) return kHostNone;
+    const int c = ctx->cfg.host_export;
+    if (c == PGRT_HOST_EXPORT_COPY) return kHostOnce;
+    if (c == PGRT_HOST_EXPORT_KERNEL) return fs->host_map ? kHostKernel : kHostOnce;
+    if (c == 2) return K > 1 ? kHostRuns : kHostOnce;
+    return fs->host_map && K > 1 ? kHostKernel : kHostOnce;
+}
+
+// DMA copies of a slot's tiles into the host framebuffer: one 2D copy per run of horizontally
+// adjacent tiles of one tile row (the deal keeps row-major order)
+void copy_tile_runs(FrameSet* fs, const std::vector<int4>& tiles, hipStream_t s) {
+    const size_t pitch_b = (size_t)fs->pitch * 4 * sizeof(float);
+    for (size_t a = 0; a < tiles.size();) {
+        size_t b = a + 1;
+        int w = tile_width(tiles[a]);
+        while (b < tiles.size() && tiles[b].y == tiles[a].y && tiles[b].w == tiles[a].w &&
+               frame_of_tile(tiles[b]) == frame_of_tile(tiles[a]) && tiles[b].x == tiles[a].x + w) {
+            w += tile_width(tiles[b]);
+            ++b;
+        }
+        const int4& t = tiles[a];
+        const size_t off = (size_t)frame_of_tile(t) * (size_t)fs->frame_stride +
+                           ((size_t)(t.y - fs->oy) * (size_t)fs->pitch + (size_t)(t.x - fs->ox)) * 4;
+        PGRT_HIP(hipMemcpy2DAsync(fs->host_dst + off, pitch_b, fs->host_src + off, pitch_b,
+                                  (size_t)w * 4 * sizeof(float), (size_t)t.w, hipMemcpyDeviceToHost, s));
+        a = b;
+    }
+}
+
 // One sample batch of a PGRT_MODE_PATH frame (path.hip): raygen, then per bounce L the closest
 // hits of the path queue, the bounce's shading, its shadow rays and their resolve; the finish
 // sums each pixel's path accumulators (a resolved level 0) and writes the output like a Whitted
@@ -379,6 +419,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
     fs->batches = 0;
     while ((int)fs->slots.size() < K) fs->slots.emplace_back(new FrameSlot(fs->slots.empty()));
     const std::vector<std::vector<int4>> deal = deal_tiles(ctx, fs, K);
+    const int hx = host_export_mode(ctx, fs, K);
     // launch timeline (pgrt_timeline_enable): every launch of this call stamps its waves into
     // fs->stamps, the slot ranges handed out by the launchers through the stamp log
     StampLog slog;
@@ -584,11 +625,14 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             debug_sync(s, "finish", 0, bi);
             ctx->timer.end(s, id);
         }
-        if (fs->host_map) {  // this slot's final pixels -> the page-locked host framebuffer, now
+        if (hx != kHostOnce) {  // this slot's final pixels -> the host framebuffer, now
             PGRT_REQUIRE(fs->out_mode == 0 && fs->out == fs->host_src, PGRT_ERR_INVALID_ARGUMENT,
                          "internal: host export of a frame that is not rendered into its staging framebuffer");
-            launch_export_tiles(sl->tiles.p, nt, fs->host_src, fs->host_map, fs->ox, fs->oy, fs->pitch,
-                                fs->frame_stride, s);
+            if (hx == kHostKernel)
+                launch_export_tiles(sl->tiles.p, nt, fs->host_src, fs->host_map, fs->ox, fs->oy, fs->pitch,
+                                    fs->frame_stride, s);
+            else
+                copy_tile_runs(fs, deal[j], s);
             debug_sync(s, "host export", 0, 0);
         }
         sl->host_fc.resize(batches);
@@ -598,7 +642,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
         debug_sync(s, "export", 0, 0);
         PGRT_HIP(hipEventRecord(sl->ev_done, s));
     }
-    if (fs->host_dst && !fs->host_map && K > 0) {  // pageable host output: after every slot, on slot 0's stream
+    if (fs->host_dst && hx == kHostOnce && K > 0) {  // one copy after every slot, on slot 0's stream
         FrameSlot* s0 = fs->slots[0].get();
         for (int j = 1; j < K; ++j) PGRT_HIP(hipStreamWaitEvent(s0->stream, fs->slots[j]->ev_done, 0));
         PGRT_HIP(hipMemcpyAsync(fs->host_dst, fs->host_src, fs->host_bytes, hipMemcpyDeviceToHost, s0->stream));

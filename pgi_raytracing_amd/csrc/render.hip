@@ -454,9 +454,11 @@ void launch_export_tiles(const int4* tiles, int ntiles, const float* src, float*
                          long long frame_stride, hipStream_t stream) {
     if (ntiles <= 0) return;
     const int rows = ntiles * kTile;
-    // 256 workgroups saturate the link (d2h_probe: 53 GB/s from 64 to 1024 workgroups)
+    // 32 workgroups: 44-51 GB/s on the link alone (d2h_probe; 53 from 64 up), and the fewest CUs
+    // whose memory pipelines wait behind PCIe stores (r5d: synchronous host frame 1.02 ms at 32,
+    // 1.12 at 64, 1.14 at 256, 1.32 at 8)
 #ifndef PGRT_EXPORT_GRID
-#define PGRT_EXPORT_GRID 256
+#define PGRT_EXPORT_GRID 32
 #endif
     const int grid = std::min(PGRT_EXPORT_GRID, ceil_div(rows, kBlock / 64));
     hipLaunchKernelGGL(k_export_tiles, dim3(grid), dim3(kBlock), 0, stream, tiles, rows,

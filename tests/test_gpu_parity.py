@@ -5,6 +5,8 @@ Integer/index results (hit primitive ids) must be bit-exact.  GPU and oracle sha
 operation order and pgrt_detmath.h, so in practice every pixel is bit-identical; the tests
 report the exact-match fraction and require it to be 1 for the hit records.
 """
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -884,6 +886,13 @@ def test_host_framebuffer_pinned_sync_equals_device(gpu_ctx, avenger_scene):
     W, H = 1920, 1080
     gpu_ctx.set_camera(abi.default_camera(W, H))
     gpu_ctx.set_frames_in_flight(1)
+    for mode in (0, 1, -1, 2):  # pgrt_config.host_export: default, kernels, one copy, per-slot copies
+        gpu_ctx.configure(host_export=mode)
+        _host_frames_equal_device(gpu_ctx, W, H)
+    gpu_ctx.configure(host_export=0)
+
+
+def _host_frames_equal_device(gpu_ctx, W, H):
     for p, (w, h) in ((abi.make_params(max_level=5), (W, H)),
                       (abi.make_params(max_level=5, jitter=abi.PGRT_JITTER_HASH, frame=3), (W, H)),
                       (abi.make_params(max_level=5, rect=(101, 37, 333, 190)), (333, 190))):
@@ -902,3 +911,22 @@ def test_host_framebuffer_pinned_sync_equals_device(gpu_ctx, avenger_scene):
         finally:
             gpu_ctx.host_free(hb)
             gpu_ctx.free(fb)
+
+
+def test_config_size_is_checked(gpu_ctx):
+    """pgrt_config carries its size (abi 2): pgrt_get_config fills it, pgrt_set_config rejects a
+    struct of another layout instead of writing its fields into the wrong places."""
+    from pgi_raytracing_amd.raytracer import PgrtError
+
+    cfg = gpu_ctx.get_config()
+    assert cfg.size == C.sizeof(abi.Config)
+    assert b"abi 2" in gpu_ctx.L.pgrt_version()
+    bad = abi.Config.from_buffer_copy(cfg)
+    bad.size = cfg.size - 4
+    with pytest.raises(PgrtError, match="pgrt_config.size"):
+        gpu_ctx.set_config(bad)
+    bad = abi.Config.from_buffer_copy(cfg)
+    bad.host_export = 5
+    with pytest.raises(PgrtError):
+        gpu_ctx.set_config(bad)
+    gpu_ctx.set_config(cfg)

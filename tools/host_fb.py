@@ -29,14 +29,18 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--async", dest="asy", nargs="*", default=["8x4"])
     ap.add_argument("--frames", type=int, default=96, help="frames per async measurement")
+    ap.add_argument("--cfg", action="append", default=[], help="pgrt_config field=value")
     a = ap.parse_args()
     sc = load_obj(scenes.AVENGER_OBJ)
     sc.set_environment(os.path.join(ROOT, "assets", "spherical_map_windows.jpg"))
     ctx = Context(0)
+    for kv in a.cfg:
+        k, v = kv.split("=", 1)
+        ctx.configure(**{k: int(v)})
     ctx.set_scene(sc)
     ctx.set_camera(abi.default_camera(W, H))
     p = abi.make_params(max_level=5)
-    out = {"lib": os.environ.get("PGRT_LIB", "in-tree")}
+    out = {"lib": os.environ.get("PGRT_LIB", "in-tree"), "cfg": a.cfg}
     hb = ctx.host_array((H, W, 4))
     ctx.set_frames_in_flight(1)
     for _ in range(3):
