@@ -223,8 +223,8 @@ typedef struct pgrt_config {
                              soon as that slot is done (the bulk slot's pixels cross PCIe while the
                              deep-tile slot still renders), frames in flight take one DMA copy per
                              call; PGRT_HOST_EXPORT_KERNEL = export kernels always;
-                             PGRT_HOST_EXPORT_COPY = one DMA copy after every frame; 2 = per-slot
-                             DMA copies of the slot's tile runs (A/B) */
+                             PGRT_HOST_EXPORT_COPY = one DMA copy after every frame (pageable
+                             destinations always take the copy) */
 } pgrt_config;
 
 /* ---- context ---- */

@@ -269,44 +269,22 @@ void probe_side_launch(pgrt_ctx* ctx, const SceneView& view, FrameSlot* sl, Fram
     launch_trace(view, pr, s);
 }
 
-// How a host-output frame's pixels reach host memory (pgrt_config.host_export).  Per slot -- right
-// after the slot's finish, so the bulk slot's pixels cross PCIe while the deep-tile slot of a
-// synchronous frame still renders -- by the export kernel (page-locked destinations only) or by
-// DMA copies of the slot's tile runs; otherwise one DMA copy after every slot.  r5d A/B (same box,
-// profiles/r5): one synchronous C2 frame into page-locked memory 1.69 ms with one copy after the
-// frame, 1.02 with per-slot export kernels of 32 workgroups (1.14 with 256: the kernel's PCIe stores
-// stall the memory pipelines of the CUs the deep-tile slot also runs on); calls in flight 0.60-0.64
-// ms/frame with one DMA copy per call, 0.75 with export kernels (their stores slow the other calls'
-// rendering), so frames in flight keep the copy.
-enum { kHostNone = 0, kHostKernel = 1, kHostRuns = 2, kHostOnce = 3 };
+// How a host-output frame's pixels reach host memory (pgrt_config.host_export): per slot by the
+// export kernel (page-locked destinations only), right after the slot's finish -- so the bulk
+// slot's pixels cross PCIe while the deep-tile slot of a synchronous frame still renders -- or by
+// one DMA copy after every slot.  r5d / r5e A/B (same box, profiles/r5): one synchronous C2 frame
+// into page-locked memory 1.69 ms with one copy after the frame, 1.02 with per-slot export kernels
+// of 32 workgroups (1.14 with 256: the kernel's PCIe stores stall the memory pipelines of CUs the
+// deep-tile slot also runs on), 5.2 with per-slot DMA copies of the slot's tile runs (2D copies);
+// calls in flight 0.61-0.65 ms/frame with one DMA copy per call, 0.76-0.83 with export kernels
+// (their stores slow the other calls' rendering), so frames in flight keep the copy.
+enum { kHostNone = 0, kHostKernel = 1, kHostOnce = 2 };
 int host_export_mode(const pgrt_ctx* ctx, const FrameSet* fs, int K) {
     if (!fs->host_dst || K == 0) return kHostNone;
     const int c = ctx->cfg.host_export;
-    if (c == PGRT_HOST_EXPORT_COPY) return kHostOnce;
-    if (c == PGRT_HOST_EXPORT_KERNEL) return fs->host_map ? kHostKernel : kHostOnce;
-    if (c == 2) return K > 1 ? kHostRuns : kHostOnce;
-    return fs->host_map && K > 1 ? kHostKernel : kHostOnce;
-}
-
-// DMA copies of a slot's tiles into the host framebuffer: one 2D copy per run of horizontally
-// adjacent tiles of one tile row (the deal keeps row-major order)
-void copy_tile_runs(FrameSet* fs, const std::vector<int4>& tiles, hipStream_t s) {
-    const size_t pitch_b = (size_t)fs->pitch * 4 * sizeof(float);
-    for (size_t a = 0; a < tiles.size();) {
-        size_t b = a + 1;
-        int w = tile_width(tiles[a]);
-        while (b < tiles.size() && tiles[b].y == tiles[a].y && tiles[b].w == tiles[a].w &&
-               frame_of_tile(tiles[b]) == frame_of_tile(tiles[a]) && tiles[b].x == tiles[a].x + w) {
-            w += tile_width(tiles[b]);
-            ++b;
-        }
-        const int4& t = tiles[a];
-        const size_t off = (size_t)frame_of_tile(t) * (size_t)fs->frame_stride +
-                           ((size_t)(t.y - fs->oy) * (size_t)fs->pitch + (size_t)(t.x - fs->ox)) * 4;
-        PGRT_HIP(hipMemcpy2DAsync(fs->host_dst + off, pitch_b, fs->host_src + off, pitch_b,
-                                  (size_t)w * 4 * sizeof(float), (size_t)t.w, hipMemcpyDeviceToHost, s));
-        a = b;
-    }
+    if (c == PGRT_HOST_EXPORT_COPY || !fs->host_map) return kHostOnce;
+    if (c == PGRT_HOST_EXPORT_KERNEL) return kHostKernel;
+    return K > 1 ? kHostKernel : kHostOnce;
 }
 
 // One sample batch of a PGRT_MODE_PATH frame (path.hip): raygen, then per bounce L the closest
@@ -625,14 +603,11 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             debug_sync(s, "finish", 0, bi);
             ctx->timer.end(s, id);
         }
-        if (hx != kHostOnce) {  // this slot's final pixels -> the host framebuffer, now
+        if (hx == kHostKernel) {  // this slot's final pixels -> the page-locked host framebuffer, now
             PGRT_REQUIRE(fs->out_mode == 0 && fs->out == fs->host_src, PGRT_ERR_INVALID_ARGUMENT,
                          "internal: host export of a frame that is not rendered into its staging framebuffer");
-            if (hx == kHostKernel)
-                launch_export_tiles(sl->tiles.p, nt, fs->host_src, fs->host_map, fs->ox, fs->oy, fs->pitch,
-                                    fs->frame_stride, s);
-            else
-                copy_tile_runs(fs, deal[j], s);
+            launch_export_tiles(sl->tiles.p, nt, fs->host_src, fs->host_map, fs->ox, fs->oy, fs->pitch,
+                                fs->frame_stride, s);
             debug_sync(s, "host export", 0, 0);
         }
         sl->host_fc.resize(batches);

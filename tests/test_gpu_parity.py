@@ -886,7 +886,7 @@ def test_host_framebuffer_pinned_sync_equals_device(gpu_ctx, avenger_scene):
     W, H = 1920, 1080
     gpu_ctx.set_camera(abi.default_camera(W, H))
     gpu_ctx.set_frames_in_flight(1)
-    for mode in (0, 1, -1, 2):  # pgrt_config.host_export: default, kernels, one copy, per-slot copies
+    for mode in (0, 1, -1):  # pgrt_config.host_export: default, export kernels, one copy
         gpu_ctx.configure(host_export=mode)
         _host_frames_equal_device(gpu_ctx, W, H)
     gpu_ctx.configure(host_export=0)
