@@ -290,6 +290,7 @@ __global__ __launch_bounds__(kSubtreeBlock) void k_subtree_ws(SceneView s, Frame
     float4 o4 = make_float4(0, 0, 0, 0), d4 = make_float4(0, 0, 0, -1.0f);
     float rtime = 0.0f;
     int L = level, h = 0, tg = gib;
+    unsigned idle_polls = 0;
     for (;;) {
         if (!have) {
             // (a) a published refraction child of any tree of the block
@@ -330,6 +331,19 @@ __global__ __launch_bounds__(kSubtreeBlock) void k_subtree_ws(SceneView s, Frame
         }
         if (!have) {
             if (lds_load(&exhausted) == kGroups && lds_load(&live_trees) == 0) break;
+            // safety net: the block's trees settle within microseconds of the last ray; a group
+            // still polling after ~2^22 sleeps (> 0.1 s) reports it and leaves (the frame fails
+            // loudly instead of hanging the GPU)
+            if (++idle_polls > (1u << 22)) {
+                if (k == 0) atomicOr(&fc->watchdog, 1);
+#ifdef PGRT_WS_DEBUG
+                if (k == 0 && blockIdx.x < 2)
+                    printf("ws watchdog blk %d grp %d out %d busy %d live %d exh %d n %d next %d bits %08x %08x\n",
+                           blockIdx.x, gib, (int)out_of_rays, home_busy[gib], live_trees, exhausted, n, next_home,
+                           task_bits[0], task_bits[1 % kTaskWords]);
+#endif
+                break;
+            }
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
