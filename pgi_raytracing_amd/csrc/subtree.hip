@@ -329,9 +329,13 @@ __global__ __launch_bounds__(kSubtreeBlock) void k_subtree_ws(SceneView s, Frame
                 }
             }
         }
-        if (!have) {
+        // Only a WHOLE idle wave polls / sleeps / leaves (a wave-uniform branch): were the idle
+        // groups' polling a divergent path, the compiler may turn it into an inner loop that runs
+        // with the busy groups of the same wave masked off -- and a busy group can be the very one
+        // whose refraction task or root an idle group waits for (measured: a deadlock, r5g)
+        if (__ballot(have) == 0ull) {
             if (lds_load(&exhausted) == kGroups && lds_load(&live_trees) == 0) break;
-            // safety net: the block's trees settle within microseconds of the last ray; a group
+            // safety net: the block's trees settle within microseconds of the last ray; a wave
             // still polling after ~2^22 sleeps (> 0.1 s) reports it and leaves (the frame fails
             // loudly instead of hanging the GPU)
             if (++idle_polls > (1u << 22)) {
@@ -347,6 +351,7 @@ __global__ __launch_bounds__(kSubtreeBlock) void k_subtree_ws(SceneView s, Frame
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
+        if (!have) continue;  // this group idles while others of its wave work (no inner loop)
         // ---- one ray: its closest hit, then trace()'s body for it ----
         float bt = d4.w, bu = 0.0f, bv = 0.0f;
         int bp = -1;
