@@ -659,8 +659,6 @@ bool read_frame_counters(pgrt_ctx* ctx, FrameSet* fs) {
         FrameSlot* sl = fs->slots[j].get();
         for (auto& h : sl->host_fc) {
             overflow |= h.overflow != 0;
-            PGRT_REQUIRE(h.watchdog == 0, PGRT_ERR_HIP,
-                         "a work-sharing subtree block gave up waiting for its ray trees (subtree.hip watchdog)");
             ctx->last_fc.push_back(h);
         }
         int shadow_need = 0;

@@ -21,8 +21,7 @@ struct FrameCounters {
     // them through fc_count / fc_shadow.
     int count0;
     int overflow;                        // set when an emit exceeded a queue capacity
-    int watchdog;                        // a work-sharing subtree block gave up waiting (never expected)
-    int pad0;
+    int pad0[2];
     unsigned long long alloc[kMaxLevels];
     // statistics only (fire-and-forget atomics), on cache lines of their own so they never
     // serialise with the allocation atomics
