@@ -439,7 +439,15 @@ __global__ __launch_bounds__(kBlock) void k_export_tiles(const int4* __restrict_
                                                          unsigned long long* __restrict__ stamps) {
     PGRT_STAMP_BEGIN(stamps);
     const int x = threadIdx.x & 63;
+#ifdef PGRT_EXPORT_XCD  // A/B: only the workgroups dispatched to XCD 0 (blockIdx % 8 == 0) copy
+    if (blockIdx.x % 8 != 0) {
+        PGRT_STAMP_END(stamps);
+        return;
+    }
+    for (int r = (blockIdx.x / 8) * (kBlock / 64) + (threadIdx.x >> 6); r < rows; r += (gridDim.x / 8) * (kBlock / 64)) {
+#else
     for (int r = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); r < rows; r += gridDim.x * (kBlock / 64)) {
+#endif
         const int4 tr = tiles[r >> 6];  // 64 rows per tile
         const int ly = r & 63;
         if (ly >= tr.w || x >= tile_width(tr)) continue;
