@@ -496,6 +496,7 @@ def main():
                 recs = ctx.timeline_read()
             finally:
                 ctx.timeline_enable(False)
+            recs = [r for r in recs if r["waves"] > 0]  # (a "dropped" marker: stamp buffer full)
             iv = sorted((r["us_start"], r["us_end"]) for r in recs if r["kind"] in TRACE_KINDS)
             busy, cur = 0.0, None
             for a, b in iv:

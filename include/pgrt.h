@@ -465,6 +465,8 @@ int pgrt_frame_diag(const pgrt_ctx* ctx, pgrt_level_diag* out, int max_levels);
 #define PGRT_TL_PATH_RESOLVE 12
 #define PGRT_TL_SUBTREE 13      /* the deep levels as one launch (pgrt_config.subtree_level) */
 #define PGRT_TL_HOST_EXPORT 14  /* a slot's finished tiles to a page-locked host framebuffer */
+#define PGRT_TL_DROPPED 15      /* marker: this call had more waves than the stamp buffer holds (4M);
+                                   its later launches are not recorded */
 typedef struct pgrt_timeline_rec {
     uint64_t ticket;     /* the call (the ticket an asynchronous call returned; synchronous calls count too) */
     int slot;            /* pipeline slot (stream) of the call */

@@ -177,7 +177,7 @@ class LevelDiag(C.Structure):
 
 
 TIMELINE_KINDS = ("raygen", "trace_pkt", "trace", "trace_8g", "trace_resume", "trace_shadow", "shade", "combine",
-                  "finish", "export", "unpack", "path_shade", "path_resolve", "subtree", "host_export")  # PGRT_TL_*
+                  "finish", "export", "unpack", "path_shade", "path_resolve", "subtree", "host_export", "dropped")  # PGRT_TL_*
 
 
 class TimelineRec(C.Structure):

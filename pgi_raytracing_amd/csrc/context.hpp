@@ -176,6 +176,7 @@ struct FrameSlot {
     int expect_count[kMaxLevels] = {0};  // grid hints from the previous frame (0 = unknown)
     int expect_defer[kMaxLevels] = {0};
     int expect_shadow_total = 0;
+    int sub_first = -1;  // the last frame's subtree level (its shadow rays never enter the shadow queue)
     // first: the frame's slot 0 -- the deep tiles of a synchronous frame (deal_tiles), whose chain
     // of small latency-bound launches is the frame's critical path -- on a high-priority stream,
     // so its launches take CUs before slot 1's level-0 blocks
@@ -243,7 +244,9 @@ struct FrameSet {
     // copied to host memory behind the unpack, ev_flags) -- the re-render agreement without a
     // control collective
     hipEvent_t ev_flags = nullptr;
-    int* peer_flags = nullptr;  // pinned, kMaxRanks words
+    int* peer_flags = nullptr;  // pinned: kMaxRanks flag words, then kMaxRanks sequence words
+    unsigned gather_seq = 0;    // this rank's distributed-frame sequence number of the frame
+    bool poison = false;        // this rank gave up on the frame (its send carries flag 2)
     // a re-gather after an overflow (rank 0): receive / unpack only the ranks marked here
     bool regather = false;
     char regather_peer[kMaxRanks] = {};
@@ -251,14 +254,15 @@ struct FrameSet {
     DevBuf<unsigned long long> stamps;
     std::vector<StampLaunch> stamp_launches;
     long long stamp_used = 0;
+    bool stamp_overflow = false;  // the call had more waves than the buffer: later launches unrecorded
     FrameSet() {
         PGRT_HIP(hipEventCreateWithFlags(&ev_ready, hipEventDisableTiming));
         PGRT_HIP(hipEventCreate(&ev_g0));
         PGRT_HIP(hipEventCreate(&ev_g1));
         PGRT_HIP(hipEventCreate(&ev_g2));
         PGRT_HIP(hipEventCreateWithFlags(&ev_flags, hipEventDisableTiming));
-        PGRT_HIP(hipHostMalloc((void**)&peer_flags, sizeof(int) * kMaxRanks, hipHostMallocMapped | hipHostMallocCoherent));
-        std::fill(peer_flags, peer_flags + kMaxRanks, 0);
+        PGRT_HIP(hipHostMalloc((void**)&peer_flags, sizeof(int) * 2 * kMaxRanks, hipHostMallocMapped | hipHostMallocCoherent));
+        std::fill(peer_flags, peer_flags + 2 * kMaxRanks, 0);
     }
     ~FrameSet() {
         for (auto& s : slots)
@@ -334,6 +338,7 @@ struct pgrt_ctx {
     // multi-GPU
     ncclComm_t comm = nullptr;
     int world = 1, rank = 0;
+    unsigned gather_count = 0;  // distributed frames submitted (the gather tail's sequence number)
     // PGRT_EMULATE_RANK=r/N (measurement tool only, no communicator): distributed frames render
     // rank r's share of an N-GPU frame on this device; the gather becomes a device copy of this
     // rank's tiles into a full-size gather buffer (+ the unpack on rank 0), so one GPU measures a

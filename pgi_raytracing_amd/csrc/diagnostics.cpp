@@ -47,6 +47,11 @@ void collect_timeline(pgrt_ctx* ctx, FrameSet* fs) {
         }
         fs->stamp_used = 0;
     }
+    if (fs->stamp_overflow) {  // launches past the buffer were not stamped: say so in the records
+        pgrt_timeline_rec r{fs->ticket, 0, PGRT_TL_DROPPED, -1, 0, 0, 0, 0, 0, 0, 0};
+        ctx->timeline.push_back(r);
+        fs->stamp_overflow = false;
+    }
 }
 
 }  // namespace pgrt
@@ -58,6 +63,8 @@ int pgrt_timeline_enable(pgrt_ctx* ctx, int on) {
     return guarded(ctx, [&] {
         drain_frames(ctx);  // pending frames were enqueued with the old choice
         ctx->timeline_on = on != 0;
+        if (!ctx->timeline_on)  // the stamp buffers (64 MB per frame set) go with the timeline
+            for (auto& fs : ctx->sets) fs->stamps.release();
     });
 }
 

@@ -18,13 +18,20 @@ bool rccl_gather(const pgrt_ctx* ctx, const FrameSet* fs) {
 
 // Wait for fs's frame, re-render it after a queue overflow (larger queues), fill fs->stats.  A
 // distributed frame's gather was queued with the frame (device-ordered, start_frame).  There is no
-// control collective: a rank whose queues overflowed re-renders its tiles and sends them again;
-// rank 0 learns which ranks did from the flag at the tail of every rank's send (gather_end copies
-// them to host memory behind the unpack), receives those ranks' tiles again and unpacks them (and
-// its own, when it overflowed).  Every rank posts its sends / receives for a frame when that frame
-// is collected, and frames are collected in submission order on every rank, so the point-to-point
-// operations stay matched.  Non-zero ranks never wait for another rank; rank 0 waits for the
-// frame's own gather only.
+// control collective: the tail of every rank's send carries its overflow flag and the frame's
+// sequence number (gather_begin).  A rank whose queues overflowed re-renders its tiles and sends
+// them again; rank 0 reads the peers' tails (gather_end copies them to host memory behind the
+// unpack), receives the flagged ranks' tiles again and unpacks them (and its own, when it
+// overflowed).  The re-send / re-receive of a frame is posted when that frame is COLLECTED, so
+// every rank must submit and wait for its distributed frames in the same order (the same calls of
+// the same program, as bench.py's ranks do) -- point-to-point operations match in posting order.
+// Rank 0 checks the sequence number of every tail it receives and fails loudly on a mismatch
+// instead of unpacking another frame's tiles.  A rank that gives up after kMaxRetries re-renders
+// still sends (flag 2, "poison"), so rank 0's receive completes and rank 0 fails too instead of
+// waiting forever.  Non-zero ranks never wait for another rank; rank 0 waits for the frame's own
+// gather only.
+constexpr int kMaxRetries = 8;
+
 void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
     int retries = 0;
     const bool rccl = rccl_gather(ctx, fs);
@@ -32,19 +39,34 @@ void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
         const bool mine = read_frame_counters(ctx, fs);
         if (!rccl || ctx->rank != 0) {
             if (!mine) break;
+            if (rccl && retries + 1 >= kMaxRetries) {  // give up, but keep rank 0's receive matched
+                fs->poison = true;
+                gather_frame(ctx, fs);
+                throw Error(PGRT_ERR_OUT_OF_MEMORY, "ray queues kept overflowing (rank " + std::to_string(ctx->rank) +
+                                                        " gave up; rank 0 is told by the poison flag of its send)");
+            }
             rerender_frame(ctx, fs, true, retries);
             if (fs->distributed) gather_frame(ctx, fs);  // rank != 0: the tiles again, to rank 0
             continue;
         }
         PGRT_HIP(hipEventSynchronize(fs->ev_flags));
         std::vector<int> peers;
-        for (int r = 1; r < fs->deal.world; ++r)
+        for (int r = 1; r < fs->deal.world; ++r) {
+            const unsigned seq = (unsigned)fs->peer_flags[kMaxRanks + r];
+            if (seq == 0) continue;  // not received in this gather (a re-gather of other ranks)
+            PGRT_REQUIRE(seq == fs->gather_seq, PGRT_ERR_RCCL,
+                         "rank " + std::to_string(r) + " sent the tiles of its distributed frame " + std::to_string(seq) +
+                             " where rank 0 expected frame " + std::to_string(fs->gather_seq) +
+                             ": every rank must submit and wait for distributed frames in the same order");
+            PGRT_REQUIRE(fs->peer_flags[r] != 2, PGRT_ERR_OUT_OF_MEMORY,
+                         "rank " + std::to_string(r) + " gave up on the frame: its ray queues kept overflowing");
             if (fs->peer_flags[r]) peers.push_back(r);
+        }
         if (!mine && peers.empty()) break;
         if (mine) {
             rerender_frame(ctx, fs, true, retries);
         } else {
-            PGRT_REQUIRE(++retries < 8, PGRT_ERR_OUT_OF_MEMORY, "ray queues kept overflowing");
+            PGRT_REQUIRE(++retries < kMaxRetries, PGRT_ERR_OUT_OF_MEMORY, "ray queues kept overflowing");
         }
         regather_rank0(ctx, fs, mine, peers);
     }
@@ -84,6 +106,8 @@ void gather_begin(pgrt_ctx* ctx, FrameSet* fs, UnpackSrc& u) {
             f.fc[j] = fs->slots[j]->pinned_fc;
             f.n[j] = (int)fs->slots[j]->host_fc.size();
         }
+        f.poison = fs->poison ? 1 : 0;
+        f.seq = fs->gather_seq;
         const size_t tiles = (size_t)fs->nframes * u.count[ctx->rank] * kTile * kTile * 3;
         launch_overflow_flag(f, reinterpret_cast<int*>(fs->tilebuf.p + tiles), ctx->stream);
     }
@@ -169,7 +193,7 @@ void regather_rank0(pgrt_ctx* ctx, FrameSet* fs, bool own, const std::vector<int
     std::fill(fs->regather_peer, fs->regather_peer + kMaxRanks, 0);
     fs->regather_peer[0] = own ? 1 : 0;
     for (int r : peers) fs->regather_peer[r] = 1;
-    std::fill(fs->peer_flags, fs->peer_flags + kMaxRanks, 0);
+    std::fill(fs->peer_flags, fs->peer_flags + 2 * kMaxRanks, 0);
     try {
         gather_frame(ctx, fs);
     } catch (...) {

@@ -176,8 +176,9 @@ int group_max(const pgrt_ctx* ctx) {
     return ctx->frames_in_flight > 1 ? kDefaultGroupMaxInFlight : kDefaultGroupMax;
 }
 
-// The tiles of each pipeline slot.  Round-robin (slot j gets tiles j, j + K, ...; multi-frame
-// calls, tile-compact and distributed outputs rely on it: FrameParams::frame_tiles, store_pixel).
+// The tiles of each pipeline slot.  Round-robin (slot j gets tiles j, j + K, ...; tile-compact and
+// distributed outputs rely on it: store_pixel's position in the caller's tile list; a multi-frame
+// call's tile records carry their frame index, frame_of_tile).
 // A synchronous one-frame render into a framebuffer records which tiles' primary rays hit a
 // dielectric (pgrt_config.tile_order) and, when the last frame of the same size had some, deals
 // those tiles to slot 0 and the rest to slot 1: the frame's critical path is the chain of deep
@@ -503,6 +504,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             ctx->timer.end(s, id);
             // levels >= sub: whole ray trees in one launch (no queues, shades or combines below it)
             const int sub = subtree_first(ctx, view, p, n0 < kSmallPacketBatch);
+            sl->sub_first = sub;
             for (int L = 0; L < levels; ++L) {
                 Queue qc = q[L & 1], qn = q[(L + 1) & 1];
                 const int maxc = L == 0 ? n0 : std::min(sl->q_cap, sl->level_cap[L]);
@@ -626,6 +628,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
     PGRT_HIP(hipGetLastError());
     fs->stats.trace_launches = trace_launches;
     fs->stamp_used = slog.used;
+    fs->stamp_overflow = slog.overflow;
 }
 
 // One look at fs's completed frame (host waits for its slots): the counters to the host, the next
@@ -661,10 +664,13 @@ bool read_frame_counters(pgrt_ctx* ctx, FrameSet* fs) {
             overflow |= h.overflow != 0;
             ctx->last_fc.push_back(h);
         }
+        // the shadow queue's grid hint: the levels below the subtree launch only (the subtree
+        // traces its own shadow rays; fc_shadow still counts them for the statistics)
         int shadow_need = 0;
+        const int shadow_levels = sl->sub_first > 0 ? sl->sub_first : kMaxLevels;
         for (auto& h : sl->host_fc) {
             int sc = 0;
-            for (int L = 0; L < kMaxLevels; ++L) sc += fc_shadow(h, L);
+            for (int L = 0; L < shadow_levels; ++L) sc += fc_shadow(h, L);
             shadow_need = std::max(shadow_need, sc);
         }
         // grid hints for the next frame: kept while the count stays within [hint/2, hint]
@@ -823,9 +829,11 @@ void start_frame(pgrt_ctx* ctx, FrameSet* fs, const pgrt_render_params* p, std::
     fs->dist_fb = fb;
     fs->cam_w = ctx->cam.width;
     fs->cam_h = ctx->cam.height;
+    fs->poison = false;
     if (distributed) {
         // this rank's tiles of every frame, frame-major (the gather's layout, unpack_layout)
         fs->deal = deal;
+        fs->gather_seq = ++ctx->gather_count;
         // + the overflow flag's tail (gather_begin / collect_frame)
         fs->tilebuf.alloc((size_t)nframes * tiles.size() * kTile * kTile * 3 + kGatherTail);
         fs->frame_out_tiles = (int)tiles.size();

@@ -377,7 +377,8 @@ __global__ void k_overflow_flag(FlagSrc f, int* out) {
     int v = 0;
     for (int j = 0; j < f.K; ++j)
         for (int b = 0; b < f.n[j]; ++b) v |= f.fc[j][b].overflow;
-    out[0] = v != 0 ? 1 : 0;
+    out[0] = f.poison ? 2 : (v != 0 ? 1 : 0);
+    out[1] = (int)f.seq;
 }
 
 void launch_overflow_flag(const FlagSrc& f, int* out, hipStream_t stream) {
@@ -386,8 +387,12 @@ void launch_overflow_flag(const FlagSrc& f, int* out, hipStream_t stream) {
 
 __global__ void k_peer_flags(UnpackSrc u, int world, size_t floats_per_tile_count, int* flags) {
     const int r = threadIdx.x;
-    if (r >= 1 && r < world)  // src NULL: a rank not received in this gather
-        flags[r] = u.src[r] ? *reinterpret_cast<const int*>(u.src[r] + floats_per_tile_count * (size_t)u.count[r]) : 0;
+    if (r >= 1 && r < world) {  // src NULL: a rank not received in this gather
+        const int* tail = u.src[r] ? reinterpret_cast<const int*>(u.src[r] + floats_per_tile_count * (size_t)u.count[r])
+                                   : nullptr;
+        flags[r] = tail ? tail[0] : 0;
+        flags[kMaxRanks + r] = tail ? tail[1] : 0;
+    }
 }
 
 void launch_peer_flags(const UnpackSrc& u, int world, size_t floats_per_tile_count, int* flags, hipStream_t stream) {

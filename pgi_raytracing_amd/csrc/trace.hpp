@@ -257,9 +257,13 @@ struct FlagSrc {
     const FrameCounters* fc[4];
     int n[4];
     int K;
+    int poison;    // this rank gave up re-rendering the frame: its tiles are garbage (flag 2)
+    unsigned seq;  // the rank's distributed-frame sequence number (tail word 1): rank 0 checks it
 };
+// tail words: [0] 0 = complete, 1 = queues overflowed (a re-send follows), 2 = gave up; [1] seq
 void launch_overflow_flag(const FlagSrc& f, int* out, hipStream_t stream);
 // flags[r] = the flag word after rank r's `floats` floats of tiles at u.src[r] (r = 1 .. world-1)
+// flags[r] / flags[kMaxRanks + r] = tail words 0 / 1 of rank r's send (0 for ranks not received)
 void launch_peer_flags(const UnpackSrc& u, int world, size_t floats_per_tile_count, int* flags, hipStream_t stream);
 
 // scene / BVH build
