@@ -21,6 +21,7 @@
 namespace pgrt {
 
 constexpr int kBlock = 256;
+constexpr int kXcds = 8;  // MI355X: workgroups are dispatched round-robin over 8 XCDs
 
 // grid of a grid-stride kernel: cover the expected count, at most 4096 workgroups
 static int grid_for(int max_count, int expect) {
@@ -444,15 +445,15 @@ __global__ __launch_bounds__(kBlock) void k_export_tiles(const int4* __restrict_
                                                          unsigned long long* __restrict__ stamps) {
     PGRT_STAMP_BEGIN(stamps);
     const int x = threadIdx.x & 63;
-#ifdef PGRT_EXPORT_XCD  // A/B: only the workgroups dispatched to XCD 0 (blockIdx % 8 == 0) copy
-    if (blockIdx.x % 8 != 0) {
+    // only the workgroups the dispatcher places on XCD 0 (workgroups go to the 8 XCDs round-robin:
+    // blockIdx % 8 == 0) copy: the PCIe stores then queue in one XCD's L2 and fabric port, and the
+    // concurrent slot's waves on the other seven XCDs never wait behind them
+    if (blockIdx.x % kXcds != 0) {
         PGRT_STAMP_END(stamps);
         return;
     }
-    for (int r = (blockIdx.x / 8) * (kBlock / 64) + (threadIdx.x >> 6); r < rows; r += (gridDim.x / 8) * (kBlock / 64)) {
-#else
-    for (int r = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); r < rows; r += gridDim.x * (kBlock / 64)) {
-#endif
+    const int wg = blockIdx.x / kXcds, nwg = gridDim.x / kXcds;
+    for (int r = wg * (kBlock / 64) + (threadIdx.x >> 6); r < rows; r += nwg * (kBlock / 64)) {
         const int4 tr = tiles[r >> 6];  // 64 rows per tile
         const int ly = r & 63;
         if (ly >= tr.w || x >= tile_width(tr)) continue;
@@ -467,13 +468,12 @@ void launch_export_tiles(const int4* tiles, int ntiles, const float* src, float*
                          long long frame_stride, hipStream_t stream) {
     if (ntiles <= 0) return;
     const int rows = ntiles * kTile;
-    // 32 workgroups: 44-51 GB/s on the link alone (d2h_probe; 53 from 64 up), and the fewest CUs
-    // whose memory pipelines wait behind PCIe stores (r5d: synchronous host frame 1.02 ms at 32,
-    // 1.12 at 64, 1.14 at 256, 1.32 at 8)
-#ifndef PGRT_EXPORT_GRID
-#define PGRT_EXPORT_GRID 32
+    // 32 copying workgroups, all on XCD 0 (r5h, synchronous host frame: 0.96 ms; 32 spread over the
+    // 8 XCDs 1.02, 8 on XCD 0 1.18; r5d spread: 64 1.12, 256 1.14, 16 1.09-1.12, 8 1.32)
+#ifndef PGRT_EXPORT_WG
+#define PGRT_EXPORT_WG 32
 #endif
-    const int grid = std::min(PGRT_EXPORT_GRID, ceil_div(rows, kBlock / 64));
+    const int grid = kXcds * std::max(1, std::min(PGRT_EXPORT_WG, ceil_div(rows, kBlock / 64)));
     hipLaunchKernelGGL(k_export_tiles, dim3(grid), dim3(kBlock), 0, stream, tiles, rows,
                        reinterpret_cast<const float4*>(src), reinterpret_cast<float4*>(dst_host), ox, oy, pitch,
                        frame_stride / 4, stamp_next(kStampExportTiles, -1, grid, kBlock));

@@ -7,6 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 timeout -k 10 120 ./build/d2h_probe > gpurun_out/d2h_probe_r5h.txt 2>&1 || exit 1
 grep -A3 "pass 1" gpurun_out/d2h_probe_r5h.txt
+bash tools/gpu_check.sh tests smoke || exit 1
 for r in 1 2; do
   for lib in base xcd256 xcd64 g16; do
     if [ $lib = base ]; then unset PGRT_LIB; else export PGRT_LIB=ablib/$lib/libpgrt.so; fi
