@@ -166,180 +166,6 @@ __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : 6) void k_shade
     PGRT_STAMP_END(s.stamps);
 }
 
-// ---- level 0 of a 1-spp pinhole batch, software-pipelined ----
-//
-// k_shade's dependent chain per grid-stride round is: the hit record (prefetched a round ahead) ->
-// the 64-B attribute record of a hit, or (a miss) the environment lookup's texel taps -> shading ->
-// the block's allocation atomic -> the emitted rays.  Here a ray's attribute or texel loads are
-// issued one round EARLY, between the block's allocation atomic and its result (shade_alloc_begin /
-// _end), together with the next ray's environment-angle math: the attribute / texel round trip and
-// the atomic's round trip overlap instead of following each other.  The fetched data of the next
-// ray lives in 16 registers (L0Pre: a hit's attribute floats, or a miss's texel window), so the
-// pipeline costs no more registers than k_shade's attribute array.  Same functions, same float
-// operations: bit-identical to k_shade (tests/test_gpu_parity.py frame tests, full C2 size).
-struct L0Pre {
-    float u[16];  // hit: n0 n1 n2 uv0 uv1 uv2 material (load_attr); miss: the env TexTap, packed
-};
-__device__ __forceinline__ void l0_pack_tap(const TexTap& q, L0Pre& p) {
-    p.u[0] = q.x;
-    p.u[1] = q.y;
-    p.u[2] = __int_as_float(q.x1);
-    p.u[3] = __int_as_float(q.x2);
-    p.u[4] = __int_as_float(q.y1);
-    p.u[5] = __int_as_float(q.y2);
-    p.u[6] = __int_as_float(q.mode);
-    p.u[7] = __uint_as_float(q.w1[0]);
-    p.u[8] = __uint_as_float(q.w1[1]);
-    p.u[9] = __uint_as_float(q.w1[2]);
-    p.u[10] = __uint_as_float(q.w2[0]);
-    p.u[11] = __uint_as_float(q.w2[1]);
-    p.u[12] = __uint_as_float(q.w2[2]);
-    p.u[13] = __uint_as_float(q.k1);
-    p.u[14] = __uint_as_float(q.k2);
-}
-__device__ __forceinline__ TexTap l0_unpack_tap(const L0Pre& p) {
-    TexTap q;
-    q.x = p.u[0];
-    q.y = p.u[1];
-    q.x1 = __float_as_int(p.u[2]);
-    q.x2 = __float_as_int(p.u[3]);
-    q.y1 = __float_as_int(p.u[4]);
-    q.y2 = __float_as_int(p.u[5]);
-    q.mode = __float_as_int(p.u[6]);
-    q.w1[0] = __float_as_uint(p.u[7]);
-    q.w1[1] = __float_as_uint(p.u[8]);
-    q.w1[2] = __float_as_uint(p.u[9]);
-    q.w2[0] = __float_as_uint(p.u[10]);
-    q.w2[1] = __float_as_uint(p.u[11]);
-    q.w2[2] = __float_as_uint(p.u[12]);
-    q.k1 = __float_as_uint(p.u[13]);
-    q.k2 = __float_as_uint(p.u[14]);
-    return q;
-}
-// issue the loads of ray (d4, h)'s shading inputs (no wait)
-__device__ __forceinline__ void l0_prefetch(const SceneView& s, bool active, float4 d4, float4 h, L0Pre& p) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) p.u[k] = 0.0f;
-    if (!active || !(d4.w >= 0.0f)) return;
-    if (__float_as_int(h.w) < 0) {
-        l0_pack_tap(env_fetch(s, normalize(v3(d4.x, d4.y, d4.z))), p);
-    } else {
-        const HitAttr a = load_attr(s, h);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) p.u[k] = a.f[k];
-    }
-}
-// shade_eval of a level-0 pinhole ray with its prefetched inputs
-__device__ __forceinline__ void l0_eval(const SceneView& s, const DevMaterial* mats, const float* lut, int max_level,
-                                        bool active, float4 o4, float4 d4, float4 h, const L0Pre& p, ShadeOut& r) {
-    shade_init(r);
-    if (!active) return;
-    r.org = v3(o4.x, o4.y, o4.z);
-    r.dirraw = v3(d4.x, d4.y, d4.z);
-    if (d4.w < 0.0f) {
-        r.color = make_float4(0, 0, 0, 0);  // padding slot
-        return;
-    }
-    const V3 d = normalize(r.dirraw);
-    if (__float_as_int(h.w) < 0) {
-        r.color = env_finish(s, lut, l0_unpack_tap(p));  // miss (raytracer.cpp:390-393)
-        return;
-    }
-    HitAttr a;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) a.f[k] = p.u[k];
-    shade_hit(s, mats, lut, 0, max_level, d, PGRT_IOR_AIR, h, a, r);
-}
-
-template <bool LDS_TABLES>
-#ifndef PGRT_L0P_WAVES
-#define PGRT_L0P_WAVES 4
-#endif
-__global__ __launch_bounds__(kShadeBlock, PGRT_L0P_WAVES) void k_shade_l0p(SceneView s, FrameParams fp, Queue q,
-                                                                           Queue next, LevelNodes nodes, ShadowQueue sq,
-                                                                           FrameCounters* fc, PinholeOrigin l0,
-                                                                           L0Final l0f) {
-    PGRT_STAMP_BEGIN(s.stamps);
-    __shared__ float lut255[256];
-    __shared__ DevMaterial smat[LDS_TABLES ? kLdsMats : 1];
-    __shared__ DevTexture stex[LDS_TABLES ? kLdsTex : 1];
-    __shared__ ShadeAllocLds<kShadeBlock> alds;
-    if constexpr (LDS_TABLES) {
-        for (int k = threadIdx.x; k < s.nmat; k += kShadeBlock) smat[k] = s.mats[k];
-        for (int k = threadIdx.x; k < s.ntex; k += kShadeBlock) stex[k] = s.tex[k];
-        s.tex = stex;
-    }
-    int it_par = 0, refr_acc = 0;
-    const DevMaterial* mats = LDS_TABLES ? smat : s.mats;
-    fill_byte_lut(lut255);
-    const int n = min(fc_count(*fc, 0), q.cap);
-    const int tid = threadIdx.x;
-    const int sbits = s.nlight > 0 ? 32 - __clz(s.nlight) : 0;
-    const int stride = gridDim.x * kShadeBlock;
-    // every valid level-0 pinhole ray starts at the camera with tnear 0.001, in air
-    const float4 cam_o = make_float4(l0.x, l0.y, l0.z, 0.001f);
-    const float4 no_hit = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
-    auto load_hit = [&](int k) {  // a miss has no hit record: its bit in the wave's mask is clear
-        const unsigned long long hm = l0f.hit[__builtin_amdgcn_readfirstlane(k >> 6)];
-        return ((hm >> (k & 63)) & 1ull) ? ld_stream(q.hit + k) : no_hit;
-    };
-    const int i0 = blockIdx.x * kShadeBlock + tid;
-    float4 cd = make_float4(0, 0, 0, -1.0f), ch = no_hit, nd = cd, nh = no_hit;
-    L0Pre cu;
-    if (i0 < n) {
-        cd = ld_stream(q.rd + i0);
-        ch = load_hit(i0);
-    }
-    l0_prefetch(s, i0 < n, cd, ch, cu);
-    if (i0 + stride < n) {
-        nd = ld_stream(q.rd + i0 + stride);
-        nh = load_hit(i0 + stride);
-    }
-    for (int base_i = blockIdx.x * kShadeBlock; base_i < n; base_i += stride) {
-        const int i = base_i + tid;
-        const bool active = i < n;
-        ShadeOut r;
-        l0_eval(s, mats, lut255, fp.max_level, active, cam_o, cd, ch, cu, r);
-        if (fp.tile_deep) {  // a wave lies in one tile (4096 * nsb rays per tile)
-            const unsigned long long dm = __ballot(active && r.nchild > 0);
-            if (dm != 0ull && __lane_id() == 0) fp.tile_deep[(i / fp.nsb) / (kTile * kTile)] = 1;
-        }
-        if (fp.count) {  // profile == 2 only: one atomic pair per wave (the whole-frame roofline)
-            const bool hit = active && cd.w >= 0.0f && __float_as_int(ch.w) >= 0;
-            const unsigned long long hm = __ballot(hit), tm = __ballot(hit && r.kind == 2 && mats[r.mid].tex >= 0);
-            if (__lane_id() == 0 && hm) {
-                atomicAdd(&fc->shade[0][0], (unsigned long long)__popcll(hm));
-                atomicAdd(&fc->shade[0][1], (unsigned long long)__popcll(tm));
-            }
-        }
-        const ShadeAllocPending pa = shade_alloc_begin<kShadeBlock>(alds, it_par, fc, 0, sbits, r, &refr_acc);
-        // behind the allocation atomic: the next ray's attribute / texel loads (and a miss's
-        // environment-angle math), then the record of the ray after it
-        L0Pre nu;
-        l0_prefetch(s, i + stride < n, nd, nh, nu);
-        float4 nnd = make_float4(0, 0, 0, -1.0f), nnh = no_hit;
-        if (i + 2 * stride < n) {
-            nnd = ld_stream(q.rd + i + 2 * stride);
-            nnh = load_hit(i + 2 * stride);
-        }
-        const ShadeSlots sl = shade_alloc_end<kShadeBlock>(alds, it_par, 0, pa);
-        // a final colour (environment texel; padding) -> the pixel, now; the others are completed
-        // by the finish (n is a multiple of 64: whole waves)
-        const bool fin = active && r.kind == 0;
-        const unsigned long long pend = __ballot(active && !fin);
-        if (active && __lane_id() == 0) st_stream_nt(l0f.pending + (i >> 6), pend);
-        if (fin) store_final_1spp(fp, l0f.tiles, l0f.fo, i, r.color);
-        if (active && !fin) shade_emit(s, mats, 0, i, r, sl, next, nodes, sq, fc);
-        cd = nd;
-        ch = nh;
-        cu = nu;
-        nd = nnd;
-        nh = nnh;
-    }
-    shade_refract_flush(fc, 0, refr_acc);
-    PGRT_STAMP_END(s.stamps);
-}
-
 void launch_shade(const SceneView& s_in, const FrameParams& fp, int level, Queue q, Queue next, LevelNodes nodes,
                   ShadowQueue sq, FrameCounters* fc, int max_count, hipStream_t stream, int expect,
                   const PinholeOrigin& l0, const L0Final& l0f) {
@@ -352,17 +178,7 @@ void launch_shade(const SceneView& s_in, const FrameParams& fp, int level, Queue
 #define PGRT_LAUNCH_SHADE(T, F)                                                                                   \
     hipLaunchKernelGGL((k_shade<T, F>), dim3(grid), dim3(kShadeBlock), 0, stream, s, fp, level, q, next, nodes, sq, \
                        fc, l0, l0f)
-#ifndef PGRT_L0_PIPELINE
-#define PGRT_L0_PIPELINE 1
-#endif
-    if (PGRT_L0_PIPELINE && l0f.hit && l0.on && level == 0) {  // 1-spp pinhole level 0: the pipelined form
-        if (lds)
-            hipLaunchKernelGGL((k_shade_l0p<true>), dim3(grid), dim3(kShadeBlock), 0, stream, s, fp, q, next, nodes, sq, fc,
-                               l0, l0f);
-        else
-            hipLaunchKernelGGL((k_shade_l0p<false>), dim3(grid), dim3(kShadeBlock), 0, stream, s, fp, q, next, nodes, sq,
-                               fc, l0, l0f);
-    } else if (l0f.hit) {
+    if (l0f.hit) {
         if (lds) PGRT_LAUNCH_SHADE(true, true); else PGRT_LAUNCH_SHADE(false, true);
     } else {
         if (lds) PGRT_LAUNCH_SHADE(true, false); else PGRT_LAUNCH_SHADE(false, false);
