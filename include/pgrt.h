@@ -178,6 +178,8 @@ typedef struct pgrt_bvh_info {
 #define PGRT_PACKETS_OFF (-1)     /* every level one lane per ray */
 #define PGRT_HOST_EXPORT_KERNEL 1 /* host frames: per-slot export kernels into page-locked memory */
 #define PGRT_HOST_EXPORT_COPY (-1) /* host frames: one device-to-host copy after the frame */
+#define PGRT_HOST_EXPORT_SPLIT 2  /* host frames: after the frame, a share by an XCD-0 blit kernel and
+                                     the rest by one DMA copy, concurrently */
 typedef struct pgrt_config {
     unsigned size;        /* sizeof(pgrt_config) of the caller's pgrt.h: pgrt_get_config fills it, and
                              pgrt_set_config rejects any other value (a caller built against another
@@ -221,10 +223,12 @@ typedef struct pgrt_config {
                              pgrt_render_frames_host_async): 0 = default -- a synchronous two-slot
                              frame exports each slot's finished tiles with a small blit kernel as
                              soon as that slot is done (the bulk slot's pixels cross PCIe while the
-                             deep-tile slot still renders), frames in flight take one DMA copy per
-                             call; PGRT_HOST_EXPORT_KERNEL = export kernels always;
+                             deep-tile slot still renders), frames in flight take the split copy
+                             (below) per call; PGRT_HOST_EXPORT_KERNEL = export kernels always;
                              PGRT_HOST_EXPORT_COPY = one DMA copy after every frame (pageable
-                             destinations always take the copy) */
+                             destinations always take the copy); PGRT_HOST_EXPORT_SPLIT = after every
+                             frame, part of the bytes by a blit kernel on XCD 0 and the rest by a
+                             DMA copy at the same time */
 } pgrt_config;
 
 /* ---- context ---- */
@@ -307,11 +311,12 @@ int pgrt_render_frames_device(pgrt_ctx* ctx, const pgrt_render_params* p, int nf
                               void* rgba_device, pgrt_stats* st);
 /* Batched frames to a HOST framebuffer (the reference's Producer hands every finished frame to
  * the host-side D3D texture, APP/simpleguidx11.cpp:105-124): frames are rendered into a device
- * staging buffer owned by the frame in flight, then ONE device-to-host copy of nframes * W*H*4
- * floats into rgba_host is queued behind them, so the PCIe transfer of one call overlaps the
- * rendering of the calls in flight behind it.  rgba_host must stay valid until the ticket is
- * waited for; pinned memory from pgrt_host_alloc makes the copy a true asynchronous DMA (pageable
- * memory works but copies synchronously).  Same pixels as pgrt_render_frames_device. */
+ * staging buffer owned by the frame in flight, then the nframes * W*H*4 floats move into
+ * rgba_host behind them (pgrt_config.host_export: by default half by a copy kernel on XCD 0 and
+ * half by one DMA copy, concurrently), so the PCIe transfer of one call overlaps the rendering of
+ * the calls in flight behind it.  rgba_host must stay valid until the ticket is waited for; pinned
+ * memory from pgrt_host_alloc makes the copy truly asynchronous (pageable memory works but takes
+ * one synchronous DMA copy).  Same pixels as pgrt_render_frames_device. */
 int pgrt_render_frames_host_async(pgrt_ctx* ctx, const pgrt_render_params* p, int nframes,
                                   float* rgba_host, unsigned long long* ticket);
 /* Page-locked host memory for framebuffers (pgrt_render, pgrt_render_frames_host_async). */
@@ -351,6 +356,18 @@ int pgrt_tile_rect(int width, int height, int tile_size, int tile_index, int rec
  * W x H RGBA framebuffer.  Host reference of the device unpack. */
 int pgrt_unpack_tiles_host(int width, int height, int tile_size, int world,
                            const float* gathered, float* rgba);
+/* The tail of a rank's distributed send (two ints after its tiles): its flag (0 ok,
+ * 1 the rank's queues overflowed -- it re-renders and sends again, 2 it gave up) and the frame's
+ * sequence number (>= 1).  pgrt_gather_tail forms it as the device does; pgrt_gather_tail_verdict
+ * is rank 0's reading of one gather's tails (flags[r], seqs[r] for r < world; seqs[r] == 0: rank r
+ * not received in this gather, rank 0's own entry ignored): PGRT_OK with regather[r] = 1 for the
+ * ranks whose tiles must be received again, PGRT_ERR_RCCL when a rank sent another frame's tiles
+ * (the ranks did not submit / wait in the same order), PGRT_ERR_OUT_OF_MEMORY when a rank gave up;
+ * *bad_rank names that rank.  The distributed frames run exactly this logic; host-only (the
+ * world-2 gloo test drives it). */
+int pgrt_gather_tail(int overflow, int poison, unsigned seq, int tail[2]);
+int pgrt_gather_tail_verdict(const int* flags, const unsigned* seqs, int world, unsigned expect_seq, int* regather,
+                             int* bad_rank);
 /* The same three with an explicit share (rank 0 renders a tiles for every b of another rank,
  * 1..64 each; a = b = 0: the default share) -- the deal of a context whose pgrt_config sets
  * rank0_share_a / rank0_share_b. */

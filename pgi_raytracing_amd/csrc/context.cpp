@@ -113,8 +113,8 @@ int pgrt_set_config(pgrt_ctx* ctx, const pgrt_config* cfg) {
                      "pgrt_config.size is " + std::to_string(cfg->size) + ", this library's pgrt_config has " +
                          std::to_string(sizeof(pgrt_config)) + " bytes (abi " + std::to_string(PGRT_ABI_VERSION) +
                          "): start from pgrt_get_config");
-        PGRT_REQUIRE(cfg->host_export >= -1 && cfg->host_export <= 1, PGRT_ERR_INVALID_ARGUMENT,
-                     "host_export must be 0, PGRT_HOST_EXPORT_KERNEL or PGRT_HOST_EXPORT_COPY");
+        PGRT_REQUIRE(cfg->host_export >= -1 && cfg->host_export <= 2, PGRT_ERR_INVALID_ARGUMENT,
+                     "host_export must be 0, PGRT_HOST_EXPORT_KERNEL, PGRT_HOST_EXPORT_COPY or PGRT_HOST_EXPORT_SPLIT");
         PGRT_REQUIRE(cfg->bvh_builder == 0 || cfg->bvh_builder == PGRT_BVH_LBVH || cfg->bvh_builder == PGRT_BVH_PLOC,
                      PGRT_ERR_INVALID_ARGUMENT, "bvh_builder must be 0, PGRT_BVH_LBVH or PGRT_BVH_PLOC");
         PGRT_REQUIRE(cfg->bvh_width == 0 || cfg->bvh_width == 2 || cfg->bvh_width == 8, PGRT_ERR_INVALID_ARGUMENT,

@@ -232,6 +232,9 @@ struct FrameSet {
     float* host_dst = nullptr;
     float* host_map = nullptr;
     size_t host_bytes = 0;
+    // PGRT_HOST_EXPORT_SPLIT: the blit kernel's share runs on host_aux beside slot 0's DMA copy
+    hipStream_t host_aux = nullptr;
+    hipEvent_t ev_host0 = nullptr, ev_host1 = nullptr;
     int cam_w = 0, cam_h = 0;  // image size at submission (the gather's layout)
     bool deep_rec = false;     // the level-0 shades record deep tiles (FrameParams::tile_deep)
     pgrt_stats stats{};
@@ -267,8 +270,10 @@ struct FrameSet {
     ~FrameSet() {
         for (auto& s : slots)
             if (s->stream) (void)hipStreamSynchronize(s->stream);
-        for (hipEvent_t e : {ev_ready, ev_g0, ev_g1, ev_g2, ev_flags})
+        if (host_aux) (void)hipStreamSynchronize(host_aux);
+        for (hipEvent_t e : {ev_ready, ev_g0, ev_g1, ev_g2, ev_flags, ev_host0, ev_host1})
             if (e) (void)hipEventDestroy(e);
+        if (host_aux) (void)hipStreamDestroy(host_aux);
         if (peer_flags) (void)hipHostFree(peer_flags);
     }
 };

@@ -51,16 +51,21 @@ void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
         }
         PGRT_HIP(hipEventSynchronize(fs->ev_flags));
         std::vector<int> peers;
-        for (int r = 1; r < fs->deal.world; ++r) {
-            const unsigned seq = (unsigned)fs->peer_flags[kMaxRanks + r];
-            if (seq == 0) continue;  // not received in this gather (a re-gather of other ranks)
-            PGRT_REQUIRE(seq == fs->gather_seq, PGRT_ERR_RCCL,
-                         "rank " + std::to_string(r) + " sent the tiles of its distributed frame " + std::to_string(seq) +
-                             " where rank 0 expected frame " + std::to_string(fs->gather_seq) +
+        {
+            const int world = fs->deal.world;
+            unsigned seqs[kMaxRanks];
+            int regather[kMaxRanks], bad = -1;
+            for (int r = 0; r < world; ++r) seqs[r] = (unsigned)fs->peer_flags[kMaxRanks + r];
+            const int v = gather_tail_verdict(fs->peer_flags, seqs, world, fs->gather_seq, regather, &bad);
+            PGRT_REQUIRE(v != -1, PGRT_ERR_RCCL,
+                         "rank " + std::to_string(bad) + " sent the tiles of its distributed frame " +
+                             std::to_string(bad >= 0 ? seqs[bad] : 0u) + " where rank 0 expected frame " +
+                             std::to_string(fs->gather_seq) +
                              ": every rank must submit and wait for distributed frames in the same order");
-            PGRT_REQUIRE(fs->peer_flags[r] != 2, PGRT_ERR_OUT_OF_MEMORY,
-                         "rank " + std::to_string(r) + " gave up on the frame: its ray queues kept overflowing");
-            if (fs->peer_flags[r]) peers.push_back(r);
+            PGRT_REQUIRE(v != -2, PGRT_ERR_OUT_OF_MEMORY,
+                         "rank " + std::to_string(bad) + " gave up on the frame: its ray queues kept overflowing");
+            for (int r = 1; r < world; ++r)
+                if (regather[r]) peers.push_back(r);
         }
         if (!mine && peers.empty()) break;
         if (mine) {

@@ -278,14 +278,20 @@ void probe_side_launch(pgrt_ctx* ctx, const SceneView& view, FrameSlot* sl, Fram
 // of 32 workgroups (1.14 with 256: the kernel's PCIe stores stall the memory pipelines of CUs the
 // deep-tile slot also runs on), 5.2 with per-slot DMA copies of the slot's tile runs (2D copies);
 // calls in flight 0.61-0.65 ms/frame with one DMA copy per call, 0.76-0.83 with export kernels
-// (their stores slow the other calls' rendering), so frames in flight keep the copy.
-enum { kHostNone = 0, kHostKernel = 1, kHostOnce = 2 };
+// (their stores slow the other calls' rendering).  But a process's SDMA rate is not fixed: the
+// same copy runs at 27 or 54 GB/s (r5k / r5l / r5n probes: typically the first process on a box),
+// where the blit kernel stays at 53-54.  So frames in flight take the split copy by default: half
+// the call's bytes by an XCD-0 blit kernel on a side stream, the other half by one DMA copy at the
+// same time (r5m, in-process A/B, 8 frames x 4 calls: 0.656-0.66 ms/frame; DMA 0.63-0.76; export
+// kernels 0.67-0.69; a 70 % kernel share 0.70-0.75).
+enum { kHostNone = 0, kHostKernel = 1, kHostOnce = 2, kHostSplit = 3 };
 int host_export_mode(const pgrt_ctx* ctx, const FrameSet* fs, int K) {
     if (!fs->host_dst || K == 0) return kHostNone;
     const int c = ctx->cfg.host_export;
     if (c == PGRT_HOST_EXPORT_COPY || !fs->host_map) return kHostOnce;
     if (c == PGRT_HOST_EXPORT_KERNEL) return kHostKernel;
-    return K > 1 ? kHostKernel : kHostOnce;
+    if (c == PGRT_HOST_EXPORT_SPLIT) return kHostSplit;
+    return K > 1 ? kHostKernel : kHostSplit;
 }
 
 // One sample batch of a PGRT_MODE_PATH frame (path.hip): raygen, then per bounce L the closest
@@ -623,6 +629,29 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
         FrameSlot* s0 = fs->slots[0].get();
         for (int j = 1; j < K; ++j) PGRT_HIP(hipStreamWaitEvent(s0->stream, fs->slots[j]->ev_done, 0));
         PGRT_HIP(hipMemcpyAsync(fs->host_dst, fs->host_src, fs->host_bytes, hipMemcpyDeviceToHost, s0->stream));
+        PGRT_HIP(hipEventRecord(s0->ev_done, s0->stream));
+    }
+    if (hx == kHostSplit) {  // after every slot: a blit kernel's share on host_aux beside one DMA copy
+#ifndef PGRT_HOST_SPLIT_PCT
+#define PGRT_HOST_SPLIT_PCT 50
+#endif
+        FrameSlot* s0 = fs->slots[0].get();
+        for (int j = 1; j < K; ++j) PGRT_HIP(hipStreamWaitEvent(s0->stream, fs->slots[j]->ev_done, 0));
+        if (!fs->host_aux) {
+            PGRT_HIP(hipStreamCreateWithFlags(&fs->host_aux, hipStreamNonBlocking));
+            PGRT_HIP(hipEventCreateWithFlags(&fs->ev_host0, hipEventDisableTiming));
+            PGRT_HIP(hipEventCreateWithFlags(&fs->ev_host1, hipEventDisableTiming));
+        }
+        const size_t kb = fs->host_bytes * PGRT_HOST_SPLIT_PCT / 100 / 256 * 256;  // 256-B aligned share
+        PGRT_HIP(hipEventRecord(fs->ev_host0, s0->stream));
+        PGRT_HIP(hipStreamWaitEvent(fs->host_aux, fs->ev_host0, 0));
+        launch_blit_host(fs->host_src, fs->host_map, kb, fs->host_aux);
+        PGRT_HIP(hipEventRecord(fs->ev_host1, fs->host_aux));
+        if (kb < fs->host_bytes)
+            PGRT_HIP(hipMemcpyAsync(reinterpret_cast<char*>(fs->host_dst) + kb,
+                                    reinterpret_cast<const char*>(fs->host_src) + kb, fs->host_bytes - kb,
+                                    hipMemcpyDeviceToHost, s0->stream));
+        PGRT_HIP(hipStreamWaitEvent(s0->stream, fs->ev_host1, 0));
         PGRT_HIP(hipEventRecord(s0->ev_done, s0->stream));
     }
     PGRT_HIP(hipGetLastError());

@@ -21,7 +21,6 @@
 namespace pgrt {
 
 constexpr int kBlock = 256;
-constexpr int kXcds = 8;  // MI355X: workgroups are dispatched round-robin over 8 XCDs
 
 // grid of a grid-stride kernel: cover the expected count, at most 4096 workgroups
 static int grid_for(int max_count, int expect) {
@@ -378,7 +377,7 @@ __global__ void k_overflow_flag(FlagSrc f, int* out) {
     int v = 0;
     for (int j = 0; j < f.K; ++j)
         for (int b = 0; b < f.n[j]; ++b) v |= f.fc[j][b].overflow;
-    out[0] = f.poison ? 2 : (v != 0 ? 1 : 0);
+    out[0] = gather_tail_flag(v != 0, f.poison != 0);
     out[1] = (int)f.seq;
 }
 
@@ -477,6 +476,27 @@ void launch_export_tiles(const int4* tiles, int ntiles, const float* src, float*
     hipLaunchKernelGGL(k_export_tiles, dim3(grid), dim3(kBlock), 0, stream, tiles, rows,
                        reinterpret_cast<const float4*>(src), reinterpret_cast<float4*>(dst_host), ox, oy, pitch,
                        frame_stride / 4, stamp_next(kStampExportTiles, -1, grid, kBlock));
+}
+
+// A linear share of a host-output call's framebuffer into page-locked memory (PGRT_HOST_EXPORT_SPLIT):
+// the copying workgroups on XCD 0 only, as k_export_tiles
+__global__ __launch_bounds__(kBlock) void k_blit_host(const float4* __restrict__ src, float4* __restrict__ dst,
+                                                      long long n4, unsigned long long* __restrict__ stamps) {
+    PGRT_STAMP_BEGIN(stamps);
+    if (blockIdx.x % kXcds == 0) {
+        const long long nthr = (long long)(gridDim.x / kXcds) * kBlock;
+        for (long long i = (long long)(blockIdx.x / kXcds) * kBlock + threadIdx.x; i < n4; i += nthr)
+            dst[i] = ld_stream(src + i);
+    }
+    PGRT_STAMP_END(stamps);
+}
+
+void launch_blit_host(const float* src, float* dst_host, size_t bytes, hipStream_t stream) {
+    const long long n4 = (long long)(bytes / 16);
+    if (n4 <= 0) return;
+    const int grid = kXcds * PGRT_EXPORT_WG;
+    hipLaunchKernelGGL(k_blit_host, dim3(grid), dim3(kBlock), 0, stream, reinterpret_cast<const float4*>(src),
+                       reinterpret_cast<float4*>(dst_host), n4, stamp_next(kStampExportTiles, -1, grid, kBlock));
 }
 
 // ------------------------------------------------------------------ counter export

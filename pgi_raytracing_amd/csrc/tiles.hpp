@@ -125,4 +125,33 @@ inline long long deal_offset(const TileDeal& d, int total, int rank) {
     return o;
 }
 
+// ---- the tail of a rank's distributed send (distributed.cpp collect_frame) ----
+// Two words after the rank's tiles: the flag (0 the frame is good, 1 its queues overflowed -- it
+// re-renders and sends again, 2 it gave up: "poison"), then the frame's sequence number (the
+// rank's count of distributed frames; 0 = nothing received from that rank in this gather).
+enum { kTailOk = 0, kTailOverflow = 1, kTailPoison = 2 };
+PGRT_TILE_HD inline int gather_tail_flag(bool overflow, bool poison) {
+    return poison ? kTailPoison : (overflow ? kTailOverflow : kTailOk);
+}
+// Rank 0's reading of the peers' tails of one gather: 0 and regather[r] = 1 for every rank whose
+// tiles must be received again; or -1 with *bad = the first rank that sent another frame's tiles
+// (the ranks do not submit / wait in the same order); or -2 with *bad = a rank that gave up.
+inline int gather_tail_verdict(const int* flags, const unsigned* seqs, int world, unsigned expect, int* regather,
+                               int* bad) {
+    for (int r = 0; r < world; ++r) regather[r] = 0;
+    for (int r = 1; r < world; ++r) {
+        if (seqs[r] == 0) continue;  // not received in this gather (a re-gather of other ranks)
+        if (seqs[r] != expect) {
+            *bad = r;
+            return -1;
+        }
+        if (flags[r] == kTailPoison) {
+            *bad = r;
+            return -2;
+        }
+        regather[r] = flags[r] != kTailOk;
+    }
+    return 0;
+}
+
 }  // namespace pgrt

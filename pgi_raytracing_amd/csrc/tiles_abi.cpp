@@ -36,6 +36,22 @@ int pgrt_tile_index(int width, int height, int tile_size, int rank, int world, i
     return pgrt_tile_index_ex(width, height, tile_size, rank, world, 0, 0, j);
 }
 
+int pgrt_gather_tail(int overflow, int poison, unsigned seq, int tail[2]) {
+    if (!tail || seq == 0) return PGRT_ERR_INVALID_ARGUMENT;
+    tail[0] = gather_tail_flag(overflow != 0, poison != 0);
+    tail[1] = (int)seq;
+    return PGRT_OK;
+}
+
+int pgrt_gather_tail_verdict(const int* flags, const unsigned* seqs, int world, unsigned expect_seq, int* regather,
+                             int* bad_rank) {
+    if (!flags || !seqs || !regather || world < 1 || world > 64 || expect_seq == 0) return PGRT_ERR_INVALID_ARGUMENT;
+    int bad = -1;
+    const int v = gather_tail_verdict(flags, seqs, world, expect_seq, regather, &bad);
+    if (bad_rank) *bad_rank = bad;
+    return v == 0 ? PGRT_OK : (v == -1 ? PGRT_ERR_RCCL : PGRT_ERR_OUT_OF_MEMORY);
+}
+
 int pgrt_tile_share(int world, int* a, int* b) {
     if (world <= 0 || !a || !b) return PGRT_ERR_INVALID_ARGUMENT;
     const TileDeal d = tile_deal(world);

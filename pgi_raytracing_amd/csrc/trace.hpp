@@ -52,6 +52,8 @@ inline int* fc_count_ptr(FrameCounters* f, int L) {
 }
 inline int* fc_shadow_counts(FrameCounters* f) { return reinterpret_cast<int*>(&f->alloc[0]) + 1; }
 
+constexpr int kXcds = 8;  // MI355X: workgroups are dispatched round-robin over 8 XCDs
+
 struct FrameParams {
     int spp_side;
     int max_level;
@@ -233,6 +235,8 @@ void launch_subtree(const SceneView& s, const FrameParams& fp, int level, Queue 
 // (device-visible address); framebuffer origin ox, oy, pitch in pixels, frame_stride in floats
 void launch_export_tiles(const int4* tiles, int ntiles, const float* src, float* dst_host, int ox, int oy, int pitch,
                          long long frame_stride, hipStream_t stream);
+// the first `bytes` of a device framebuffer into page-locked host memory (device-visible address)
+void launch_blit_host(const float* src, float* dst_host, size_t bytes, hipStream_t stream);
 void launch_export_counters(FrameCounters* dev, FrameCounters* host, int n, int* deep_dev, int* deep_host, int ndeep,
                             hipStream_t stream);
 // Distributed frames: rank r's tile-compact buffer (frame-major, count[r] tiles per frame in its

@@ -79,6 +79,9 @@ def lib():
         "pgrt_tile_share": (ip, [ip, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "pgrt_tile_rect": (ip, [ip, ip, ip, ip, C.POINTER(C.c_int)]),
         "pgrt_unpack_tiles_host": (ip, [ip, ip, ip, ip, fp, fp]),
+        "pgrt_gather_tail": (ip, [ip, ip, C.c_uint, C.POINTER(C.c_int)]),
+        "pgrt_gather_tail_verdict": (ip, [C.POINTER(C.c_int), C.POINTER(C.c_uint), ip, C.c_uint, C.POINTER(C.c_int),
+                                          C.POINTER(C.c_int)]),
         "pgrt_tile_count_ex": (ip, [ip, ip, ip, ip, ip, ip, ip]),
         "pgrt_tile_index_ex": (ip, [ip, ip, ip, ip, ip, ip, ip, ip]),
         "pgrt_unpack_tiles_host_ex": (ip, [ip, ip, ip, ip, ip, ip, fp, fp]),

@@ -18,10 +18,5 @@ python3 -c "import json; d=json.load(open('gpurun_out/bench_r5b_C5.json')); r=d[
 bash tools/profile.sh r5b C2 || exit 1
 echo "=== timeline"
 timeout -k 10 300 python3 tools/frame_timeline.py --out gpurun_out/timeline_r5b.json > gpurun_out/timeline_r5b.txt 2>&1 || { tail -5 gpurun_out/timeline_r5b.txt; exit 1; }
-echo "=== GPU suite under the host-sanitized library"
-RT=$(ls /opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so | head -1)
-env LD_PRELOAD="$RT" ASAN_OPTIONS=detect_leaks=0:halt_on_error=1 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 \
-    PGRT_LIB=build/asan/libpgrt.so \
-    timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread \
-    > gpurun_out/gpu_tests_asan_r5b.log 2>&1
-echo "asan gpu suite rc=$?"; tail -5 gpurun_out/gpu_tests_asan_r5b.log
+# (a GPU-suite pass under the host-sanitized library was tried here and abandoned: it replaced the
+# harness's preload; the sanitized host build runs on the CPU only, tools/asan_check.sh)

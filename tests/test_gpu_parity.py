@@ -897,10 +897,48 @@ def test_host_framebuffer_pinned_sync_equals_device(gpu_ctx, avenger_scene):
     W, H = 1920, 1080
     gpu_ctx.set_camera(abi.default_camera(W, H))
     gpu_ctx.set_frames_in_flight(1)
-    for mode in (0, 1, -1):  # pgrt_config.host_export: default, export kernels, one copy
-        gpu_ctx.configure(host_export=mode)
-        _host_frames_equal_device(gpu_ctx, W, H)
-    gpu_ctx.configure(host_export=0)
+    try:
+        for mode in (0, 1, -1, 2):  # pgrt_config.host_export: default, export kernels, one copy, split
+            gpu_ctx.configure(host_export=mode)
+            _host_frames_equal_device(gpu_ctx, W, H)
+    finally:
+        gpu_ctx.configure(host_export=0)
+
+
+def test_host_framebuffer_in_flight_modes_equal_device(gpu_ctx, avenger_scene):
+    """pgrt_render_frames_host_async (3 frames per call, 2 calls in flight) into page-locked
+    memory under every host_export mode -- one DMA copy, export kernels, and the split copy (a blit
+    kernel's share on a side stream beside the DMA copy of the rest) -- equals the device frames."""
+    gpu_ctx.set_scene(avenger_scene)
+    W, H, F = 640, 360, 3
+    gpu_ctx.set_camera(abi.default_camera(W, H))
+    params = [abi.make_params(max_level=5, jitter=abi.PGRT_JITTER_HASH, frame=20 + 3 * k) for k in range(2)]
+    dev = gpu_ctx.alloc(F * W * H * 16)
+    refs = []
+    try:
+        for p in params:
+            gpu_ctx.render_frames_device(p, F, dev)
+            refs.append(gpu_ctx.to_host(dev, (F, H, W, 4)))
+        gpu_ctx.set_frames_in_flight(2)
+        for mode in (0, 1, -1, 2):
+            gpu_ctx.configure(host_export=mode)
+            hb = [gpu_ctx.host_array((F, H, W, 4)) for _ in params]
+            try:
+                for a in hb:
+                    a.fill(-7.0)
+                ts = [gpu_ctx.render_frames_host_async(p, F, a) for p, a in zip(params, hb)]
+                for t in ts:
+                    gpu_ctx.render_wait(t)
+                for k, (a, ref) in enumerate(zip(hb, refs)):
+                    same = (a == ref) | (np.isnan(a) & np.isnan(ref))
+                    assert same.all(), f"host_export {mode} call {k}: {(~same).sum()} pixels differ"
+            finally:
+                for a in hb:
+                    gpu_ctx.host_free(a)
+    finally:
+        gpu_ctx.configure(host_export=0)
+        gpu_ctx.set_frames_in_flight(1)
+        gpu_ctx.free(dev)
 
 
 def _host_frames_equal_device(gpu_ctx, W, H):
