@@ -3,6 +3,8 @@
 // context stream, queued behind the frame on the device) and unpacked there; the queue-overflow
 // agreement (a flag at the tail of every rank's send); the single-process multi-device context
 // (pgrt_create_devices); and the distributed C ABI.
+#include <thread>
+
 #include "context.hpp"
 
 using namespace pgrt;
@@ -29,8 +31,27 @@ bool rccl_gather(const pgrt_ctx* ctx, const FrameSet* fs) {
 // instead of unpacking another frame's tiles.  A rank that gives up after kMaxRetries re-renders
 // still sends (flag 2, "poison"), so rank 0's receive completes and rank 0 fails too instead of
 // waiting forever.  Non-zero ranks never wait for another rank; rank 0 waits for the frame's own
-// gather only.
+// gather only, and at most kPeerWaitSeconds (a rank that died without sending).
 constexpr int kMaxRetries = 8;
+// Rank 0's wait for the peers' tiles of one gather is bounded: a peer that died or never submitted
+// the frame leaves rank 0's ncclRecv pending forever, and the caller gets PGRT_ERR_RCCL instead of a
+// hang (the communicator is unusable after that; the process should tear it down)
+constexpr double kPeerWaitSeconds = 120.0;
+
+// hipEventSynchronize with a time limit: spin on hipEventQuery for the first 2 ms (a frame's gather
+// usually lands within it), then poll every 50 us; false on timeout
+bool wait_event_bounded(hipEvent_t e, double seconds) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t q = hipEventQuery(e);
+        if (q == hipSuccess) return true;
+        if (q != hipErrorNotReady) PGRT_HIP(q);
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (el > seconds) return false;
+        if (el > 2e-3) std::this_thread::sleep_for(std::chrono::microseconds(50));
+        else std::this_thread::yield();
+    }
+}
 
 void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
     int retries = 0;
@@ -49,7 +70,10 @@ void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
             if (fs->distributed) gather_frame(ctx, fs);  // rank != 0: the tiles again, to rank 0
             continue;
         }
-        PGRT_HIP(hipEventSynchronize(fs->ev_flags));
+        PGRT_REQUIRE(wait_event_bounded(fs->ev_flags, kPeerWaitSeconds), PGRT_ERR_RCCL,
+                     "rank 0 received no tiles of distributed frame " + std::to_string(fs->gather_seq) + " within " +
+                         std::to_string((int)kPeerWaitSeconds) +
+                         " s: a rank failed or did not submit the frame (the communicator is unusable now)");
         std::vector<int> peers;
         {
             const int world = fs->deal.world;
