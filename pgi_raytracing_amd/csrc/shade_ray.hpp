@@ -198,6 +198,122 @@ __device__ __forceinline__ void shade_eval(const SceneView& s, const DevMaterial
     shade_hit(s, mats, lut, level, max_level, d, rtime, h, load_attr(s, h), r);
 }
 
+// shade_eval in two parts around the block's slot allocation (k_shade's bounce levels): part A
+// settles what the allocation needs -- the kind and the children / shadow-ray counts (hit,
+// attributes, normal, material, reflection / refraction directions) -- and part B, run while the
+// allocation atomic is in flight, the long-latency colours: a miss's environment texel, a textured
+// hit's texel, a dielectric's attenuation and R.  Same functions, same float operations in the same
+// order per value: bit-identical to shade_eval.
+struct ShadeDefer {
+    float t, tu, tv;  // hit distance (attenuation), texture coordinates (textured opaque hits)
+};
+__device__ __forceinline__ void shade_eval_a(const SceneView& s, const DevMaterial* mats, int level, int max_level,
+                                             bool active, float4 o4, float4 d4, float rtime, float4 h, ShadeOut& r,
+                                             ShadeDefer& df) {
+    shade_init(r);
+    df.t = df.tu = df.tv = 0.0f;
+    if (!active) return;
+    r.org = v3(o4.x, o4.y, o4.z);
+    r.dirraw = v3(d4.x, d4.y, d4.z);
+    if (d4.w < 0.0f) {
+        r.color = make_float4(0, 0, 0, 0);  // padding slot
+        return;
+    }
+    const int prim = __float_as_int(h.w);
+    if (prim < 0) {
+        r.kind = 3;  // a miss: its environment texel in part B (raytracer.cpp:390-393)
+        return;
+    }
+    const V3 d = normalize(r.dirraw);
+    const HitAttr ha = load_attr(s, h);
+    const float* a = ha.f;
+    const float t = h.x, u = h.y, v = h.z;
+    V3 nn = v3(interp1(a[0], a[3], a[6], u, v), interp1(a[1], a[4], a[7], u, v), interp1(a[2], a[5], a[8], u, v));
+    const int mid = __float_as_int(a[15]);
+    const DevMaterial& m = mats[mid];
+    nn = normalize(nn);
+    const V3 hitp = r.org + scale(t, r.dirraw);
+    float n1, n2;
+    if (rtime == PGRT_IOR_AIR) {
+        n1 = PGRT_IOR_AIR;
+        n2 = m.ior;
+    } else {
+        n1 = m.ior;
+        n2 = PGRT_IOR_AIR;
+    }
+    if (dot(nn, d) > 0) nn = -nn;
+    r.mid = mid;
+    r.hitp = hitp;
+    r.n1 = n1;
+    r.n2 = n2;
+    r.nrm = nn;
+    if (level >= max_level) return;  // r.color (0, 0, 0, 1): raytracer.cpp:282-283
+    if (m.type == PGRT_MATERIAL_DIELECTRIC) {
+        V3 refl, refr;
+        {  // get_reflection_ray (raytracer.cpp:209-235)
+            const V3 dd = normalize(d), rn = normalize(nn);
+            refl = dd - scale(2, scale(dot(dd, rn), rn));
+        }
+        {  // get_refraction_ray (raytracer.cpp:178-207)
+            const V3 dd = normalize(d), rn = normalize(nn);
+            const float n1_n2 = n1 / n2;
+            const float d_n = dot(dd, rn);
+            const V3 sd = v3(dd.x * n1_n2, dd.y * n1_n2, dd.z * n1_n2);
+            const float kk = n1_n2 * d_n + sqrtf(1 - ((n1_n2 * n1_n2) * (1 - (d_n * d_n))));
+            refr = sd - scale(kk, rn);
+        }
+        r.kind = 1;
+        r.nchild = refr.x == refr.x ? 2 : 1;  // 1: total internal reflection
+        r.refl_dir = refl;
+        r.refr_dir = refr;
+        df.t = t;
+    } else {
+        if (m.tex >= 0) {
+            df.tu = interp1(a[9], a[11], a[13], u, v);
+            df.tv = interp1(a[10], a[12], a[14], u, v);
+        }
+        int nshadow = 0;
+        for (int li = 0; li < s.nlight; ++li) {
+            const DevLight& L = s.lights[li];
+            if (!(dot(nn, v3(L.pos[0], L.pos[1], L.pos[2])) < 0)) ++nshadow;
+        }
+        r.kind = 2;
+        r.nshadow = nshadow;
+    }
+}
+__device__ __forceinline__ void shade_eval_b(const SceneView& s, const DevMaterial* mats, const float* lut,
+                                             ShadeOut& r, const ShadeDefer& df) {
+    if (r.kind == 3) {
+        r.color = env_texel(s, lut, normalize(r.dirraw));
+        r.kind = 0;
+    } else if (r.kind == 1) {
+        const DevMaterial& m = mats[r.mid];
+        const float ax = pg_expf(-(1 - m.kd[0]) * df.t);  // raytracer.cpp:303-305
+        const float ay = pg_expf(-(1 - m.kd[1]) * df.t);
+        const float az = pg_expf(-(1 - m.kd[2]) * df.t);
+        float R = 0.0f;
+        if (r.nchild == 2) {
+            const V3 d = normalize(r.dirraw);
+            const float cos1 = fabsf(dot(r.nrm, -d));
+            const float alpha = (r.n1 - r.n2) / (r.n1 + r.n2);
+            R = (float)((double)(alpha * alpha + (1 - (alpha * alpha))) * pg_pow_d((double)(1 - cos1), 5.0));
+        }
+        r.att = make_float4(ax, ay, az, R);
+    } else if (r.kind == 2) {
+        const DevMaterial& m = mats[r.mid];
+        if (m.tex < 0) {
+            r.m_d_r = m.kd[2];
+            r.m_d_g = m.kd[1];
+            r.m_d_b = m.kd[0];
+        } else {
+            const V3 tx = tex_texel(s.tex[m.tex], s.texels, lut, df.tu, 1.0f - df.tv);
+            r.m_d_r = tx.x;
+            r.m_d_g = tx.y;
+            r.m_d_b = tx.z;
+        }
+    }
+}
+
 // LDS of the block-level allocation (BLOCK threads)
 template <int BLOCK>
 struct ShadeAllocLds {
