@@ -138,7 +138,10 @@ __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : 6) void k_shade
 #ifndef PGRT_SHADE_SPLIT
 #define PGRT_SHADE_SPLIT 1
 #endif
-        constexpr bool split = PGRT_SHADE_SPLIT && !L0F;  // bounce levels: colours behind the allocation
+#ifndef PGRT_SHADE_SPLIT_L0
+#define PGRT_SHADE_SPLIT_L0 1
+#endif
+        constexpr bool split = PGRT_SHADE_SPLIT && (!L0F || PGRT_SHADE_SPLIT_L0);  // colours behind the allocation
         ShadeDefer df;
         if constexpr (split)
             shade_eval_a(s, mats, level, fp.max_level, active, cur_o, cur_d, cur_t, cur_h, r, df);
