@@ -47,7 +47,10 @@ struct SubFrameRef {
 };
 
 template <int G, bool LDS_TABLES, bool COUNT>
-__global__ __launch_bounds__(kSubtreeBlock) void k_subtree(SceneView s, FrameParams fp, int level, Queue q,
+#ifndef PGRT_SUBTREE_WAVES
+#define PGRT_SUBTREE_WAVES 1
+#endif
+__global__ __launch_bounds__(kSubtreeBlock, PGRT_SUBTREE_WAVES) void k_subtree(SceneView s, FrameParams fp, int level, Queue q,
                                                            LevelNodes nodes, FrameCounters* fc, int frames) {
     PGRT_STAMP_BEGIN(s.stamps);
     constexpr int kGroups = kSubtreeBlock / G;
