@@ -220,11 +220,10 @@ typedef struct pgrt_config {
                              (the frame's critical path) start after a short level 0 while the
                              other slot's level 0 still runs; -1 = tiles dealt round-robin */
     int host_export;    /* frames into page-locked host memory (pgrt_render,
-                             pgrt_render_frames_host_async): 0 = default -- a synchronous two-slot
-                             frame exports each slot's finished tiles with a small blit kernel as
-                             soon as that slot is done (the bulk slot's pixels cross PCIe while the
-                             deep-tile slot still renders), frames in flight take the split copy
-                             (below) per call; PGRT_HOST_EXPORT_KERNEL = export kernels always;
+                             pgrt_render_frames_host_async): 0 = default -- each pipeline slot exports
+                             its finished tiles with a small blit kernel as soon as that slot is done
+                             (a synchronous frame's bulk slot crosses PCIe while its deep-tile slot
+                             still renders; a call in flight right after its frames); PGRT_HOST_EXPORT_KERNEL = export kernels always;
                              PGRT_HOST_EXPORT_COPY = one DMA copy after every frame (pageable
                              destinations always take the copy); PGRT_HOST_EXPORT_SPLIT = after every
                              frame, part of the bytes by a blit kernel on XCD 0 and the rest by a
@@ -312,8 +311,8 @@ int pgrt_render_frames_device(pgrt_ctx* ctx, const pgrt_render_params* p, int nf
 /* Batched frames to a HOST framebuffer (the reference's Producer hands every finished frame to
  * the host-side D3D texture, APP/simpleguidx11.cpp:105-124): frames are rendered into a device
  * staging buffer owned by the frame in flight, then the nframes * W*H*4 floats move into
- * rgba_host behind them (pgrt_config.host_export: by default half by a copy kernel on XCD 0 and
- * half by one DMA copy, concurrently), so the PCIe transfer of one call overlaps the rendering of
+ * rgba_host behind them (pgrt_config.host_export: by default a copy kernel on XCD 0), so the PCIe
+ * transfer of one call overlaps the rendering of
  * the calls in flight behind it.  rgba_host must stay valid until the ticket is waited for; pinned
  * memory from pgrt_host_alloc makes the copy truly asynchronous (pageable memory works but takes
  * one synchronous DMA copy).  Same pixels as pgrt_render_frames_device. */

@@ -280,10 +280,11 @@ void probe_side_launch(pgrt_ctx* ctx, const SceneView& view, FrameSlot* sl, Fram
 // calls in flight 0.61-0.65 ms/frame with one DMA copy per call, 0.76-0.83 with export kernels
 // (their stores slow the other calls' rendering).  But a process's SDMA rate is not fixed: the
 // same copy runs at 27 or 54 GB/s (r5k / r5l / r5n probes: typically the first process on a box),
-// where the blit kernel stays at 53-54.  So frames in flight take the split copy by default: half
-// the call's bytes by an XCD-0 blit kernel on a side stream, the other half by one DMA copy at the
-// same time (r5m, in-process A/B, 8 frames x 4 calls: 0.656-0.66 ms/frame; DMA 0.63-0.76; export
-// kernels 0.67-0.69; a 70 % kernel share 0.70-0.75).
+// where the blit kernel stays at 53-54.  In-process A/B on a fast-SDMA box (r5m, 8 frames x 4
+// calls): DMA 0.63-0.76 ms/frame, half kernel + half DMA concurrently (split) 0.656-0.66, export
+// kernels 0.67-0.69; on slow-SDMA boxes the bench line read DMA 0.93-0.96 (r5fin) and split 0.84
+// (r5fin2).  So every page-locked destination takes the export kernels by default -- the one form
+// whose rate does not depend on the box -- and split / DMA stay selectable.
 enum { kHostNone = 0, kHostKernel = 1, kHostOnce = 2, kHostSplit = 3 };
 int host_export_mode(const pgrt_ctx* ctx, const FrameSet* fs, int K) {
     if (!fs->host_dst || K == 0) return kHostNone;
@@ -291,7 +292,7 @@ int host_export_mode(const pgrt_ctx* ctx, const FrameSet* fs, int K) {
     if (c == PGRT_HOST_EXPORT_COPY || !fs->host_map) return kHostOnce;
     if (c == PGRT_HOST_EXPORT_KERNEL) return kHostKernel;
     if (c == PGRT_HOST_EXPORT_SPLIT) return kHostSplit;
-    return K > 1 ? kHostKernel : kHostSplit;
+    return kHostKernel;
 }
 
 // One sample batch of a PGRT_MODE_PATH frame (path.hip): raygen, then per bounce L the closest
