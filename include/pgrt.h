@@ -205,7 +205,8 @@ typedef struct pgrt_config {
     int subtree_level;    /* Whitted levels >= k evaluated as whole ray trees, one launch (every ray of
                              level k traces and shades its reflection / refraction / shadow rays
                              depth first, as the reference's recursive trace does): 0 = default
-                             (from level 3 for one-frame batches of scenes up to 262144 triangles,
+                             (one-frame batches of scenes up to 262144 triangles: from level 2 for
+                             synchronous frames, from level 3 with frames in flight;
                              one launch per level otherwise), -1 = one launch per level, k >= 1 =
                              from level k */
     int call_order;     /* frames in flight: 1 = each call's level-0 trace waits for the previous

@@ -209,16 +209,19 @@ std::vector<std::vector<int4>> deal_tiles(pgrt_ctx* ctx, FrameSet* fs, int K) {
 
 // first level evaluated as whole ray trees in one launch (pgrt_config.subtree_level, subtree.hip),
 // -1 = one launch per level
-// Default: from level kSubtreeLevelSmall for one-frame batches of scenes up to kPacketBigScene
-// triangles (the synchronous frame: levels 3.. are a few ten thousand rays whose per-level
-// launches each last as long as their slowest ray; r4l timeline 0.583-0.597 -> 0.563 ms), one
+// Default: one-frame batches of scenes up to kPacketBigScene triangles -- synchronous frames from
+// level kSubtreeLevelSync, one-frame calls in flight from kSubtreeLevelSmall (the synchronous
+// frame's deep levels are a few ten thousand rays whose per-level launches each last as long as
+// their slowest ray; r4l timeline 0.583-0.597 -> 0.563 ms from level 3, r5za 0.556 -> 0.530 ms
+// from level 2; calls in flight lose throughput from level 2: 0.255 -> 0.290 ms/frame), one
 // launch per level otherwise (the subtree launch's 8 lanes per ray cost multi-frame calls
 // throughput: r4h driver line 0.179 -> 0.209 ms/frame).
 int subtree_first(const pgrt_ctx* ctx, const SceneView& view, const pgrt_render_params* p, bool small_batch) {
     const int k = ctx->cfg.subtree_level;
     if (k < 0 || p->mode != PGRT_MODE_WHITTED || !subtree_available(view)) return -1;
     if (k > 0) return k <= p->max_level ? k : -1;
-    return small_batch && view.ntri <= kPacketBigScene && kSubtreeLevelSmall <= p->max_level ? kSubtreeLevelSmall : -1;
+    const int first = ctx->frames_in_flight > 1 ? kSubtreeLevelSmall : kSubtreeLevelSync;
+    return small_batch && view.ntri <= kPacketBigScene && first <= p->max_level ? first : -1;
 }
 
 // step budget of the bounce levels' packet launches (pgrt_config.packet_budget)

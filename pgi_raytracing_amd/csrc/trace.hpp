@@ -286,8 +286,11 @@ constexpr int kDefaultPacketBudget = 256;
 // on their bounce levels (context.cpp packet_budget)
 constexpr int kSmallPacketBatch = 1 << 22;
 constexpr int kSmallBatchPacketBudget = 64;
-// one-frame batches: levels >= this as whole ray trees in one launch (pgrt_config.subtree_level)
+// one-frame batches: levels >= this as whole ray trees in one launch (pgrt_config.subtree_level);
+// synchronous frames (one frame in flight) from level 2 (r5za: 0.556 -> 0.530 ms), one-frame calls
+// in flight from level 3 (from level 2 their throughput drops: 0.255 -> 0.290 ms/frame)
 constexpr int kSubtreeLevelSmall = 3;
+constexpr int kSubtreeLevelSync = 2;
 // "big" scenes (BVH + triangles far beyond the L2, fetches served by the MALL / HBM): the
 // level-0 packet kernel is built for 8 waves (trace.hip), level 0 of calls in flight is ordered
 // (context.cpp call_ordered)
