@@ -135,18 +135,10 @@ __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : 6) void k_shade
             }
         }
         ShadeOut r;
-#ifndef PGRT_SHADE_SPLIT
-#define PGRT_SHADE_SPLIT 1
-#endif
-#ifndef PGRT_SHADE_SPLIT_L0
-#define PGRT_SHADE_SPLIT_L0 1
-#endif
-        constexpr bool split = PGRT_SHADE_SPLIT && (!L0F || PGRT_SHADE_SPLIT_L0);  // colours behind the allocation
+        // the kind and slot counts first, the long-latency colours while the allocation atomic is
+        // in flight (shade_eval_a / _b; r5s / r5t)
         ShadeDefer df;
-        if constexpr (split)
-            shade_eval_a(s, mats, level, fp.max_level, active, cur_o, cur_d, cur_t, cur_h, r, df);
-        else
-            shade_eval(s, mats, lut255, level, fp.max_level, active, cur_o, cur_d, cur_t, cur_h, r);
+        shade_eval_a(s, mats, level, fp.max_level, active, cur_o, cur_d, cur_t, cur_h, r, df);
         if (level == 0 && fp.tile_deep) {  // a wave lies in one tile (4096 * nsb rays per tile)
             const unsigned long long dm = __ballot(active && r.nchild > 0);
             if (dm != 0ull && __lane_id() == 0) fp.tile_deep[(i / fp.nsb) / (kTile * kTile)] = 1;
@@ -159,14 +151,9 @@ __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : 6) void k_shade
                 atomicAdd(&fc->shade[level][1], (unsigned long long)__popcll(tm));
             }
         }
-        ShadeSlots sl;
-        if constexpr (split) {
-            const ShadeAllocPending pa = shade_alloc_begin<kShadeBlock>(alds, it_par, fc, level, sbits, r, &refr_acc);
-            shade_eval_b(s, mats, lut255, r, df);
-            sl = shade_alloc_end<kShadeBlock>(alds, it_par, sq_base, pa);
-        } else {
-            sl = shade_alloc<kShadeBlock>(alds, it_par, fc, level, sq_base, sbits, r, &refr_acc);
-        }
+        const ShadeAllocPending pa = shade_alloc_begin<kShadeBlock>(alds, it_par, fc, level, sbits, r, &refr_acc);
+        shade_eval_b(s, mats, lut255, r, df);
+        const ShadeSlots sl = shade_alloc_end<kShadeBlock>(alds, it_par, sq_base, pa);
         if constexpr (l0final) {
             // a final colour (environment texel; padding; a hit at max_level) -> the pixel, now;
             // the others are completed by the finish (n is a multiple of 64: whole waves)

@@ -89,116 +89,7 @@ __device__ __forceinline__ void shade_init(ShadeOut& r) {
     r.mid = 0;
 }
 
-// Phase 1, hit part: the ray (r.org, r.dirraw set; d = normalize(r.dirraw)) hit triangle h.w,
-// whose shading attributes are ha (raytracer.cpp:246-386 up to the emitted rays).
-__device__ __forceinline__ void shade_hit(const SceneView& s, const DevMaterial* mats, const float* lut, int level,
-                                          int max_level, V3 d, float rtime, float4 h, const HitAttr& ha,
-                                          ShadeOut& r) {
-    // every ShadeOut field is written whole, once, at the end of its branch: partial stores of a
-    // member in some branches only (r.att.w, r.color) let the optimiser merge them into one store
-    // through a phi of addresses, which kept ShadeOut in scratch memory (measured: wrong pixels)
-    const float t = h.x;
-    const float* a = ha.f;
-    const float u = h.y, v = h.z;
-    V3 nn = v3(interp1(a[0], a[3], a[6], u, v), interp1(a[1], a[4], a[7], u, v), interp1(a[2], a[5], a[8], u, v));
-    const int mid = __float_as_int(a[15]);
-    const DevMaterial& m = mats[mid];
-    nn = normalize(nn);
-    const V3 hitp = r.org + scale(t, r.dirraw);
-    float n1, n2;
-    if (rtime == PGRT_IOR_AIR) {
-        n1 = PGRT_IOR_AIR;
-        n2 = m.ior;
-    } else {
-        n1 = m.ior;
-        n2 = PGRT_IOR_AIR;
-    }
-    if (dot(nn, d) > 0) nn = -nn;
-    r.mid = mid;
-    r.hitp = hitp;
-    r.n1 = n1;
-    r.n2 = n2;
-    r.nrm = nn;
-    if (level >= max_level) return;  // r.color (0, 0, 0, 1): raytracer.cpp:282-283
-    if (m.type == PGRT_MATERIAL_DIELECTRIC) {
-        V3 refl, refr;
-        {  // get_reflection_ray (raytracer.cpp:209-235)
-            const V3 dd = normalize(d), rn = normalize(nn);
-            refl = dd - scale(2, scale(dot(dd, rn), rn));
-        }
-        const float ax = pg_expf(-(1 - m.kd[0]) * t);  // raytracer.cpp:303-305
-        const float ay = pg_expf(-(1 - m.kd[1]) * t);
-        const float az = pg_expf(-(1 - m.kd[2]) * t);
-        {  // get_refraction_ray (raytracer.cpp:178-207)
-            const V3 dd = normalize(d), rn = normalize(nn);
-            const float n1_n2 = n1 / n2;
-            const float d_n = dot(dd, rn);
-            const V3 sd = v3(dd.x * n1_n2, dd.y * n1_n2, dd.z * n1_n2);
-            const float kk = n1_n2 * d_n + sqrtf(1 - ((n1_n2 * n1_n2) * (1 - (d_n * d_n))));
-            refr = sd - scale(kk, rn);
-        }
-        int nchild = 1;
-        float R = 0.0f;
-        if (refr.x == refr.x) {  // no total internal reflection
-            nchild = 2;
-            const float cos1 = fabsf(dot(nn, -d));
-            const float alpha = (n1 - n2) / (n1 + n2);
-            R = (float)((double)(alpha * alpha + (1 - (alpha * alpha))) * pg_pow_d((double)(1 - cos1), 5.0));
-        }
-        r.kind = 1;
-        r.nchild = nchild;
-        r.refl_dir = refl;
-        r.refr_dir = refr;
-        r.att = make_float4(ax, ay, az, R);
-    } else {
-        float mr, mg, mb;
-        if (m.tex < 0) {
-            mr = m.kd[2];
-            mg = m.kd[1];
-            mb = m.kd[0];
-        } else {
-            const float tu = interp1(a[9], a[11], a[13], u, v);
-            const float tv = interp1(a[10], a[12], a[14], u, v);
-            const V3 tx = tex_texel(s.tex[m.tex], s.texels, lut, tu, 1.0f - tv);
-            mr = tx.x;
-            mg = tx.y;
-            mb = tx.z;
-        }
-        int nshadow = 0;
-        for (int li = 0; li < s.nlight; ++li) {
-            const DevLight& L = s.lights[li];
-            if (!(dot(nn, v3(L.pos[0], L.pos[1], L.pos[2])) < 0)) ++nshadow;
-        }
-        r.kind = 2;
-        r.m_d_r = mr;
-        r.m_d_g = mg;
-        r.m_d_b = mb;
-        r.nshadow = nshadow;
-    }
-}
-
-// Phase 1 for one ray (o4 = org|tnear, d4 = dir|tfar, rtime = medium IOR, h = t|u|v|prim).
-__device__ __forceinline__ void shade_eval(const SceneView& s, const DevMaterial* mats, const float* lut,
-                                           int level, int max_level, bool active, float4 o4, float4 d4,
-                                           float rtime, float4 h, ShadeOut& r) {
-    shade_init(r);
-    if (!active) return;
-    r.org = v3(o4.x, o4.y, o4.z);
-    r.dirraw = v3(d4.x, d4.y, d4.z);
-    if (d4.w < 0.0f) {
-        r.color = make_float4(0, 0, 0, 0);  // padding slot
-        return;
-    }
-    const V3 d = normalize(r.dirraw);
-    const int prim = __float_as_int(h.w);
-    if (prim < 0) {
-        r.color = env_texel(s, lut, d);  // miss (raytracer.cpp:390-393)
-        return;
-    }
-    shade_hit(s, mats, lut, level, max_level, d, rtime, h, load_attr(s, h), r);
-}
-
-// shade_eval in two parts around the block's slot allocation (k_shade's bounce levels): part A
+// Phase 1 in two parts around the block's slot allocation (k_shade): part A
 // settles what the allocation needs -- the kind and the children / shadow-ray counts (hit,
 // attributes, normal, material, reflection / refraction directions) -- and part B, run while the
 // allocation atomic is in flight, the long-latency colours: a miss's environment texel, a textured
@@ -312,6 +203,16 @@ __device__ __forceinline__ void shade_eval_b(const SceneView& s, const DevMateri
             r.m_d_b = tx.z;
         }
     }
+}
+
+// Phase 1 for one ray (o4 = org|tnear, d4 = dir|tfar, rtime = medium IOR, h = t|u|v|prim): both
+// parts back to back (the subtree and path kernels, which allocate no queue slots)
+__device__ __forceinline__ void shade_eval(const SceneView& s, const DevMaterial* mats, const float* lut,
+                                           int level, int max_level, bool active, float4 o4, float4 d4,
+                                           float rtime, float4 h, ShadeOut& r) {
+    ShadeDefer df;
+    shade_eval_a(s, mats, level, max_level, active, o4, d4, rtime, h, r, df);
+    shade_eval_b(s, mats, lut, r, df);
 }
 
 // LDS of the block-level allocation (BLOCK threads)
