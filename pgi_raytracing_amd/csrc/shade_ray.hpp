@@ -1,9 +1,14 @@
 // shade_ray.hpp -- the per-ray Whitted shading step (APP/raytracer.cpp:237-394, one level of
-// Raytracer::trace), in three phases (k_shade, render.hip):
-//   shade_eval   what the ray's hit produces (final colour, dielectric children, shadow rays)
-//   shade_alloc  queue slots for the children / shadow rays: ballot + mbcnt inside the wave, ONE
-//                packed 64-bit atomic (children | shadow rays << 32) per block and iteration
-//   shade_emit   writes the children, the shadow rays with their Phong terms and the node record
+// Raytracer::trace), in phases (k_shade, render.hip):
+//   shade_eval_a  what the ray's hit produces and how many queue slots it needs (kind, dielectric
+//                 children, shadow rays)
+//   shade_alloc   queue slots for the children / shadow rays: ballot + mbcnt inside the wave, ONE
+//                 packed 64-bit atomic (children | shadow rays << 32) per block and iteration --
+//                 split in _begin / _end, and between them
+//   shade_eval_b  the long-latency colours (environment / texture fetch, attenuation, R) while the
+//                 atomic is in flight
+//   shade_emit    writes the children, the shadow rays with their Phong terms and the node record
+// (shade_eval = _a then _b, for the kernels that allocate no slots: subtree, path tracer)
 // Float operation order is the reference's (see shade_ops.hpp), so results are bit-identical
 // wherever the phases run.
 #pragma once
