@@ -464,7 +464,11 @@ __device__ __forceinline__ int pkt_nodes(const cfloat_ptr nodes, int node, int& 
         if constexpr (BUDGET) {
             if (++steps > budget) return kDefer;
         }
-        const cfloat_ptr nd = nodes + 16 * node;
+        // the pop target, read before the node loads (wstk[0] holds kSentinel): one wait for both
+        const int top = __builtin_amdgcn_readfirstlane(wstk[sp]);
+        // base + zero-extended 32-bit byte offset: the scalar loads take it as their offset operand
+        const cfloat_ptr nd = (cfloat_ptr)((const __attribute__((address_space(4))) char*)nodes +
+                                           (unsigned long long)((unsigned)node << 6));
         const float4 a = cload4(nd), b = cload4(nd + 4), c = cload4(nd + 8);
         const int4 d = make_int4(__float_as_int(nd[12]), __float_as_int(nd[13]), __float_as_int(nd[14]),
                                  __float_as_int(nd[15]));
@@ -490,13 +494,14 @@ __device__ __forceinline__ int pkt_nodes(const cfloat_ptr nodes, int node, int& 
         }
         const unsigned long long b0 = __ballot(h0), b1 = __ballot(h1);
         if (b0 == 0ull && b1 == 0ull) {
-            node = sp > 0 ? __builtin_amdgcn_readfirstlane(wstk[--sp]) : kSentinel;
+            node = top;  // kSentinel at sp == 0: the traversal is over (sp -1 is never read)
+            --sp;
         } else if (b0 != 0ull && b1 != 0ull) {
             // nearer first, by majority of the lanes that hit both
             const unsigned long long near0 = __ballot(h0 && h1 && t0 <= t1);
             const unsigned long long both = b0 & b1;
             const bool first0 = 2 * __popcll(near0) >= __popcll(both);
-            wstk[sp++] = first0 ? d.y : d.x;
+            wstk[++sp] = first0 ? d.y : d.x;
             node = first0 ? d.x : d.y;
         } else {
             node = b0 != 0ull ? d.x : d.y;
@@ -527,6 +532,7 @@ __device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __re
     // stream the ray needed (pgrt_config.packet_levels AUTO decides per level from it)
     constexpr bool sample = SAMPLE;
     unsigned useful = 0, live_steps = 0;
+    if (lane == 0) wstack[wib][0] = kSentinel;  // the bottom entry: entries are wstack[wib][1..sp]
     for (int base = (blockIdx.x * kTraceBlock) + wib * 64; base < n; base += gridDim.x * kTraceBlock) {
         const int slot_i = base + lane;
         const bool valid = slot_i < n;
@@ -602,15 +608,19 @@ __device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __re
             const int first = leaf_first(node), end = first + leaf_count(node);
             if constexpr (BUDGET) steps += end - first;
             for (int k = first; k < end; ++k) {
-                const cfloat_ptr q = tris + 12 * k;
+                // base + zero-extended 32-bit byte offsets (scalar-load offset operands, as the nodes)
+                const cfloat_ptr q = (cfloat_ptr)((const __attribute__((address_space(4))) char*)tris +
+                                                  (unsigned long long)((unsigned)k * 48u));
                 const float4 q0 = cload4(q), q1 = cload4(q + 4), q2 = cload4(q + 8);
                 if (COUNT) ++rtest;
-                const float4 ng = cload4((cfloat_ptr)(const void*)s.tri_ng + 4 * k);  // precomputed Ng
+                const float4 ng = cload4((cfloat_ptr)((const __attribute__((address_space(4))) char*)s.tri_ng +
+                                                      (unsigned long long)((unsigned)k << 4)));  // precomputed Ng
                 if (live)
                     tri_test_ng(q0, q1, q2, ng, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v,
                                 best_prim);
             }
-            node = sp > 0 ? __builtin_amdgcn_readfirstlane(wstack[wib][--sp]) : kSentinel;
+            node = __builtin_amdgcn_readfirstlane(wstack[wib][sp]);  // wstack[wib][0]: kSentinel
+            sp -= sp > 0 ? 1 : 0;
         }
         if constexpr (GEN) {
             if (gen.hitmask) {  // 1-spp level 0 (L0Final): hit records of the hits only + the wave's mask
@@ -704,8 +714,12 @@ void set_trace_events(hipEvent_t start, hipEvent_t stop) {
 #define PGRT_TLAUNCH(kernel, grid, block, lds, stream, ...) \
     hipExtLaunchKernelGGL(kernel, grid, block, lds, stream, t_ev_start, t_ev_stop, 0, __VA_ARGS__)
 
+// the packet kernel addresses nodes and triangles by 32-bit byte offsets (node << 6, reference * 48):
+// scenes up to 2^24 triangles (with split budgets up to 4x, references stay below 2^32 / 48 B and
+// nodes below 2^26)
+constexpr int kPktMaxTris = 1 << 24;
 bool trace_packets_available(const SceneView& s) {
-    return !s.wide && s.root >= 0 && s.depth + 2 <= kPktStack;
+    return !s.wide && s.root >= 0 && s.depth + 2 <= kPktStack && s.ntri <= kPktMaxTris;
 }
 
 // 4 lanes per ray (two child slots each) above this many rays, 8 at or below it (r1 A/B)
