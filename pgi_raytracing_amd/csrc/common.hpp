@@ -122,6 +122,14 @@ __host__ __device__ inline unsigned wide_leaf_bits(unsigned meta) {  // the leaf
     return ((2u << ((meta >> 5) & 3u)) - 1u) << (meta & 31u);
 }
 
+// base + a 32-bit byte offset, zero-extended: a global load then takes the (wave-uniform) base as
+// its scalar address operand and the offset as one VGPR -- no 64-bit address arithmetic per node or
+// triangle.  Every BVH / triangle array of a scene stays below 4 GiB (scene.cpp checks the sizes).
+template <class T>
+__device__ __forceinline__ const T* at_bytes(const T* base, unsigned off) {
+    return reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + off);
+}
+
 struct SceneView {  // kernel-argument view of the device scene
     const float4* tri;     // 3 x float4 per sorted triangle: (v0, orig id bits) (e1) (e2)
     const float4* tri_ng;  // per sorted triangle: its Ng = e2 x e1 (tri_normal), w = 0

@@ -182,6 +182,10 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
         build_lbvh(pos.p, n, ctx->tri.p, ctx->nodes.p, scratch.p, sort_tmp.p, tmp_bytes, pad, &bo, st);
     }
     const int m = bo.refs;
+    // the traversal kernels address nodes and triangles by 32-bit byte offsets (common.hpp at_bytes,
+    // the packet kernel's scalar loads): every array below 4 GiB -- up to ~53 M references
+    PGRT_REQUIRE((unsigned long long)m * sizeof(Bvh8Node) < (1ull << 32), PGRT_ERR_INVALID_ARGUMENT,
+                 "scene of " + std::to_string(m) + " triangle references: the BVH arrays would exceed 4 GiB");
     // the 8-wide layout is always built: the multi-lane kernel traces small (deep-level) queues
     // over it; PGRT_BVH_WIDTH=8 also sends the big queues to the one-lane 8-wide kernel
     int wide_nodes = 0, wide_depth = 0;

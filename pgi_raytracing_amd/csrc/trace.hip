@@ -127,7 +127,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
                 // the stack top (the pop target when neither child is hit) is read before the node
                 // fetch, so its LDS latency hides behind the global loads
                 const int top = SPILL ? 0 : lstack[sp * kTraceBlock + tid];
-                const BvhNode* nd = s.nodes + node;
+                const BvhNode* nd = at_bytes(s.nodes, (unsigned)node << 6);
                 long long tq0 = 0;
                 if (COUNT) tq0 = clock64();
                 const float4 a = nd->a, b = nd->b, c = nd->c;
@@ -180,14 +180,16 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
                 const int first = leaf_first(leaf), end = first + leaf_count(leaf);
                 // software-pipelined: the next triangle's loads are in flight while this one is
                 // tested, so a leaf costs about one memory latency instead of one per triangle
-                float4 p0 = s.tri[3 * first], p1 = s.tri[3 * first + 1], p2 = s.tri[3 * first + 2];
+                const float4* pt = at_bytes(s.tri, (unsigned)first * 48u);
+                float4 p0 = pt[0], p1 = pt[1], p2 = pt[2];
                 for (int k = first; k < end; ++k) {
                     if (COUNT) ++rtest;
                     const float4 q0 = p0, q1 = p1, q2 = p2;
                     if (k + 1 < end) {
-                        p0 = s.tri[3 * k + 3];
-                        p1 = s.tri[3 * k + 4];
-                        p2 = s.tri[3 * k + 5];
+                        const float4* pn = at_bytes(s.tri, (unsigned)(k + 1) * 48u);
+                        p0 = pn[0];
+                        p1 = pn[1];
+                        p2 = pn[2];
                     }
                     tri_test(q0, q1, q2, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v, best_prim);
                 }
@@ -303,7 +305,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8(SceneView s, const float
                     else gst[sp - kLdsStack8] = make_uint2(gbase, gbits);
                     ++sp;
                 }
-                const Bvh8Node* nd = s.nodes8 + child;
+                const Bvh8Node* nd = at_bytes(s.nodes8, (unsigned)child * (unsigned)sizeof(Bvh8Node));
                 const float4 p = nd->p;
                 const uint4 m = nd->m, qx = nd->qx, qy = nd->qy, qz = nd->qz;
                 if (COUNT) ++rvis;
@@ -714,12 +716,8 @@ void set_trace_events(hipEvent_t start, hipEvent_t stop) {
 #define PGRT_TLAUNCH(kernel, grid, block, lds, stream, ...) \
     hipExtLaunchKernelGGL(kernel, grid, block, lds, stream, t_ev_start, t_ev_stop, 0, __VA_ARGS__)
 
-// the packet kernel addresses nodes and triangles by 32-bit byte offsets (node << 6, reference * 48):
-// scenes up to 2^24 triangles (with split budgets up to 4x, references stay below 2^32 / 48 B and
-// nodes below 2^26)
-constexpr int kPktMaxTris = 1 << 24;
 bool trace_packets_available(const SceneView& s) {
-    return !s.wide && s.root >= 0 && s.depth + 2 <= kPktStack && s.ntri <= kPktMaxTris;
+    return !s.wide && s.root >= 0 && s.depth + 2 <= kPktStack;
 }
 
 // 4 lanes per ray (two child slots each) above this many rays, 8 at or below it (r1 A/B)

@@ -206,7 +206,7 @@ __device__ __forceinline__ void trace8_group(const SceneView& s, float4 o4, floa
                 stk[sp * stride] = make_uint2(gbase, gbits);  // same value from all lanes of the group
                 ++sp;
             }
-            const Bvh8Node* nd = s.nodes8 + child;
+            const Bvh8Node* nd = at_bytes(s.nodes8, (unsigned)child * (unsigned)sizeof(Bvh8Node));
             const float4 p = nd->p;
             const uint4 m = nd->m, qx = nd->qx, qy = nd->qy, qz = nd->qz;
             if (COUNT) ++rvis;
@@ -241,7 +241,8 @@ __device__ __forceinline__ void trace8_group(const SceneView& s, float4 o4, floa
             for (int q = 0; q < k; ++q) mine &= mine - 1u;  // this lane's set bit
             if (mine != 0u) {
                 const int tr = (int)tbase + __ffs((int)mine) - 1;
-                const float4 q0 = s.tri8[3 * tr], q1 = s.tri8[3 * tr + 1], q2 = s.tri8[3 * tr + 2];
+                const float4* q = at_bytes(s.tri8, (unsigned)tr * 48u);
+                const float4 q0 = q[0], q1 = q[1], q2 = q[2];
                 tri_test(q0, q1, q2, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v, best_prim);
             }
             if (COUNT) rtest += (unsigned)min(__popc(tbits), G);
