@@ -103,6 +103,9 @@ void set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* d) {
         texs[i] = DevTexture{t.width, t.height, t.pitch, t.bpp, pool, (long long)t.pitch * t.height};
         pool += ((long long)t.pitch * t.height + 255) / 256 * 256;
     }
+    // texel windows are addressed by 32-bit pool offsets (shade_ops.hpp tex_fetch)
+    PGRT_REQUIRE(pool + 16 < (1ll << 32), PGRT_ERR_INVALID_ARGUMENT,
+                 "textures of " + std::to_string(pool) + " bytes: the texel pool would exceed 4 GiB");
     if (d->num_lights > 0)
         for (int k = 0; k < 3; ++k) ctx->light0[k] = d->lights[0].position[k];
     std::vector<DevLight> lights(std::max(1, d->num_lights));

@@ -97,12 +97,13 @@ __device__ __forceinline__ TexTap tex_fetch(const DevTexture& t, const unsigned 
     if (q.x2 == q.x1 + 1 && t.bpp <= 4 && o1 >= 0 && o2 >= 0 && o1 + t.bpp + 2 < t.size && o2 + t.bpp + 2 < t.size) {
         // the usual case: both taps of a row are neighbours inside the texture -> one aligned
         // 12-byte window per row (the texel pool is padded for it) instead of 6 byte loads
-        const unsigned char* p1 = pool + t.offset + o1;
-        const unsigned char* p2 = pool + t.offset + o2;
-        q.k1 = (unsigned)((uintptr_t)p1 & 3u);
-        q.k2 = (unsigned)((uintptr_t)p2 & 3u);
-        const unsigned* a = reinterpret_cast<const unsigned*>((uintptr_t)p1 & ~(uintptr_t)3);
-        const unsigned* b = reinterpret_cast<const unsigned*>((uintptr_t)p2 & ~(uintptr_t)3);
+        // 32-bit pool offsets (the pool stays below 4 GiB, set_scene checks; its base is 256-B
+        // aligned, so an offset's low bits are the address's): a scalar base + one VGPR per load
+        const unsigned f1 = (unsigned)t.offset + (unsigned)o1, f2 = (unsigned)t.offset + (unsigned)o2;
+        q.k1 = f1 & 3u;
+        q.k2 = f2 & 3u;
+        const unsigned* a = at_bytes(reinterpret_cast<const unsigned*>(pool), f1 & ~3u);
+        const unsigned* b = at_bytes(reinterpret_cast<const unsigned*>(pool), f2 & ~3u);
         q.w1[0] = a[0];
         q.w1[1] = a[1];
         q.w1[2] = a[2];

@@ -65,7 +65,7 @@ __device__ __forceinline__ HitAttr load_attr(const SceneView& s, float4 h) {
     const int prim = __float_as_int(h.w);
     float4 q0 = make_float4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0;
     if (prim >= 0) {
-        const float4* p = reinterpret_cast<const float4*>(s.attr + 16 * (size_t)prim);
+        const float4* p = at_bytes(reinterpret_cast<const float4*>(s.attr), (unsigned)prim << 6);
         q0 = p[0];
         q1 = p[1];
         q2 = p[2];
