@@ -227,8 +227,11 @@ __device__ __forceinline__ TexTap env_fetch(const SceneView& s, V3 d) {
         return q;
     }
     const V3 vec = normalize(v3(d.x, d.z, d.y));
-    const float u = (float)(0.5 + (double)atan2f_env(vec.x, vec.z) / (2 * 3.14159265358979323846));
-    const float v = (float)(0.5 - (double)asinf_env(vec.y) / 3.14159265358979323846);
+    // SphericalMap.cpp's divisions by 2 pi and pi as products with the double reciprocals: the
+    // float results are identical for every float angle in [-pi, pi] / [-pi/2, pi/2] (exhaustive
+    // check, tools/env_div_check.py; a double division is a ~10-instruction sequence)
+    const float u = (float)(0.5 + (double)atan2f_env(vec.x, vec.z) * (1.0 / (2 * 3.14159265358979323846)));
+    const float v = (float)(0.5 - (double)asinf_env(vec.y) * (1.0 / 3.14159265358979323846));
     return tex_fetch(s.tex[s.env], s.texels, u, v);
 }
 __device__ __forceinline__ float4 env_finish(const SceneView& s, const float* lut, const TexTap& q) {
