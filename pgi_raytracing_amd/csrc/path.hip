@@ -207,7 +207,7 @@ __global__ __launch_bounds__(kPathBlock) void k_path_resolve(SceneView s, int le
             const float4 c = j == k ? c0 : sq.contrib[j];
             if (j > k && __float_as_int(c.w) != -1) break;
             const int prim = __float_as_int(sq.hit[j].w);
-            if (prim < 0 || s.prim_glass[prim] != 0) {  // no occluder, or a dielectric one
+            if (prim < 0 || *at_bytes(s.prim_glass, (unsigned)prim) != 0) {  // no occluder, or a dielectric one
                 acc.x = acc.x + c.x;
                 acc.y = acc.y + c.y;
                 acc.z = acc.z + c.z;

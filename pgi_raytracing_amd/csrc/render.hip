@@ -212,7 +212,7 @@ __device__ __forceinline__ float4 opaque_color(const SceneView& s, const ShadowQ
             lit = ld_stream_nt(sq.lit + k) != 0;  // decided by the shadow trace (compact queue)
         } else {
             const int prim = __float_as_int(ld_stream(sq.hit + k).w);
-            lit = prim < 0 || s.prim_glass[prim] != 0;  // no occluder, or a dielectric one
+            lit = prim < 0 || *at_bytes(s.prim_glass, (unsigned)prim) != 0;  // no occluder, or a dielectric one
         }
         if (lit) {
             blue += c.x;

@@ -142,7 +142,7 @@ __global__ __launch_bounds__(kSubtreeBlock, PGRT_SUBTREE_WAVES) void k_subtree(S
                         atomicAdd(&bst.shadow_vis, (unsigned long long)svis);
                         atomicAdd(&bst.shadow_test, (unsigned long long)stest);
                     }
-                    if (sprim < 0 || s.prim_glass[sprim] != 0) {  // raytracer.cpp:163-173
+                    if (sprim < 0 || *at_bytes(s.prim_glass, (unsigned)sprim) != 0) {  // raytracer.cpp:163-173
                         const float4 c = phong_term(m, Lt, r);
                         blue += c.x;
                         green += c.y;

@@ -202,7 +202,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
             if (COUNT) rcyc_leaf += (unsigned long long)(clock64() - tl0);
         }
         if (lit)  // is_illuminated (raytracer.cpp:163-173): no hit, or the occluder is dielectric
-            st_stream_nt(lit + i, (unsigned char)((best_prim < 0 || s.prim_glass[best_prim] != 0) ? 1 : 0));
+            st_stream_nt(lit + i, (unsigned char)((best_prim < 0 || *at_bytes(s.prim_glass, (unsigned)best_prim) != 0) ? 1 : 0));
         else
             st_stream(hits + i, make_float4(best_t, best_u, best_v, __int_as_float(best_prim)));
         if (COUNT) {

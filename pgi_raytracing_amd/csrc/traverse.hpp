@@ -237,8 +237,10 @@ __device__ __forceinline__ void trace8_group(const SceneView& s, float4 o4, floa
         if (tbits == 0u) break;
         // ---- triangle phase: G triangles per round, then the group's closest hit ----
         while (tbits != 0u) {
+            // this lane's set bit: the lowest k cleared, branch-free (k is the lane in the group)
             unsigned mine = tbits;
-            for (int q = 0; q < k; ++q) mine &= mine - 1u;  // this lane's set bit
+#pragma unroll
+            for (int q = 0; q < G - 1; ++q) mine = q < k ? mine & (mine - 1u) : mine;
             if (mine != 0u) {
                 const int tr = (int)tbase + __ffs((int)mine) - 1;
                 const float4* q = at_bytes(s.tri8, (unsigned)tr * 48u);
