@@ -68,10 +68,13 @@ static_assert(kShadeBlock % kBlock == 0, "k_shade blocks are whole multiples of 
 #define PGRT_SHADE_L0F_WAVES 6
 #endif
 constexpr int kShadeL0fWaves = PGRT_SHADE_L0F_WAVES;
+#ifndef PGRT_SHADE_WAVES
+#define PGRT_SHADE_WAVES 6
+#endif
 
 // L0F: level 0 of a 1-spp batch (L0Final) -- final-colour pixels written here
 template <bool LDS_TABLES, bool L0F>
-__global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : 6) void k_shade(SceneView s, FrameParams fp, int level, Queue q, Queue next,
+__global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : PGRT_SHADE_WAVES) void k_shade(SceneView s, FrameParams fp, int level, Queue q, Queue next,
                                                        LevelNodes nodes, ShadowQueue sq, FrameCounters* fc,
                                                        PinholeOrigin l0, L0Final l0f) {
     PGRT_STAMP_BEGIN(s.stamps);
