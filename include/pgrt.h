@@ -260,6 +260,10 @@ int pgrt_set_config(pgrt_ctx* ctx, const pgrt_config* cfg);
 
 /* ---- scene / camera (replaces Raytracer::LoadScene's Embree upload, raytracer.cpp:71-127,
  *      and the PinHoleCamera ctor, PinHoleCamera.cpp:5-29) ---- */
+/* Limits: the traversal and shading kernels address BVH nodes, triangle records and texels by
+ * 32-bit byte offsets, so every BVH / triangle array stays below 4 GiB (~53 M triangle references,
+ * split duplicates included) and the texel pool too; larger scenes return
+ * PGRT_ERR_INVALID_ARGUMENT with a message. */
 int pgrt_set_scene(pgrt_ctx* ctx, const pgrt_scene_desc* scene);
 int pgrt_bvh_get_info(const pgrt_ctx* ctx, pgrt_bvh_info* info);
 int pgrt_set_camera(pgrt_ctx* ctx, const pgrt_camera* cam);
