@@ -617,6 +617,9 @@ __device__ __forceinline__ void pkt_trace(const SceneView& s, const float4* __re
                 if (COUNT) ++rtest;
                 const float4 ng = cload4((cfloat_ptr)((const __attribute__((address_space(4))) char*)s.tri_ng +
                                                       (unsigned long long)((unsigned)k << 4)));  // precomputed Ng
+                // whole records, in one wait: the unused words keep the loads at full width (3 + 1
+                // scalar loads instead of 7 narrowed ones)
+                asm volatile("" ::"s"(q0.w), "s"(q1.w), "s"(q2.w), "s"(ng.w));
                 if (live)
                     tri_test_ng(q0, q1, q2, ng, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v,
                                 best_prim);
