@@ -100,6 +100,9 @@ def parse():
                          "(no jitter, one framebuffer shared by every call) -- A/B only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--hw-queues", type=int, default=None,
+                    help="A/B only: GPU_MAX_HW_QUEUES for this process (default: 16, as the C++ drop-in sets it; "
+                         "HIP reads it at its first call, after this)")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the profiled roofline frames (the run profiles/ rocprofv3 summaries are taken of)")
     ap.add_argument("--in-flight", type=int, default=None,
@@ -277,6 +280,8 @@ class _stdout_to_stderr:
 
 def main():
     args = parse()
+    if args.hw_queues is not None:  # before the first HIP call (Context below)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -31,7 +31,8 @@
 extern "C" {
 #endif
 
-#define PGRT_ABI_VERSION 2 /* 2 (round 5): pgrt_config carries its size (checked) and host_export */
+#define PGRT_ABI_VERSION 3 /* 2 (round 5): pgrt_config carries its size (checked) and host_export;
+                              3 (round 6): pgrt_config.peer_wait_ms */
 
 #define PGRT_OK 0
 #define PGRT_ERR_INVALID_ARGUMENT (-1)
@@ -229,6 +230,10 @@ typedef struct pgrt_config {
                              destinations always take the copy); PGRT_HOST_EXPORT_SPLIT = after every
                              frame, part of the bytes by a blit kernel on XCD 0 and the rest by a
                              DMA copy at the same time */
+    int peer_wait_ms;   /* distributed frames (rank 0): how long to wait for the peers' tiles of one
+                             gather before giving up -- the communicator is then aborted
+                             (ncclCommAbort), the call and every later distributed call return
+                             PGRT_ERR_RCCL, and pgrt_destroy still returns; 0 = default 120000 */
 } pgrt_config;
 
 /* ---- context ---- */

@@ -10,6 +10,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -41,6 +42,8 @@ struct Vector3 {  // vector3.h (only what the host side needs)
 struct Color4f {  // structs.h:11-14
     float r, g, b, a;
 };
+
+constexpr int kHwQueues = 16;  // GPU_MAX_HW_QUEUES the library is benched with (prefer_hw_queues)
 
 inline float deg2rad(const float x) { return x * float(3.14159265358979323846) / 180.0f; }  // mymath.h:27-30
 
@@ -98,12 +101,23 @@ public:
     Vector3 view_from_, view_at_, up_{0.0f, 0.0f, 1.0f};  // PinHoleCamera.h:36
 };
 
+// Hardware queues for libpgrt's streams.  HIP reads GPU_MAX_HW_QUEUES once, when its runtime
+// initialises (the first HIP call of the process), and defaults to 4; libpgrt keeps every frame in
+// flight on streams of its own (pgrt_set_frames_in_flight, up to 16 calls), so with 4 queues the
+// calls in flight share hardware queues.  bench.py and the drop-in below run with 16 (pgrt.h,
+// INTEGRATION.md).  Sets the variable only if the caller has not (an explicit value wins, <= 32),
+// and only takes effect if no HIP call ran in this process before -- in-process, never a re-exec.
+inline void prefer_hw_queues(int n = kHwQueues) {
+    if (!std::getenv("GPU_MAX_HW_QUEUES")) setenv("GPU_MAX_HW_QUEUES", std::to_string(n).c_str(), 0);
+}
+
 // Raytracer(width, height, fov_y, view_from, view_at) (raytracer.h:18-20)
 class Raytracer {
 public:
     Raytracer(const int width, const int height, const float fov_y, const Vector3 view_from,
               const Vector3 view_at, const int hip_device = 0)
         : camera_(width, height, fov_y, view_from, view_at) {
+        prefer_hw_queues();  // before pgrt_create: the process's first HIP call
         check(nullptr, pgrt_create(hip_device, &ctx_), "pgrt_create");
         init();
     }
@@ -112,6 +126,7 @@ public:
     Raytracer(const int width, const int height, const float fov_y, const Vector3 view_from,
               const Vector3 view_at, const std::vector<int>& hip_devices)
         : camera_(width, height, fov_y, view_from, view_at) {
+        prefer_hw_queues();
         check(nullptr, pgrt_create_devices(hip_devices.data(), (int)hip_devices.size(), &ctx_),
               "pgrt_create_devices");
         init();

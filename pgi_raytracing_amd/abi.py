@@ -31,6 +31,7 @@ ERRORS = {
     -7: "PGRT_ERR_IO",
     -8: "PGRT_ERR_NO_DEVICE",
 }
+globals().update({name: code for code, name in ERRORS.items()})  # PGRT_ERR_* as module constants
 
 
 class Material(C.Structure):
@@ -132,6 +133,7 @@ class Config(C.Structure):
         ("call_order", C.c_int),
         ("tile_order", C.c_int),
         ("host_export", C.c_int),
+        ("peer_wait_ms", C.c_int),
     ]
 
 

@@ -2,6 +2,8 @@
 // camera, synchronous / asynchronous / batched renders, host-output frames, batch ray queries
 // (rtcIntersect1 / rtcOccluded1 analogues) and the progressive frame sink.  The frame state and
 // the other translation units are listed in context.hpp.
+#include <thread>
+
 #include "context.hpp"
 
 using namespace pgrt;
@@ -10,7 +12,7 @@ using namespace pgrt;
 
 extern "C" {
 
-const char* pgrt_version(void) { return "pgrt 0.2.0 (gfx950, abi 2)"; }
+const char* pgrt_version(void) { return "pgrt 0.3.0 (gfx950, abi 3)"; }
 
 int pgrt_device_count(int* count) {
     if (!count) return PGRT_ERR_INVALID_ARGUMENT;
@@ -93,6 +95,16 @@ void pgrt_destroy(pgrt_ctx* ctx) {
     if (!ctx) return;
     if (ctx->group) (void)guarded(ctx, [&] { drain_frames(ctx); });
     (void)hipSetDevice(ctx->device);
+    if (!ctx->comm_aborted.empty() && ctx->stream) {
+        // the communicator was aborted with a receive pending on this stream: the abort ends it,
+        // but never wait for that without a bound -- if the stream has not drained after 10 s the
+        // context's memory is left behind rather than the caller hung in the destructor
+        const auto t0 = std::chrono::steady_clock::now();
+        while (hipStreamQuery(ctx->stream) == hipErrorNotReady) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) return;
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        }
+    }
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     delete ctx;
 }
@@ -135,6 +147,7 @@ int pgrt_set_config(pgrt_ctx* ctx, const pgrt_config* cfg) {
         PGRT_REQUIRE(cfg->rank0_share_a >= 0 && cfg->rank0_share_a <= 64 && cfg->rank0_share_b >= 0 &&
                          cfg->rank0_share_b <= 64,
                      PGRT_ERR_INVALID_ARGUMENT, "rank0_share_a / rank0_share_b must be in [0, 64]");
+        PGRT_REQUIRE(cfg->peer_wait_ms >= 0, PGRT_ERR_INVALID_ARGUMENT, "peer_wait_ms must be >= 0 (0 = default)");
         drain_frames(ctx);  // pending frames were enqueued with the old choices
         ctx->cfg = *cfg;
         for (pgrt_ctx* m : ctx->members) m->cfg = *cfg;  // a multi-device context: every rank
@@ -521,6 +534,7 @@ int pgrt_render_wait(pgrt_ctx* ctx, unsigned long long ticket, pgrt_stats* st) {
         FrameSet* fs = nullptr;
         for (auto& s : ctx->sets)
             if ((s->pending || s->has_result) && s->ticket == ticket) fs = s.get();
+        if (!fs) check_comm(ctx);  // a distributed frame dropped when its communicator was aborted
         PGRT_REQUIRE(fs, PGRT_ERR_INVALID_ARGUMENT, "unknown ticket (or its frame set was reused)");
         finish_through(ctx, ticket);
         PGRT_HIP(hipEventSynchronize(fs->ev_ready));

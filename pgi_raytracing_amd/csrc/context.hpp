@@ -344,6 +344,10 @@ struct pgrt_ctx {
     ncclComm_t comm = nullptr;
     int world = 1, rank = 0;
     unsigned gather_count = 0;  // distributed frames submitted (the gather tail's sequence number)
+    // non-empty once rank 0's bounded wait for the peers' tiles ran out: the communicator was
+    // aborted (ncclCommAbort ends the pending ncclRecv, so the context stream drains), the frames
+    // in flight were dropped, and every later distributed call fails at once with this reason
+    std::string comm_aborted;
     // PGRT_EMULATE_RANK=r/N (measurement tool only, no communicator): distributed frames render
     // rank r's share of an N-GPU frame on this device; the gather becomes a device copy of this
     // rank's tiles into a full-size gather buffer (+ the unpack on rank 0), so one GPU measures a
@@ -440,6 +444,7 @@ void frame_rect(const pgrt_ctx* ctx, const pgrt_render_params* p, int& x, int& y
 
 // ---- distributed.cpp
 void collect_frame(pgrt_ctx* ctx, FrameSet* fs);
+void check_comm(const pgrt_ctx* ctx);
 void gather_frame(pgrt_ctx* ctx, FrameSet* fs);
 void gather_times(FrameSet* fs, pgrt_stats* st);
 TileDeal ctx_deal(const pgrt_ctx* ctx, int world);

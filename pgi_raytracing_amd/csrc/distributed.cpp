@@ -33,10 +33,47 @@ bool rccl_gather(const pgrt_ctx* ctx, const FrameSet* fs) {
 // waiting forever.  Non-zero ranks never wait for another rank; rank 0 waits for the frame's own
 // gather only, and at most kPeerWaitSeconds (a rank that died without sending).
 constexpr int kMaxRetries = 8;
-// Rank 0's wait for the peers' tiles of one gather is bounded: a peer that died or never submitted
-// the frame leaves rank 0's ncclRecv pending forever, and the caller gets PGRT_ERR_RCCL instead of a
-// hang (the communicator is unusable after that; the process should tear it down)
+// Rank 0's wait for the peers' tiles of one gather is bounded (pgrt_config.peer_wait_ms, default
+// 120 s): a peer that died or never submitted the frame would leave rank 0's ncclRecv pending
+// forever.  On timeout the communicator is aborted (abort_comm) and the caller gets PGRT_ERR_RCCL
+// -- from this call, from every later distributed call, and pgrt_destroy still returns.
 constexpr double kPeerWaitSeconds = 120.0;
+double peer_wait_seconds(const pgrt_ctx* ctx) {
+    return ctx->cfg.peer_wait_ms > 0 ? ctx->cfg.peer_wait_ms * 1e-3 : kPeerWaitSeconds;
+}
+
+// The peers' tiles did not arrive in time: ncclCommAbort (RCCL's kernels poll the communicator's
+// abort flag, so the pending ncclRecv on the context stream ends and that stream drains), drop
+// every frame still in flight (their gathers used the same communicator) and fail.  Later
+// distributed calls fail at once (check_comm); pgrt_destroy does not wait on a stream that never
+// drains (context.cpp).
+[[noreturn]] void abort_comm(pgrt_ctx* ctx, const std::string& why) {
+    if (ctx->comm) {
+        (void)ncclCommAbort(ctx->comm);
+        ctx->comm = nullptr;
+    }
+    ctx->comm_aborted = why;
+    for (auto& s : ctx->sets)
+        if (s->distributed) s->pending = false;
+    throw Error(PGRT_ERR_RCCL, why);
+}
+
+void check_comm(const pgrt_ctx* ctx) {
+    PGRT_REQUIRE(ctx->comm_aborted.empty(), PGRT_ERR_RCCL,
+                 "the communicator was aborted (" + ctx->comm_aborted +
+                     "); distributed frames need a new context or pgrt_comm_init");
+}
+
+// diagnostics only (tests/test_gpu_parity.py): PGRT_DEBUG_PEER_STALL=1 makes rank 0 of an
+// emulated world (PGRT_EMULATE_RANK=0/N) behave as if its peers never sent: the bounded wait runs
+// out and the abort path above is taken (one GPU cannot host a world-2 RCCL communicator)
+bool debug_peer_stall() {
+    static const bool on = [] {
+        const char* e = getenv("PGRT_DEBUG_PEER_STALL");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
 
 // hipEventSynchronize with a time limit: spin on hipEventQuery for the first 2 ms (a frame's gather
 // usually lands within it), then poll every 50 us; false on timeout
@@ -53,9 +90,27 @@ bool wait_event_bounded(hipEvent_t e, double seconds) {
     }
 }
 
+// rank 0: the peers' tails of fs's gather have landed, or the communicator is aborted
+void rank0_await_peers(pgrt_ctx* ctx, FrameSet* fs) {
+    const double limit = peer_wait_seconds(ctx);
+    bool ok;
+    if (ctx->emulated) {  // the diagnostics stall: nothing was sent, wait out the limit
+        std::this_thread::sleep_for(std::chrono::duration<double>(limit));
+        ok = false;
+    } else {
+        ok = wait_event_bounded(fs->ev_flags, limit);
+    }
+    if (!ok)
+        abort_comm(ctx, "rank 0 received no tiles of distributed frame " + std::to_string(fs->gather_seq) +
+                            " within " + std::to_string(limit) +
+                            " s: a rank failed or did not submit the frame (communicator aborted)");
+}
+
 void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
     int retries = 0;
     const bool rccl = rccl_gather(ctx, fs);
+    if (fs->distributed && ctx->rank == 0 && ctx->emulated && fs->deal.world > 1 && debug_peer_stall())
+        rank0_await_peers(ctx, fs);  // diagnostics: always times out
     for (;;) {
         const bool mine = read_frame_counters(ctx, fs);
         if (!rccl || ctx->rank != 0) {
@@ -70,10 +125,7 @@ void collect_frame(pgrt_ctx* ctx, FrameSet* fs) {
             if (fs->distributed) gather_frame(ctx, fs);  // rank != 0: the tiles again, to rank 0
             continue;
         }
-        PGRT_REQUIRE(wait_event_bounded(fs->ev_flags, kPeerWaitSeconds), PGRT_ERR_RCCL,
-                     "rank 0 received no tiles of distributed frame " + std::to_string(fs->gather_seq) + " within " +
-                         std::to_string((int)kPeerWaitSeconds) +
-                         " s: a rank failed or did not submit the frame (the communicator is unusable now)");
+        rank0_await_peers(ctx, fs);
         std::vector<int> peers;
         {
             const int world = fs->deal.world;
@@ -464,6 +516,7 @@ int pgrt_comm_init(pgrt_ctx* ctx, int world, int rank, const char id[128]) {
         std::memcpy(u.internal, id, 128);
         ncclResult_t r = ncclCommInitRank(&ctx->comm, world, u, rank);
         if (r != ncclSuccess) throw Error(PGRT_ERR_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+        ctx->comm_aborted.clear();
     });
 }
 

@@ -845,6 +845,7 @@ void start_frame(pgrt_ctx* ctx, FrameSet* fs, const pgrt_render_params* p, std::
                  int out_mode, int ox, int oy, int pitch, bool distributed, float* fb, int nframes,
                  long long frame_stride, TileDeal deal, bool defer_gather) {
     check_frame(ctx, p);
+    if (distributed) check_comm(ctx);
     PGRT_REQUIRE(nframes >= 1 && nframes <= kMaxFramesPerCall, PGRT_ERR_INVALID_ARGUMENT,
                  "frames per call must be in [1, 64]");
     PGRT_REQUIRE(!fs->host_dst || (!distributed && out == fs->host_src && out_mode == 0), PGRT_ERR_INVALID_ARGUMENT,

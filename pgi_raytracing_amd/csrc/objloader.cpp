@@ -300,13 +300,16 @@ int pgrt_obj_load(const char* obj_path, int flip_yz, pgrt_obj** out) {
             parse_indices(tok, buf);
             // atoi(b) - 1 in the reference (objloader.cpp:443-452), range-checked here in 64 bits:
             // an index past INT_MAX (atoi's overflow, then INT_MIN - 1) is undefined there
-            // (make asan: UBSan caught it); strtoll saturates instead
-            const long long iv = std::strtoll(buf[0].c_str(), nullptr, 10) - 1;
-            const long long it = std::strtoll(buf[1].c_str(), nullptr, 10) - 1;
-            const long long in = std::strtoll(buf[2].c_str(), nullptr, 10) - 1;
-            if (iv < 0 || iv >= nv || it < 0 || it >= nt || in < 0 || in >= nn)
-                throw std::runtime_error("face index out of range in '" + tok + "'");
-            return FaceVertex{(int)iv, (int)it, (int)in};
+            // (make asan: UBSan caught it).  The raw 1-based value is checked against [1, n] BEFORE
+            // the subtraction, so no value strtoll can return (LLONG_MIN / LLONG_MAX when it
+            // saturates, 0 for an empty field) reaches an overflowing expression
+            auto index = [&](const std::string& b, long long n) -> int {
+                const long long raw = std::strtoll(b.c_str(), nullptr, 10);
+                if (raw < 1 || raw > n) throw std::runtime_error("face index out of range in '" + tok + "'");
+                return (int)(raw - 1);
+            };
+            const int iv = index(buf[0], nv), it = index(buf[1], nt), in = index(buf[2], nn);
+            return FaceVertex{iv, it, in};
         };
         for (const auto& line : lines) {  // pass 3: groups, materials, faces
             const char c = line[0];

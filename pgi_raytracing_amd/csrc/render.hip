@@ -78,6 +78,7 @@ __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : PGRT_SHADE_WAVE
                                                        LevelNodes nodes, ShadowQueue sq, FrameCounters* fc,
                                                        PinholeOrigin l0, L0Final l0f) {
     PGRT_STAMP_BEGIN(s.stamps);
+    if (!L0F && level > 0) chain_priority();
     __shared__ float lut255[256];
     __shared__ DevMaterial smat[LDS_TABLES ? kLdsMats : 1];
     __shared__ DevTexture stex[LDS_TABLES ? kLdsTex : 1];

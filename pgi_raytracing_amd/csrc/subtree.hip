@@ -46,6 +46,14 @@ struct SubFrameRef {
     int* info;     // nchild | phase << 4 (phase 1: the refraction child is being evaluated)
 };
 
+#if PGRT_STEP_PROFILE
+// diagnostics build only: one record per evaluated ray tree (tools/step_profile.py)
+constexpr int kStepRecs = 1 << 18;
+constexpr int kStepWords = 12;
+__device__ unsigned long long g_step_rec[kStepRecs][kStepWords];
+__device__ unsigned g_step_count;
+#endif
+
 template <int G, bool LDS_TABLES, bool COUNT>
 #ifndef PGRT_SUBTREE_WAVES
 #define PGRT_SUBTREE_WAVES 1
@@ -53,6 +61,7 @@ template <int G, bool LDS_TABLES, bool COUNT>
 __global__ __launch_bounds__(kSubtreeBlock, PGRT_SUBTREE_WAVES) void k_subtree(SceneView s, FrameParams fp, int level, Queue q,
                                                            LevelNodes nodes, FrameCounters* fc, int frames) {
     PGRT_STAMP_BEGIN(s.stamps);
+    chain_priority();
     constexpr int kGroups = kSubtreeBlock / G;
     __shared__ uint2 gstk[kGroupStack][kGroups];
     __shared__ float lut255[256];
@@ -87,16 +96,34 @@ __global__ __launch_bounds__(kSubtreeBlock, PGRT_SUBTREE_WAVES) void k_subtree(S
         float rtime = ld_stream_nt(q.time + i);
         int sp = 0;  // pending dielectric frames; the ray being evaluated is of level `level + sp`
         float4 val = make_float4(0, 0, 0, 1);
+        StepProf prof{};
+        StepProf* pp = nullptr;
+        (void)prof;
+#if PGRT_STEP_PROFILE
+        pp = &prof;
+        const long long tw0 = wall_clock64(), tc0 = clock64();
+        unsigned long long shade_cyc = 0;
+        unsigned ntrace = 0, maxsp = 0;
+#endif
         for (;;) {
             // ---- evaluate one ray: its closest hit, then trace()'s body for it ----
             const int L = level + sp;
             float bt = d4.w, bu = 0.0f, bv = 0.0f;
             int bp = -1;
             unsigned rvis = 0, rtest = 0;
-            trace8_group<G, COUNT>(s, o4, d4, k, gshift, &gstk[0][gib], kGroups, bt, bu, bv, bp, rvis, rtest);
+            trace8_group<G, COUNT>(s, o4, d4, k, gshift, &gstk[0][gib], kGroups, bt, bu, bv, bp, rvis, rtest, pp);
             ShadeOut r;
+#if PGRT_STEP_PROFILE
+            ++ntrace;
+            maxsp = max(maxsp, (unsigned)sp);
+            const long long sc0 = clock64();
+#endif
             shade_eval(s, mats, lut255, L, fp.max_level, true, o4, d4, rtime, make_float4(bt, bu, bv, __int_as_float(bp)),
                        r);
+#if PGRT_STEP_PROFILE
+            asm volatile("" ::"v"(r.kind), "v"(r.color.x));
+            shade_cyc += (unsigned long long)(clock64() - sc0);
+#endif
             if (COUNT && k == 0) {
                 atomicAdd(&bst.trav_vis, (unsigned long long)rvis);
                 atomicAdd(&bst.trav_test, (unsigned long long)rtest);
@@ -137,7 +164,10 @@ __global__ __launch_bounds__(kSubtreeBlock, PGRT_SUBTREE_WAVES) void k_subtree(S
                     int sprim = -1;
                     unsigned svis = 0, stest = 0;
                     trace8_group<G, COUNT>(s, so, sd, k, gshift, &gstk[0][gib], kGroups, st, su, sv, sprim, svis,
-                                           stest);
+                                           stest, pp);
+#if PGRT_STEP_PROFILE
+                    ++ntrace;
+#endif
                     if (COUNT && k == 0) {
                         atomicAdd(&bst.shadow_vis, (unsigned long long)svis);
                         atomicAdd(&bst.shadow_test, (unsigned long long)stest);
@@ -184,6 +214,29 @@ __global__ __launch_bounds__(kSubtreeBlock, PGRT_SUBTREE_WAVES) void k_subtree(S
             st_stream(nodes.color + i, val);
             st_stream(nodes.link + i, make_int4(-1, -1, -1, 0));
         }
+#if PGRT_STEP_PROFILE
+        if (k == 0) {
+            const long long tc1 = clock64(), tw1 = wall_clock64();
+            const unsigned slot = atomicAdd(&g_step_count, 1u);
+            if (slot < (unsigned)kStepRecs) {
+                unsigned long long* rec = g_step_rec[slot];
+                const unsigned wave = (blockIdx.x * kSubtreeBlock + tid) >> 6;
+                rec[0] = (unsigned long long)tw0;
+                rec[1] = (unsigned long long)tw1;
+                rec[2] = (unsigned long long)(tc1 - tc0);
+                rec[3] = prof.node_cyc;
+                rec[4] = prof.node_wait;
+                rec[5] = prof.tri_cyc;
+                rec[6] = prof.tri_wait;
+                rec[7] = shade_cyc;
+                rec[8] = (unsigned long long)prof.nodes | ((unsigned long long)prof.tris << 32);
+                rec[9] = (unsigned long long)ntrace | ((unsigned long long)maxsp << 16) | ((unsigned long long)level << 24) |
+                         ((unsigned long long)G << 32) | ((unsigned long long)(gib % (64 / G)) << 40);
+                rec[10] = (unsigned long long)wave | ((unsigned long long)(unsigned)i << 32);
+                rec[11] = (unsigned long long)(size_t)q.ro;
+            }
+        }
+#endif
     }
     __syncthreads();
     for (int L = tid; L < kMaxLevels; L += kSubtreeBlock) {
@@ -200,6 +253,24 @@ __global__ __launch_bounds__(kSubtreeBlock, PGRT_SUBTREE_WAVES) void k_subtree(S
     }
     PGRT_STAMP_END(s.stamps);
 }
+
+#if PGRT_STEP_PROFILE
+// diagnostics build only: copy out (and optionally reset) the per-tree step records
+extern "C" int pgrt_diag_step_profile(unsigned long long* out, int max_records, int* n, int reset) {
+    unsigned cnt = 0;
+    if (hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(g_step_count), sizeof(cnt)) != hipSuccess) return PGRT_ERR_HIP;
+    const int m = (int)std::min<unsigned>(std::min<unsigned>(cnt, (unsigned)kStepRecs), (unsigned)std::max(0, max_records));
+    if (out && m > 0 &&
+        hipMemcpyFromSymbol(out, HIP_SYMBOL(g_step_rec), sizeof(unsigned long long) * kStepWords * m) != hipSuccess)
+        return PGRT_ERR_HIP;
+    if (n) *n = (int)cnt;
+    if (reset) {
+        cnt = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_step_count), &cnt, sizeof(cnt)) != hipSuccess) return PGRT_ERR_HIP;
+    }
+    return PGRT_OK;
+}
+#endif
 
 bool subtree_available(const SceneView& s) { return s.depth8 + 1 <= kGroupStack; }
 

@@ -168,6 +168,18 @@ __device__ __forceinline__ SlotTest test_slot(unsigned slot, const uint4& m, con
 }
 
 
+// Diagnostics build only (-DPGRT_STEP_PROFILE=1, tools/step_profile.py): the dependent steps of
+// one traced ray on the shader clock (s_memtime cycles) -- each 8-wide node step and each triangle
+// round, and inside them the wait from issuing the step's loads to their first use.  The product
+// build compiles none of it.
+#ifndef PGRT_STEP_PROFILE
+#define PGRT_STEP_PROFILE 0
+#endif
+struct StepProf {
+    unsigned long long node_cyc, node_wait, tri_cyc, tri_wait;
+    unsigned nodes, tris;
+};
+
 // One ray traced by a group of G lanes (k = lane in the group, gshift = the group's first lane in
 // the wave) over the 8-wide BVH; stk[sp * stride] is the group's node-group stack (kGroupStack
 // entries, LDS).  Every lane of the group ends with the closest hit in best_* (in: the bound to
@@ -176,7 +188,8 @@ __device__ __forceinline__ SlotTest test_slot(unsigned slot, const uint4& m, con
 template <int G, bool COUNT>
 __device__ __forceinline__ void trace8_group(const SceneView& s, float4 o4, float4 d4, int k, int gshift, uint2* stk,
                                              int stride, float& best_t, float& best_u, float& best_v, int& best_prim,
-                                             unsigned& rvis, unsigned& rtest) {
+                                             unsigned& rvis, unsigned& rtest, StepProf* prof = nullptr) {
+    (void)prof;
     const float ox = o4.x, oy = o4.y, oz = o4.z, tnear = o4.w;
     const float dx = d4.x, dy = d4.y, dz = d4.z, tfar = d4.w;
     const float sdx = fabsf(dx) < 1e-30f ? copysignf(1e-30f, dx) : dx;
@@ -191,6 +204,8 @@ __device__ __forceinline__ void trace8_group(const SceneView& s, float4 o4, floa
     unsigned tbase = 0, tbits = 0;
     for (;;) {
         while (tbits == 0u) {  // ---- node phase (group-uniform) ----
+            long long pc0 = 0;
+            if constexpr (PGRT_STEP_PROFILE) pc0 = clock64();
             if (gbits <= 0x00ffffffu) {
                 if (sp == 0) break;
                 --sp;
@@ -207,8 +222,14 @@ __device__ __forceinline__ void trace8_group(const SceneView& s, float4 o4, floa
                 ++sp;
             }
             const Bvh8Node* nd = at_bytes(s.nodes8, (unsigned)child * (unsigned)sizeof(Bvh8Node));
+            long long pc1 = 0;
+            if constexpr (PGRT_STEP_PROFILE) pc1 = clock64();
             const float4 p = nd->p;
             const uint4 m = nd->m, qx = nd->qx, qy = nd->qy, qz = nd->qz;
+            if constexpr (PGRT_STEP_PROFILE) {  // the node's loads have landed
+                asm volatile("" ::"v"(p.w), "v"(m.z), "v"(qx.x), "v"(qy.x), "v"(qz.x));
+                prof->node_wait += (unsigned long long)(clock64() - pc1);
+            }
             if (COUNT) ++rvis;
             const unsigned eb = __float_as_uint(p.w);
             const unsigned imask = eb >> 24;
@@ -233,10 +254,17 @@ __device__ __forceinline__ void trace8_group(const SceneView& s, float4 o4, floa
             gbits = (nb << 24) | imask;
             tbase = m.y;
             tbits = (unsigned)tb;
+            if constexpr (PGRT_STEP_PROFILE) {
+                asm volatile("" ::"v"(tbits), "v"(gbits));
+                prof->node_cyc += (unsigned long long)(clock64() - pc0);
+                ++prof->nodes;
+            }
         }
         if (tbits == 0u) break;
         // ---- triangle phase: G triangles per round, then the group's closest hit ----
         while (tbits != 0u) {
+            long long pc0 = 0;
+            if constexpr (PGRT_STEP_PROFILE) pc0 = clock64();
             // this lane's set bit: the lowest k cleared, branch-free (k is the lane in the group)
             unsigned mine = tbits;
 #pragma unroll
@@ -244,12 +272,23 @@ __device__ __forceinline__ void trace8_group(const SceneView& s, float4 o4, floa
             if (mine != 0u) {
                 const int tr = (int)tbase + __ffs((int)mine) - 1;
                 const float4* q = at_bytes(s.tri8, (unsigned)tr * 48u);
+                long long pc1 = 0;
+                if constexpr (PGRT_STEP_PROFILE) pc1 = clock64();
                 const float4 q0 = q[0], q1 = q[1], q2 = q[2];
+                if constexpr (PGRT_STEP_PROFILE) {
+                    asm volatile("" ::"v"(q0.x), "v"(q1.x), "v"(q2.x));
+                    if (k == 0) prof->tri_wait += (unsigned long long)(clock64() - pc1);
+                }
                 tri_test(q0, q1, q2, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v, best_prim);
             }
             if (COUNT) rtest += (unsigned)min(__popc(tbits), G);
             for (int q = 0; q < G; ++q) tbits &= tbits - 1u;
             group_merge_hit<G>(best_t, best_u, best_v, best_prim);
+            if constexpr (PGRT_STEP_PROFILE) {
+                asm volatile("" ::"v"(best_t), "v"(best_prim));
+                prof->tri_cyc += (unsigned long long)(clock64() - pc0);
+                ++prof->tris;
+            }
         }
     }
 }

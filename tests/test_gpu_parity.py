@@ -963,13 +963,13 @@ def _host_frames_equal_device(gpu_ctx, W, H):
 
 
 def test_config_size_is_checked(gpu_ctx):
-    """pgrt_config carries its size (abi 2): pgrt_get_config fills it, pgrt_set_config rejects a
+    """pgrt_config carries its size (abi 2; abi 3 added peer_wait_ms): pgrt_get_config fills it, pgrt_set_config rejects a
     struct of another layout instead of writing its fields into the wrong places."""
     from pgi_raytracing_amd.raytracer import PgrtError
 
     cfg = gpu_ctx.get_config()
     assert cfg.size == C.sizeof(abi.Config)
-    assert b"abi 2" in gpu_ctx.L.pgrt_version()
+    assert b"abi 3" in gpu_ctx.L.pgrt_version()
     bad = abi.Config.from_buffer_copy(cfg)
     bad.size = cfg.size - 4
     with pytest.raises(PgrtError, match="pgrt_config.size"):
@@ -977,6 +977,10 @@ def test_config_size_is_checked(gpu_ctx):
     bad = abi.Config.from_buffer_copy(cfg)
     bad.host_export = 5
     with pytest.raises(PgrtError):
+        gpu_ctx.set_config(bad)
+    bad = abi.Config.from_buffer_copy(cfg)
+    bad.peer_wait_ms = -1
+    with pytest.raises(PgrtError, match="peer_wait_ms"):
         gpu_ctx.set_config(bad)
     gpu_ctx.set_config(cfg)
 

@@ -25,6 +25,10 @@ CORPUS = {
     "zero_index": (V4 + "g a\nf 0/1/1 2/2/1 3/3/1\n", None),
     "huge_index": (V4 + "g a\nf 99999999999999999999/1/1 2/2/1 3/3/1\n", None),
     "int_min_index": (V4 + "g a\nf 2147483648/1/1 2/2/1 3/3/1\n", None),
+    # strtoll saturates to LLONG_MIN here if the sign ever reaches it (the reference's %[0-9]
+    # scan stops at the '-', so the token keeps the previous face's indices)
+    "huge_negative_index": (V4 + "g a\nf -99999999999999999999/1/1 2/2/1 3/3/1\n", None),
+    "huge_negative_first_face": (V4 + "g a\nf 1/1/1 -99999999999999999999/-99999999999999999999/1 3/3/1\n", None),
     "missing_normals": (V4 + "g a\nf 1/1 2/2 3/3\n", None),
     "double_slash": (V4 + "g a\nf 1//1 2//1 3//1\n", None),
     "bare_indices": (V4 + "g a\nf 1 2 3\n", None),
