@@ -102,13 +102,17 @@ public:
 };
 
 // Hardware queues for libpgrt's streams.  HIP reads GPU_MAX_HW_QUEUES once, when its runtime
-// initialises (the first HIP call of the process), and defaults to 4; libpgrt keeps every frame in
-// flight on streams of its own (pgrt_set_frames_in_flight, up to 16 calls), so with 4 queues the
-// calls in flight share hardware queues.  bench.py and the drop-in below run with 16 (pgrt.h,
-// INTEGRATION.md).  Sets the variable only if the caller has not (an explicit value wins, <= 32),
-// and only takes effect if no HIP call ran in this process before -- in-process, never a re-exec.
+// initialises (the first HIP call of the process), and defaults to 4 (the MI355X boxes this was
+// measured on export GPU_MAX_HW_QUEUES=4).  libpgrt keeps every call in flight and both pipeline
+// slots of a synchronous frame on streams of their own, so with 4 queues they share hardware
+// queues: measured (profiles/r6/r6b_hw_queues.txt) the throughput line is the same but one
+// synchronous C2 frame takes 0.66-0.70 ms instead of 0.54.  bench.py and the drop-in run with 16:
+// prefer_hw_queues raises an unset or smaller value to n (a larger one is kept, <= 32) in the
+// process environment -- in-process, never a re-exec -- and only takes effect if no HIP call ran
+// in this process before.
 inline void prefer_hw_queues(int n = kHwQueues) {
-    if (!std::getenv("GPU_MAX_HW_QUEUES")) setenv("GPU_MAX_HW_QUEUES", std::to_string(n).c_str(), 0);
+    const char* v = std::getenv("GPU_MAX_HW_QUEUES");
+    if (!v || std::atoi(v) < n) setenv("GPU_MAX_HW_QUEUES", std::to_string(n).c_str(), 1);
 }
 
 // Raytracer(width, height, fov_y, view_from, view_at) (raytracer.h:18-20)

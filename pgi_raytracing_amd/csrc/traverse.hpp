@@ -205,7 +205,7 @@ __device__ __forceinline__ void trace8_group(const SceneView& s, float4 o4, floa
     for (;;) {
         while (tbits == 0u) {  // ---- node phase (group-uniform) ----
             long long pc0 = 0;
-            if constexpr (PGRT_STEP_PROFILE) pc0 = clock64();
+            if constexpr (PGRT_STEP_PROFILE) pc0 = clock64();  // (prof NULL: callers without a record)
             if (gbits <= 0x00ffffffu) {
                 if (sp == 0) break;
                 --sp;
@@ -228,7 +228,7 @@ __device__ __forceinline__ void trace8_group(const SceneView& s, float4 o4, floa
             const uint4 m = nd->m, qx = nd->qx, qy = nd->qy, qz = nd->qz;
             if constexpr (PGRT_STEP_PROFILE) {  // the node's loads have landed
                 asm volatile("" ::"v"(p.w), "v"(m.z), "v"(qx.x), "v"(qy.x), "v"(qz.x));
-                prof->node_wait += (unsigned long long)(clock64() - pc1);
+                if (prof) prof->node_wait += (unsigned long long)(clock64() - pc1);
             }
             if (COUNT) ++rvis;
             const unsigned eb = __float_as_uint(p.w);
@@ -256,8 +256,10 @@ __device__ __forceinline__ void trace8_group(const SceneView& s, float4 o4, floa
             tbits = (unsigned)tb;
             if constexpr (PGRT_STEP_PROFILE) {
                 asm volatile("" ::"v"(tbits), "v"(gbits));
-                prof->node_cyc += (unsigned long long)(clock64() - pc0);
-                ++prof->nodes;
+                if (prof) {
+                    prof->node_cyc += (unsigned long long)(clock64() - pc0);
+                    ++prof->nodes;
+                }
             }
         }
         if (tbits == 0u) break;
@@ -277,7 +279,7 @@ __device__ __forceinline__ void trace8_group(const SceneView& s, float4 o4, floa
                 const float4 q0 = q[0], q1 = q[1], q2 = q[2];
                 if constexpr (PGRT_STEP_PROFILE) {
                     asm volatile("" ::"v"(q0.x), "v"(q1.x), "v"(q2.x));
-                    if (k == 0) prof->tri_wait += (unsigned long long)(clock64() - pc1);
+                    if (prof && k == 0) prof->tri_wait += (unsigned long long)(clock64() - pc1);
                 }
                 tri_test(q0, q1, q2, ox, oy, oz, dx, dy, dz, tnear, tfar, best_t, best_u, best_v, best_prim);
             }
@@ -286,8 +288,10 @@ __device__ __forceinline__ void trace8_group(const SceneView& s, float4 o4, floa
             group_merge_hit<G>(best_t, best_u, best_v, best_prim);
             if constexpr (PGRT_STEP_PROFILE) {
                 asm volatile("" ::"v"(best_t), "v"(best_prim));
-                prof->tri_cyc += (unsigned long long)(clock64() - pc0);
-                ++prof->tris;
+                if (prof) {
+                    prof->tri_cyc += (unsigned long long)(clock64() - pc0);
+                    ++prof->tris;
+                }
             }
         }
     }
