@@ -72,6 +72,28 @@ constexpr int kShadeL0fWaves = PGRT_SHADE_L0F_WAVES;
 #define PGRT_SHADE_WAVES 6
 #endif
 
+#if PGRT_STEP_PROFILE
+// diagnostics build only (tools/step_profile.py --shade): one record per wave and shading iteration
+// -- the level, the shader-clock cycles of each phase (part A, allocation begin, part B, allocation
+// end, emit) and the wave's rays by kind after part A (miss, dielectric, opaque, other)
+constexpr int kShadeRecs = 1 << 20;
+__device__ unsigned long long g_shade_rec[kShadeRecs][4];
+__device__ unsigned g_shade_count;
+extern "C" int pgrt_diag_shade_profile(unsigned long long* out, int max_records, int* n, int reset) {
+    unsigned cnt = 0;
+    if (hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(g_shade_count), sizeof(cnt)) != hipSuccess) return PGRT_ERR_HIP;
+    const unsigned m = std::min<unsigned>(std::min<unsigned>(cnt, (unsigned)kShadeRecs), (unsigned)std::max(0, max_records));
+    if (out && m > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_shade_rec), sizeof(unsigned long long) * 4 * m) != hipSuccess)
+        return PGRT_ERR_HIP;
+    if (n) *n = (int)cnt;
+    if (reset) {
+        cnt = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_shade_count), &cnt, sizeof(cnt)) != hipSuccess) return PGRT_ERR_HIP;
+    }
+    return PGRT_OK;
+}
+#endif
+
 // L0F: level 0 of a 1-spp batch (L0Final) -- final-colour pixels written here
 template <bool LDS_TABLES, bool L0F>
 __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : PGRT_SHADE_WAVES) void k_shade(SceneView s, FrameParams fp, int level, Queue q, Queue next,
@@ -142,7 +164,16 @@ __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : PGRT_SHADE_WAVE
         // the kind and slot counts first, the long-latency colours while the allocation atomic is
         // in flight (shade_eval_a / _b; r5s / r5t)
         ShadeDefer df;
+#if PGRT_STEP_PROFILE
+        const long long pc0 = clock64();
+#endif
         shade_eval_a(s, mats, level, fp.max_level, active, cur_o, cur_d, cur_t, cur_h, r, df);
+#if PGRT_STEP_PROFILE
+        asm volatile("" ::"v"(r.kind), "v"(r.nchild), "v"(r.nshadow));
+        const long long pc1 = clock64();
+        const unsigned long long kmiss = __ballot(active && r.kind == 3), kdiel = __ballot(active && r.kind == 1),
+                                 kopq = __ballot(active && r.kind == 2), kact = __ballot(active);
+#endif
         if (level == 0 && fp.tile_deep) {  // a wave lies in one tile (4096 * nsb rays per tile)
             const unsigned long long dm = __ballot(active && r.nchild > 0);
             if (dm != 0ull && __lane_id() == 0) fp.tile_deep[(i / fp.nsb) / (kTile * kTile)] = 1;
@@ -156,8 +187,18 @@ __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : PGRT_SHADE_WAVE
             }
         }
         const ShadeAllocPending pa = shade_alloc_begin<kShadeBlock>(alds, it_par, fc, level, sbits, r, &refr_acc);
+#if PGRT_STEP_PROFILE
+        const long long pc2 = clock64();
+#endif
         shade_eval_b(s, mats, lut255, r, df);
+#if PGRT_STEP_PROFILE
+        asm volatile("" ::"v"(r.color.x), "v"(r.att.x), "v"(r.m_d_r));
+        const long long pc3 = clock64();
+#endif
         const ShadeSlots sl = shade_alloc_end<kShadeBlock>(alds, it_par, sq_base, pa);
+#if PGRT_STEP_PROFILE
+        const long long pc4 = clock64();
+#endif
         if constexpr (l0final) {
             // a final colour (environment texel; padding; a hit at max_level) -> the pixel, now;
             // the others are completed by the finish (n is a multiple of 64: whole waves)
@@ -169,6 +210,25 @@ __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : PGRT_SHADE_WAVE
         } else if (active) {
             shade_emit(s, mats, level, i, r, sl, next, nodes, sq, fc);
         }
+#if PGRT_STEP_PROFILE
+        {
+            const long long pc5 = clock64();
+            if (__lane_id() == 0) {
+                const unsigned slot = atomicAdd(&g_shade_count, 1u);
+                if (slot < (unsigned)kShadeRecs) {
+                    unsigned long long* rec = g_shade_rec[slot];
+                    // [0] level | active | miss | dielectric | opaque lanes; [1] part A | alloc begin;
+                    // [2] part B | alloc end; [3] emit | total (cycles, 32 bits each)
+                    rec[0] = (unsigned long long)level | ((unsigned long long)__popcll(kact) << 8) |
+                             ((unsigned long long)__popcll(kmiss) << 16) | ((unsigned long long)__popcll(kdiel) << 24) |
+                             ((unsigned long long)__popcll(kopq) << 32);
+                    rec[1] = (unsigned long long)(unsigned)(pc1 - pc0) | ((unsigned long long)(unsigned)(pc2 - pc1) << 32);
+                    rec[2] = (unsigned long long)(unsigned)(pc3 - pc2) | ((unsigned long long)(unsigned)(pc4 - pc3) << 32);
+                    rec[3] = (unsigned long long)(unsigned)(pc5 - pc4) | ((unsigned long long)(unsigned)(pc5 - pc0) << 32);
+                }
+            }
+        }
+#endif
     }
     shade_refract_flush(fc, level, refr_acc);
     PGRT_STAMP_END(s.stamps);

@@ -254,6 +254,315 @@ __global__ __launch_bounds__(kSubtreeBlock, PGRT_SUBTREE_WAVES) void k_subtree(S
     PGRT_STAMP_END(s.stamps);
 }
 
+// ---- cooperative ray trees ---------------------------------------------------------------------
+// k_subtree evaluates each tree in ONE lane group, so a launch lasts as long as its largest tree: a
+// canopy pixel's tree is 11-13 traces in series (r5zh), ~10x the median tree.  Here the groups of a
+// block share their trees.  A dielectric node's refraction child becomes a task on a block-wide LDS
+// stack that any idle group of the block takes, while the group that met the node goes on with the
+// reflection child; a group whose own tree is done takes tasks first and new roots only when no task
+// waits.  A node's frame sits at its heap position in its tree's slot (children of heap index h at
+// 2h+1 = reflection, 2h+2 = refraction), and the two children join on an LDS counter: the group that
+// delivers a frame's last child mixes and attenuates (raytracer.cpp:318-321) and carries the colour
+// on up.  Every node's arithmetic is the one k_subtree runs (shade_eval, is_illuminated's shadow
+// rays, mix_srgb, attenuation), so the colours are bit-identical; only which group evaluates which
+// ray, and when, changes.  Trees with at most kCoopMaxDepth levels below the first (2^D - 1 frames).
+//
+// Work exchange is wave-uniform: once per iteration a wave that has a task to publish or an idle
+// group takes the block lock (lane 0 spins, so a wave never spins on a lock its own lanes hold),
+// pushes its groups' tasks, hands out tasks / roots to its idle groups, and leaves when nothing is
+// queued, no root is left and no group of the block holds a ray (only a busy group can make work).
+#ifndef PGRT_COOP_WATCHDOG
+#define PGRT_COOP_WATCHDOG 0
+#endif
+constexpr int kCoopMaxDepth = 4;
+constexpr int kCoopFrameBytes = 5 * (int)sizeof(float4) + 3 * (int)sizeof(int);  // att c0 c1 org rdir | cnt nch task
+
+template <int G, bool LDS_TABLES, bool COUNT>
+__global__ __launch_bounds__(kSubtreeBlock, PGRT_SUBTREE_WAVES) void k_subtree_coop(SceneView s, FrameParams fp, int level,
+                                                                                Queue q, LevelNodes nodes,
+                                                                                FrameCounters* fc, int depth) {
+    PGRT_STAMP_BEGIN(s.stamps);
+    constexpr int kGroups = kSubtreeBlock / G;
+    static_assert(kGroups <= 64, "tree slots are the bits of one 64-bit mask");
+    __shared__ uint2 gstk[kGroupStack][kGroups];
+    __shared__ float lut255[256];
+    __shared__ DevMaterial smat[LDS_TABLES ? kLdsMats : 1];
+    __shared__ DevTexture stex[LDS_TABLES ? kLdsTex : 1];
+    __shared__ SubtreeStats bst;
+    __shared__ int root_i[kGroups];  // queue index of the root ray of tree slot t
+    __shared__ int s_top, s_root_next, s_lock, s_busy;
+    __shared__ unsigned long long s_free;  // free tree slots
+    extern __shared__ float4 cstore[];
+    const int NF = (1 << depth) - 1;  // frames per tree: the dielectric nodes of levels level .. level + depth - 1
+    const int nfr = kGroups * NF;
+    float4* f_att = cstore;            // (att.r, att.g, att.b, R)
+    float4* f_c0 = cstore + nfr;       // the reflection child's colour
+    float4* f_c1 = cstore + 2 * nfr;   // the refraction child's colour
+    float4* f_org = cstore + 3 * nfr;  // the children's origin (hit point, tnear 0.01)
+    float4* f_rdir = cstore + 4 * nfr; // the refraction direction, medium n2 in w
+    int* f_cnt = reinterpret_cast<int*>(cstore + 5 * nfr);  // children delivered
+    int* f_nch = f_cnt + nfr;                              // children (1: total internal reflection)
+    int* tasks = f_nch + nfr;                              // stack of (slot << 8 | heap index) refraction tasks
+    const int tid = threadIdx.x;
+    if constexpr (LDS_TABLES) {
+        for (int k = tid; k < s.nmat; k += kSubtreeBlock) smat[k] = s.mats[k];
+        for (int k = tid; k < s.ntex; k += kSubtreeBlock) stex[k] = s.tex[k];
+        s.tex = stex;
+    }
+    for (int k = tid; k < kMaxLevels; k += kSubtreeBlock) {
+        bst.alloc[k] = 0;
+        bst.refract[k] = 0;
+    }
+    if (tid == 0) {
+        bst.trav_vis = bst.trav_test = bst.shadow_vis = bst.shadow_test = bst.hits = bst.textured = 0;
+        s_top = s_root_next = s_lock = s_busy = 0;
+        s_free = kGroups == 64 ? ~0ull : ((1ull << kGroups) - 1ull);
+    }
+    const DevMaterial* mats = LDS_TABLES ? smat : s.mats;
+    fill_byte_lut(lut255);  // ends with __syncthreads
+    const int k = tid & (G - 1);
+    const int gib = tid / G;
+    const int gshift = __lane_id() & ~(G - 1);
+    const bool lead = k == 0;
+    const int n = min(fc_count(*fc, level), q.cap);
+    // the block's roots: the grid-stride sequence k_subtree's groups take (increasing in r)
+    auto root_index = [&](int r) { return blockIdx.x * kGroups + (r % kGroups) + (r / kGroups) * gridDim.x * kGroups; };
+    auto below = [](unsigned long long m) {
+        return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+    };
+    bool have = false;
+    int t = 0, h = 0, L = level, push = -1;
+    float4 o4 = make_float4(0, 0, 0, 0), d4 = o4;
+    float rtime = 0.0f;
+#if PGRT_COOP_WATCHDOG
+    unsigned iters = 0;
+#endif
+    for (;;) {
+#if PGRT_COOP_WATCHDOG
+        if (++iters > (1u << 20)) {  // diagnostics: a wave that never finishes reports its block's state
+            if (__lane_id() == 0)
+                printf("coop watchdog: block %d wave %d level %d n %d top %d busy %d root_next %d next_root_index %d "
+                       "free %llx have %llx push %llx\n",
+                       (int)blockIdx.x, (int)(tid >> 6), level, n, s_top, s_busy, s_root_next, root_index(s_root_next),
+                       s_free, (unsigned long long)__ballot(lead && have), (unsigned long long)__ballot(lead && push >= 0));
+            atomicOr(&fc->overflow, 8);
+            break;
+        }
+#endif
+        // ---- exchange (wave-uniform) ----
+        const unsigned long long pm = __ballot(lead && push >= 0);
+        const unsigned long long wm = __ballot(lead && !have);
+        if ((pm | wm) != 0ull) {
+            if (__lane_id() == 0) {
+#if PGRT_COOP_WATCHDOG
+                unsigned spins = 0;
+                while (atomicCAS(&s_lock, 0, 1) != 0) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins == (1u << 22))
+                        printf("coop watchdog: block %d wave %d spins on the lock (holder state %d)\n", (int)blockIdx.x,
+                               (int)(tid >> 6), s_lock);
+                }
+#else
+                while (atomicCAS(&s_lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(1);
+#endif
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            int top = __builtin_amdgcn_readfirstlane(s_top);
+            if (lead && push >= 0) tasks[top + below(pm)] = push;
+            top += (int)__popcll(pm);
+            const int wr = below(wm), nw = (int)__popcll(wm);
+            const int ntake = min(nw, top);
+            int got = -1, got_root = -1, got_slot = -1;
+            if (lead && !have && wr < ntake) got = tasks[top - 1 - wr];
+            top -= ntake;
+            const int rn = __builtin_amdgcn_readfirstlane(s_root_next);
+            int roots = 0;
+            unsigned long long taken = 0ull;
+            if (nw > ntake) {  // the other idle groups start roots (no task is left waiting)
+                unsigned long long fr = s_free;
+                const int j = wr - ntake;
+                const int want = min(nw - ntake, (int)__popcll(fr));
+                const bool mine = lead && !have && wr >= ntake && j < want && root_index(rn + j) < n;
+                roots = (int)__popcll(__ballot(mine));
+                for (int m = 0; m < roots; ++m) {  // the lowest `roots` free slots, in root order
+                    const unsigned long long bit = fr & (~fr + 1ull);
+                    if (mine && m == j) {
+                        got_root = root_index(rn + j);
+                        got_slot = __ffsll((long long)bit) - 1;
+                    }
+                    taken |= bit;
+                    fr &= fr - 1ull;
+                }
+            }
+            const int busy_before = __builtin_amdgcn_readfirstlane(s_busy);
+            if (__lane_id() == 0) {
+                s_top = top;
+                s_root_next = rn + roots;
+                if (taken) atomicAnd(&s_free, ~taken);
+                if (ntake + roots) atomicAdd(&s_busy, ntake + roots);
+            }
+            if (got_root >= 0) root_i[got_slot] = got_root;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (__lane_id() == 0) atomicExch(&s_lock, 0);
+            // nothing to give and nothing that could make work: this wave is done
+            const bool all_idle = __ballot(have) == 0ull && ntake + roots == 0;
+            if (all_idle && top == 0 && busy_before == 0 && root_index(rn) >= n) break;
+            got = __shfl(got, gshift, 64);
+            got_root = __shfl(got_root, gshift, 64);
+            got_slot = __shfl(got_slot, gshift, 64);
+            if (got >= 0) {  // a refraction child: frame (slot, p) holds its origin, direction and medium
+                t = got >> 8;
+                const int p = got & 255;
+                const int fi = t * NF + p;
+                o4 = f_org[fi];
+                const float4 rd4 = f_rdir[fi];
+                d4 = make_float4(rd4.x, rd4.y, rd4.z, 3.402823466e+38f);
+                rtime = rd4.w;
+                h = 2 * p + 2;
+                L = level + (31 - __clz(h + 1));
+                have = true;
+            } else if (got_root >= 0) {
+                t = got_slot;
+                h = 0;
+                L = level;
+                o4 = ld_stream(q.ro + got_root);
+                d4 = ld_stream(q.rd + got_root);
+                rtime = ld_stream_nt(q.time + got_root);
+                have = true;
+            }
+            push = -1;
+            if (__ballot(have) == 0ull) {  // every group idle, others still busy: wait for work
+                __builtin_amdgcn_s_sleep(4);
+                continue;
+            }
+        }
+        if (!have) continue;
+#if PGRT_COOP_WATCHDOG
+        if (lead && !(d4.x == d4.x && d4.y == d4.y && d4.z == d4.z && o4.x == o4.x && o4.y == o4.y && o4.z == o4.z))
+            printf("coop watchdog: block %d group %d non-finite ray t %d h %d L %d o %f %f %f d %f %f %f %f\n",
+                   (int)blockIdx.x, gib, t, h, L, o4.x, o4.y, o4.z, d4.x, d4.y, d4.z, d4.w);
+        const long long wd_t0 = wall_clock64();
+#endif
+        // ---- one ray: trace and shade (raytracer.cpp:241-393) ----
+        float bt = d4.w, bu = 0.0f, bv = 0.0f;
+        int bp = -1;
+        unsigned rvis = 0, rtest = 0;
+        trace8_group<G, COUNT>(s, o4, d4, k, gshift, &gstk[0][gib], kGroups, bt, bu, bv, bp, rvis, rtest);
+#if PGRT_COOP_WATCHDOG
+        if (lead && wall_clock64() - wd_t0 > 100000)  // 1 ms for one trace
+            printf("coop watchdog: block %d group %d slow trace %lld us t %d h %d L %d o %f %f %f d %f %f %f\n",
+                   (int)blockIdx.x, gib, (long long)(wall_clock64() - wd_t0) / 100, t, h, L, o4.x, o4.y, o4.z, d4.x,
+                   d4.y, d4.z);
+#endif
+        ShadeOut r;
+        shade_eval(s, mats, lut255, L, fp.max_level, true, o4, d4, rtime, make_float4(bt, bu, bv, __int_as_float(bp)), r);
+        if (COUNT && lead) {
+            atomicAdd(&bst.trav_vis, (unsigned long long)rvis);
+            atomicAdd(&bst.trav_test, (unsigned long long)rtest);
+            if (bp >= 0) {
+                atomicAdd(&bst.hits, 1ull);
+                if (r.kind == 2 && mats[r.mid].tex >= 0) atomicAdd(&bst.textured, 1ull);
+            }
+        }
+        if (r.kind == 1) {  // dielectric: the node's frame, the refraction child as a task, on with the reflection
+            if (lead) {
+                atomicAdd(&bst.alloc[L], (unsigned long long)r.nchild);
+                if (r.nchild == 2 && L + 1 < kMaxLevels) atomicAdd(&bst.refract[L + 1], 1);
+            }
+            const int fi = t * NF + h;
+            f_att[fi] = r.att;
+            f_org[fi] = child_org(r);
+            f_rdir[fi] = make_float4(r.refr_dir.x, r.refr_dir.y, r.refr_dir.z, r.n2);
+            f_nch[fi] = r.nchild;
+            f_cnt[fi] = 0;
+            if (r.nchild == 2) push = (t << 8) | h;
+            o4 = child_org(r);
+            d4 = child_dir(r.refl_dir);
+            rtime = r.n1;
+            h = 2 * h + 1;
+            ++L;
+            continue;
+        }
+        float4 val;
+        if (r.kind == 2 && r.nshadow > 0) {  // opaque: is_illuminated per light, the lit Phong terms
+            if (lead) atomicAdd(&bst.alloc[L], (unsigned long long)r.nshadow << 32);
+            const DevMaterial& m = mats[r.mid];
+            float blue = 0, green = 0, red = 0;
+            for (int li = 0; li < s.nlight; ++li) {
+                const DevLight& Lt = s.lights[li];
+                const V3 lp = v3(Lt.pos[0], Lt.pos[1], Lt.pos[2]);
+                if (dot(r.nrm, lp) < 0) continue;  // raytracer.cpp:155
+                const float4 so = make_float4(lp.x, lp.y, lp.z, 0.01f);
+                const float4 sd = make_float4(r.hitp.x, r.hitp.y, r.hitp.z,
+                                              length(v3(lp.x - r.hitp.x, lp.y - r.hitp.y, lp.z - r.hitp.z)));
+                float st = sd.w, su = 0.0f, sv = 0.0f;
+                int sprim = -1;
+                unsigned svis = 0, stest = 0;
+                trace8_group<G, COUNT>(s, so, sd, k, gshift, &gstk[0][gib], kGroups, st, su, sv, sprim, svis, stest);
+                if (COUNT && lead) {
+                    atomicAdd(&bst.shadow_vis, (unsigned long long)svis);
+                    atomicAdd(&bst.shadow_test, (unsigned long long)stest);
+                }
+                if (sprim < 0 || *at_bytes(s.prim_glass, (unsigned)sprim) != 0) {  // raytracer.cpp:163-173
+                    const float4 c = phong_term(m, Lt, r);
+                    blue += c.x;
+                    green += c.y;
+                    red += c.z;
+                }
+            }
+            val = make_float4(blue, green, red, 1.0f);
+        } else {
+            val = r.color;  // a miss (environment), a hit at max_level, an opaque hit with no lit candidate
+        }
+        // ---- deliver the colour up the tree: the last child of a frame settles it ----
+        for (;;) {
+            if (h == 0) {  // the root is final: k_combine(level - 1) reads its colour
+                if (lead) {
+                    const int i = root_i[t];
+                    st_stream(nodes.color + i, val);
+                    st_stream(nodes.link + i, make_int4(-1, -1, -1, 0));
+                    atomicOr(&s_free, 1ull << t);
+                    atomicSub(&s_busy, 1);
+                }
+                have = false;
+                break;
+            }
+            const int p = (h - 1) >> 1;
+            const int fi = t * NF + p;
+            if (h & 1) f_c0[fi] = val;
+            else f_c1[fi] = val;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            int old = 0;
+            if (lead) old = atomicAdd(&f_cnt[fi], 1);
+            old = __shfl(old, gshift, 64);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (old + 1 < f_nch[fi]) {  // the sibling is still being evaluated: it settles the frame
+                if (lead) atomicSub(&s_busy, 1);
+                have = false;
+                break;
+            }
+            const float4 att = f_att[fi];
+            const float4 c = f_nch[fi] == 2 ? mix_srgb(f_c0[fi], f_c1[fi], att.w) : f_c0[fi];  // raytracer.cpp:318-321
+            val = make_float4(c.x * att.x, c.y * att.y, c.z * att.z, 1);
+            h = p;
+        }
+    }
+    __syncthreads();
+    for (int l = tid; l < kMaxLevels; l += kSubtreeBlock) {
+        if (bst.alloc[l]) atomicAdd(&fc->alloc[l], bst.alloc[l]);
+        if (bst.refract[l]) atomicAdd(&fc->refract[l], bst.refract[l]);
+    }
+    if (COUNT && tid == 0) {
+        atomicAdd(&fc->trav[level][14], bst.trav_vis);
+        atomicAdd(&fc->trav[level][1], bst.trav_test);
+        atomicAdd(&fc->trav[kMaxLevels][14], bst.shadow_vis);
+        atomicAdd(&fc->trav[kMaxLevels][1], bst.shadow_test);
+        atomicAdd(&fc->shade[level][0], bst.hits);
+        atomicAdd(&fc->shade[level][1], bst.textured);
+    }
+    PGRT_STAMP_END(s.stamps);
+}
+
 #if PGRT_STEP_PROFILE
 // diagnostics build only: copy out (and optionally reset) the per-tree step records
 extern "C" int pgrt_diag_step_profile(unsigned long long* out, int max_records, int* n, int reset) {
@@ -274,6 +583,14 @@ extern "C" int pgrt_diag_step_profile(unsigned long long* out, int max_records, 
 
 bool subtree_available(const SceneView& s) { return s.depth8 + 1 <= kGroupStack; }
 
+// PGRT_COOP_WATCHDOG (diagnostics): a coop wave past 2^20 loop iterations prints its block's state and stops
+// PGRT_SUBTREE_COOP (A/B switch, compile time): 1 = the cooperative kernel where it applies
+#ifndef PGRT_SUBTREE_COOP
+#define PGRT_SUBTREE_COOP 0
+#endif
+constexpr size_t kCoopLdsBytes = 48 * 1024;
+static bool subtree_coop_enabled() { return PGRT_SUBTREE_COOP != 0; }
+
 void launch_subtree(const SceneView& s_in, const FrameParams& fp, int level, Queue q, LevelNodes nodes,
                     FrameCounters* fc, int max_count, int expect, bool count, hipStream_t stream) {
     if (max_count <= 0) return;
@@ -286,6 +603,22 @@ void launch_subtree(const SceneView& s_in, const FrameParams& fp, int level, Que
     SceneView s = s_in;
     s.stamps = stamp_next(kStampSubtree, level, grid, kSubtreeBlock);
     const bool tables = s.nmat <= kLdsMats && s.ntex <= kLdsTex;
+    // cooperative trees: depth <= kCoopMaxDepth and their frames within kCoopLdsBytes
+    const size_t coop_lds = (size_t)groups * ((1u << frames) - 1u) * kCoopFrameBytes;
+    if (subtree_coop_enabled() && frames <= kCoopMaxDepth && coop_lds <= kCoopLdsBytes) {
+#define PGRT_LAUNCH_COOP(G, T, C)                                                                                  \
+    hipLaunchKernelGGL((k_subtree_coop<G, T, C>), dim3(grid), dim3(kSubtreeBlock), coop_lds, stream, s, fp, level, q, \
+                       nodes, fc, frames)
+        if (count) {
+            if (g4) { if (tables) PGRT_LAUNCH_COOP(4, true, true); else PGRT_LAUNCH_COOP(4, false, true); }
+            else { if (tables) PGRT_LAUNCH_COOP(8, true, true); else PGRT_LAUNCH_COOP(8, false, true); }
+        } else {
+            if (g4) { if (tables) PGRT_LAUNCH_COOP(4, true, false); else PGRT_LAUNCH_COOP(4, false, false); }
+            else { if (tables) PGRT_LAUNCH_COOP(8, true, false); else PGRT_LAUNCH_COOP(8, false, false); }
+        }
+#undef PGRT_LAUNCH_COOP
+        return;
+    }
 #define PGRT_LAUNCH_SUB(G, T, C)                                                                                       \
     hipLaunchKernelGGL((k_subtree<G, T, C>), dim3(grid), dim3(kSubtreeBlock), lds, stream, s, fp, level, q, nodes, fc, \
                        frames)

@@ -9,9 +9,9 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-PGRT_LIB=ablib/stepprof/libpgrt.so timeout -k 10 200 python3 tools/step_profile.py --out gpurun_out/step_profile_r6c.json > gpurun_out/step_profile_r6c.log 2>&1 || { tail -20 gpurun_out/step_profile_r6c.log; exit 1; }
+PGRT_LIB=ablib/stepprof/libpgrt.so timeout -k 10 90 python3 tools/step_profile.py --out gpurun_out/step_profile_r6c.json > gpurun_out/step_profile_r6c.log 2>&1 || { tail -20 gpurun_out/step_profile_r6c.log; exit 1; }
 head -c 3000 gpurun_out/step_profile_r6c.json
-DIAG_CFG=subtree_level=-1 timeout -k 10 200 python3 tools/diag.py > gpurun_out/diag_r6c_one_lane.txt 2>&1 || { tail -20 gpurun_out/diag_r6c_one_lane.txt; exit 1; }
+DIAG_CFG=subtree_level=-1 timeout -k 10 90 python3 tools/diag.py > gpurun_out/diag_r6c_one_lane.txt 2>&1 || { tail -20 gpurun_out/diag_r6c_one_lane.txt; exit 1; }
 tail -8 gpurun_out/diag_r6c_one_lane.txt
 OUT=gpurun_out/pmc_r6c
 mkdir -p $OUT
@@ -25,3 +25,10 @@ for grp in "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_A
 done
 python3 tools/pmc_summary.py "$OUT" > "$OUT/summary.txt" 2>&1
 grep -E "k_subtree|k_trace|k_shade" "$OUT/summary.txt" | head -40
+# the bench line with the r6 roofline changes (level-0 byte charge from the launched kernels, frac rule)
+timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 > gpurun_out/bench_r6c_C2_k20.json 2> gpurun_out/bench_r6c_C2_k20.err || { tail -5 gpurun_out/bench_r6c_C2_k20.err; exit 1; }
+python3 -c "import json; d=json.load(open('gpurun_out/bench_r6c_C2_k20.json')); r=d['roofline']; print('driver line', d['ms_per_step'], 'lat', d.get('frame_latency_ms'), 'frac', r['frac'], r['frac_source'], r['level0_kernels'], r['level0_bytes_per_ray'], 'frame', r['frame']['frac'])"
+for r in 1 2; do
+  timeout -k 10 120 build/pg1_pgrt bench assets/avenger/6887_allied_avenger_proxy.obj assets/spherical_map_windows.jpg 20 5 > gpurun_out/cpp_dropin_r6c_k20_$r.json 2> gpurun_out/cpp_dropin_r6c.err || { tail -5 gpurun_out/cpp_dropin_r6c.err; exit 1; }
+  cat gpurun_out/cpp_dropin_r6c_k20_$r.json
+done

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--frames", type=int, default=3, help="synchronous frames (the last one is recorded)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--cfg", action="append", default=[])
+    ap.add_argument("--shade", action="store_true",
+                    help="instead: per-wave phase cycles of k_shade over the driver's 20 frames (calls of 8 in flight)")
     args = ap.parse_args()
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
     import scenes
@@ -47,6 +49,8 @@ def main():
         sys.exit("this libpgrt.so is not the PGRT_STEP_PROFILE build (set PGRT_LIB=ablib/stepprof/libpgrt.so)")
     L.pgrt_diag_step_profile.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.c_int]
     p = abi.make_params(spp_side=1, max_level=5)
+    if args.shade:
+        return shade_report(ctx, abi, p, args.out)
     fb = ctx.alloc(1920 * 1080 * 16)
     ctx.set_frames_in_flight(1)
     n = C.c_int(0)
@@ -123,6 +127,86 @@ def main():
     print(txt)
     if args.out:
         with open(args.out, "w") as f:
+            f.write(txt + "\n")
+
+
+def shade_report(ctx, abi, p, out):
+    """k_shade per wave and iteration: cycles of part A (hit, attributes, normal, material, child
+    directions), the allocation's first barrier + atomic issue, part B (environment / texel fetch,
+    attenuation, R), the allocation's second barrier, the emit -- by level and by the wave's mix of
+    ray kinds (verdict r5 #3: why a bounce-level ray costs more than a level-0 ray)."""
+    L = ctx.L
+    if not hasattr(L, "pgrt_diag_shade_profile"):
+        sys.exit("this libpgrt.so is not the PGRT_STEP_PROFILE build")
+    L.pgrt_diag_shade_profile.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.c_int]
+    W, H, F, inflight = 1920, 1080, 8, 8
+    fb = ctx.alloc(inflight * F * W * H * 16)
+    ctx.set_frames_in_flight(inflight)
+    frame = [0]
+
+    def run(nframes):
+        pend = []
+        k = 0
+        while nframes > 0:
+            nf = min(F, nframes)
+            pc = abi.RenderParams.from_buffer_copy(p)
+            pc.jitter = abi.PGRT_JITTER_HASH
+            pc.frame = frame[0]
+            frame[0] += nf
+            pend.append(ctx.render_frames_device_async(pc, nf, fb + (k % inflight) * F * W * H * 16))
+            k += 1
+            nframes -= nf
+            if len(pend) >= inflight:
+                ctx.render_wait(pend.pop(0))
+        for t in pend:
+            ctx.render_wait(t)
+
+    n = C.c_int(0)
+    run(inflight * F)
+    run(5)
+    ctx.synchronize()
+    L.pgrt_diag_shade_profile(None, 0, C.byref(n), 1)
+    run(20)
+    ctx.synchronize()
+    L.pgrt_diag_shade_profile(None, 0, C.byref(n), 0)
+    cnt = min(n.value, 1 << 20)
+    rec = np.zeros((cnt, 4), np.uint64)
+    L.pgrt_diag_shade_profile(rec.ctypes.data, cnt, C.byref(n), 0)
+    lo = lambda x: (x & np.uint64(0xFFFFFFFF)).astype(np.float64)
+    hi = lambda x: (x >> np.uint64(32)).astype(np.float64)
+    level = (rec[:, 0] & np.uint64(0xFF)).astype(np.int64)
+    act = ((rec[:, 0] >> np.uint64(8)) & np.uint64(0xFF)).astype(np.int64)
+    miss = ((rec[:, 0] >> np.uint64(16)) & np.uint64(0xFF)).astype(np.int64)
+    diel = ((rec[:, 0] >> np.uint64(24)) & np.uint64(0xFF)).astype(np.int64)
+    opq = ((rec[:, 0] >> np.uint64(32)) & np.uint64(0xFF)).astype(np.int64)
+    ph = np.stack([lo(rec[:, 1]), hi(rec[:, 1]), lo(rec[:, 2]), hi(rec[:, 2]), lo(rec[:, 3])], 1)
+    tot = hi(rec[:, 3])
+    names = ["part_a", "alloc_begin", "part_b", "alloc_end", "emit"]
+    rep = {"wave_iterations": int(cnt), "note": "shader-clock cycles per wave and shading iteration (diagnostics build; "
+           "s_memtime stamps add ~10%)", "levels": []}
+    for lv in sorted(set(level.tolist())):
+        m = (level == lv) & (act > 0)
+        if not m.any():
+            continue
+        kinds = (miss[m] > 0).astype(int) + 2 * (diel[m] > 0).astype(int) + 4 * (opq[m] > 0).astype(int)
+        mix = {}
+        for code, name in ((1, "miss only"), (2, "dielectric only"), (4, "opaque only"), (3, "miss+dielectric"),
+                           (5, "miss+opaque"), (6, "dielectric+opaque"), (7, "all three")):
+            sel = kinds == code
+            if sel.any():
+                mix[name] = {"waves": int(sel.sum()), "cycles_mean": round(float(tot[m][sel].mean()), 0),
+                             "phase_mean": {nm: round(float(ph[m][sel][:, j].mean()), 0) for j, nm in enumerate(names)}}
+        rep["levels"].append({
+            "level": int(lv), "wave_iterations": int(m.sum()), "rays": int(act[m].sum()),
+            "rays_miss_dielectric_opaque": [int(miss[m].sum()), int(diel[m].sum()), int(opq[m].sum())],
+            "cycles_per_wave_iteration": round(float(tot[m].mean()), 0),
+            "cycles_per_ray": round(float(tot[m].sum() / act[m].sum()), 1),
+            "phase_share": {nm: round(float(ph[m][:, j].sum() / tot[m].sum()), 3) for j, nm in enumerate(names)},
+            "by_wave_mix": mix})
+    txt = json.dumps(rep, indent=1)
+    print(txt)
+    if out:
+        with open(out, "w") as f:
             f.write(txt + "\n")
 
 
