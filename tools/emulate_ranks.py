@@ -106,7 +106,10 @@ def main():
         print(json.dumps(rec), flush=True)
         lines.append(rec)
         for n in [int(x) for x in args.worlds.split(",")]:
-            ranks = [run_child(config, n, r) for r in range(n)]
+            ranks = []
+            for r in range(n):  # one line per rank child (a long silent run looks hung to the box's guard)
+                ranks.append(run_child(config, n, r))
+                print(f"# {config} world {n} rank {r}: {ranks[-1]['ms_per_frame']:.4f} ms/frame", flush=True)
             ms = [r["ms_per_frame"] for r in ranks]
             slow = max(ms)
             rec = {"config": config, "world": n, "emulated": True,
