@@ -804,7 +804,11 @@ void frame_stats(pgrt_ctx* ctx, FrameSet* fs, int retries) {
 void finish_frame(pgrt_ctx* ctx, FrameSet* fs) {
     fs->pending = false;
     collect_frame(ctx, fs);  // a distributed frame's gather was queued at submission
-    PGRT_HIP(hipEventRecord(fs->ev_ready, ctx->stream));
+    // a distributed frame's set is free once its own gather has read the tiles: gather_end recorded
+    // ev_ready right behind it (also after a re-render's gather).  Recording it here again would put
+    // the gathers of every frame submitted since in front of the set's next frame -- the frames in
+    // flight would drain before each distributed call could start.
+    if (!fs->distributed) PGRT_HIP(hipEventRecord(fs->ev_ready, ctx->stream));
     fs->has_result = true;
     fs->stats.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - fs->t0).count();
 }

@@ -54,6 +54,10 @@ __device__ unsigned long long g_step_rec[kStepRecs][kStepWords];
 __device__ unsigned g_step_count;
 #endif
 
+#ifndef PGRT_SUBTREE_SPREAD
+#define PGRT_SUBTREE_SPREAD 0
+#endif
+
 template <int G, bool LDS_TABLES, bool COUNT>
 #ifndef PGRT_SUBTREE_WAVES
 #define PGRT_SUBTREE_WAVES 1
@@ -91,7 +95,11 @@ __global__ __launch_bounds__(kSubtreeBlock, PGRT_SUBTREE_WAVES) void k_subtree(S
     const int n = min(fc_count(*fc, level), q.cap);
     const float4 no_hit_h = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
     (void)no_hit_h;
-    for (int i = blockIdx.x * kGroups + gib; i < n; i += gridDim.x * kGroups) {
+    // PGRT_SUBTREE_SPREAD: tree i -> group i / grid of block i % grid, so the trees of a wave lie grid
+    // apart in the queue instead of adjacent (neighbouring pixels' trees are alike: a cluster of heavy
+    // trees no longer lands in one wave, whose groups run one after another where they diverge)
+    const int first = PGRT_SUBTREE_SPREAD ? gib * (int)gridDim.x + (int)blockIdx.x : (int)blockIdx.x * kGroups + gib;
+    for (int i = first; i < n; i += gridDim.x * kGroups) {
         float4 o4 = ld_stream(q.ro + i), d4 = ld_stream(q.rd + i);
         float rtime = ld_stream_nt(q.time + i);
         int sp = 0;  // pending dielectric frames; the ray being evaluated is of level `level + sp`

@@ -320,6 +320,34 @@ def test_distributed_world1_equals_render(gpu_ctx, avenger_scene):
     finally:
         gpu_ctx.set_frames_in_flight(1)
         gpu_ctx.free(buf)
+    # distributed calls in flight that reuse frame sets: a set's next frame waits for its own gather
+    # only (not for the gathers of the calls submitted after it), and every frame still lands intact
+    calls, F2 = 7, 2
+    refs = [gpu_ctx.render(abi.make_params(max_level=5, spp_side=1, jitter=abi.PGRT_JITTER_HASH, frame=f))[0]
+            for f in range(calls * F2)]
+    bufs = [gpu_ctx.alloc(F2 * 150 * 100 * 16) for _ in range(calls)]
+    try:
+        gpu_ctx.set_frames_in_flight(3)
+        pend = []
+
+        def check(c, t):
+            gpu_ctx.render_wait(t)
+            out = gpu_ctx.to_host(bufs[c], (F2, 100, 150, 4))
+            for f in range(F2):
+                ref = refs[c * F2 + f]
+                assert (np.nan_to_num(out[f], nan=5) == np.nan_to_num(ref, nan=5)).all(), f"call {c} frame {f}"
+
+        for c in range(calls):
+            if len(pend) == 3:
+                check(*pend.pop(0))
+            q = abi.make_params(max_level=5, spp_side=1, jitter=abi.PGRT_JITTER_HASH, frame=c * F2)
+            pend.append((c, gpu_ctx.render_frames_distributed_device_async(q, F2, bufs[c])))
+        for c, t in pend:
+            check(c, t)
+    finally:
+        gpu_ctx.set_frames_in_flight(1)
+        for b in bufs:
+            gpu_ctx.free(b)
 
 
 @pytest.mark.parametrize("ranks", [1, 2, 3, 8])

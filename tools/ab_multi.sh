@@ -14,8 +14,8 @@ for r in $(seq 1 "$RUNS"); do
   for S in "$@"; do
     lib=""; extra=""
     if [ "$S" = base ]; then name=base
-    elif [[ "$S" == *=* ]]; then name=${S%%=*}; extra=${S#*=}
     elif [[ "$S" == *@* ]]; then lib=${S%%@*}; extra=${S#*@}; name=$(basename "$(dirname "$lib")")+$(echo "$extra" | tr -d ' -')
+    elif [[ "$S" == *=* ]]; then name=${S%%=*}; extra=${S#*=}
     else lib=$S; name=$(basename "$(dirname "$S")"); fi
     if [ -n "$lib" ]; then export PGRT_LIB=$lib; else unset PGRT_LIB; fi
     timeout -k 10 200 python3 bench.py --no-cpu-baseline --no-roofline $ARGS $extra > "$OUT/b.json" 2> "$OUT/b.err" || { tail -5 "$OUT/b.err"; exit 1; }
