@@ -271,6 +271,10 @@ void probe_side_launch(pgrt_ctx* ctx, const SceneView& view, FrameSlot* sl, Fram
     pr.defer_count = &fcd->probe_defer;
     pr.resume = false;
     launch_trace(view, pr, s);
+    // one probe per re-probe period: the launch sits on the call's level chain (~0.1 ms at C2's level
+    // 3, as long as its slowest packet wave), and every call submitted before the next collect would
+    // otherwise probe as well (8 calls in flight: up to 8 probes per period)
+    ctx->probe_level = -1;
 }
 
 // How a host-output frame's pixels reach host memory (pgrt_config.host_export): per slot by the

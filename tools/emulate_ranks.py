@@ -10,7 +10,12 @@ imbalance), rank 0's unpack per frame, and the projected N-GPU time = the slowes
 the one-GPU time (world 1).  NOT included: the xGMI transfer into rank 0 (DESIGN.md §6 computes
 it) and RCCL itself -- RCCL at world > 1 is unmeasured on hardware (this pool has one GPU per box).
 
-usage: python tools/emulate_ranks.py [--configs C2,C4] [--worlds 2,4,8] [--out file.jsonl]
+Driver-shaped runs (--frames 20 --warmup 5 --repeat 5, optionally --fpc F): every rank times the same
+short job bench.py's N-GPU line times (20 frames after 5 warm-up frames, calls of F frames, the median
+of --repeat runs) -- the strong-scaling case, where one call's latency chain is a large part of the job.
+
+usage: python tools/emulate_ranks.py [--configs C2,C4] [--worlds 2,4,8] [--frames N --warmup W --repeat R]
+                                     [--fpc F] [--out file.jsonl]
 """
 import argparse
 import json
@@ -34,10 +39,20 @@ def child(config, world):
     from pgi_raytracing_amd import abi  # noqa: E402
     from pgi_raytracing_amd.raytracer import Context, load_obj  # noqa: E402
 
-    c = CFG[config]
+    c = dict(CFG[config])
+    if os.environ.get("EMU_FRAMES"):  # driver-shaped: a short job, warm-up frames, repeats
+        nfr, warm, rep = (int(x) for x in os.environ["EMU_FRAMES"].split(":"))
+        c["frames"] = lambda n: nfr
+    else:
+        nfr, warm, rep = None, None, 1
+    if os.environ.get("EMU_FPC"):
+        c["fpc"] = lambda n: int(os.environ["EMU_FPC"])
     sc = load_obj(scenes.AVENGER_OBJ)
     sc.set_environment(os.path.join(ROOT, "assets", "spherical_map_windows.jpg"))
     ctx = Context(0)
+    for kv in filter(None, os.environ.get("EMU_CFG", "").split(",")):  # pgrt_config overrides (--cfg)
+        k, v = kv.split("=", 1)
+        ctx.configure(**{k: int(v)})
     ctx.set_scene(sc)
     ctx.set_camera(abi.default_camera(c["W"], c["H"]))
     F = c["fpc"](world)
@@ -52,13 +67,14 @@ def child(config, world):
         for k in range(0, n, F):
             pc = abi.RenderParams.from_buffer_copy(p)
             pc.frame = k
-            pend.append(ctx.render_frames_distributed_device_async(pc, F, fb) if world > 1
-                        else ctx.render_frames_device_async(pc, F, fb))
+            nf = min(F, n - k)  # a short last call, as bench.py's (8 + 8 + 4 for 20 frames)
+            pend.append(ctx.render_frames_distributed_device_async(pc, nf, fb) if world > 1
+                        else ctx.render_frames_device_async(pc, nf, fb))
             if len(pend) >= c["in_flight"]:
                 st = ctx.render_wait(pend.popleft())
                 rays += st.rays()
                 if record and world > 1:
-                    unpack.append(st.ms_resolve / F)
+                    unpack.append(st.ms_resolve / F)  # (approximate for a short last call)
         while pend:
             st = ctx.render_wait(pend.popleft())
             rays += st.rays()
@@ -68,17 +84,29 @@ def child(config, world):
 
     run(c["in_flight"] * F)  # every frame set allocated before the timed region
     ctx.synchronize()
-    t = time.perf_counter()
-    rays = run(frames, record=True)
-    ctx.synchronize()
-    dt = time.perf_counter() - t
+    times = []
+    for _ in range(rep):
+        if warm:
+            run(warm)
+            ctx.synchronize()
+        t = time.perf_counter()
+        rays = run(frames, record=True)
+        ctx.synchronize()
+        times.append(time.perf_counter() - t)
+    dt = sorted(times)[len(times) // 2]
     print(json.dumps({"ms_per_frame": dt / frames * 1e3, "rays_per_frame": rays / frames, "frames": frames,
-                      "frames_per_call": F,
+                      "frames_per_call": F, "repeats": rep,
                       "unpack_ms_per_frame": (sum(unpack) / len(unpack)) if unpack else None}))
 
 
-def run_child(config, world, rank):
+def run_child(config, world, rank, args):
     env = dict(os.environ, EMU_CHILD=f"{config}:{world}", GPU_MAX_HW_QUEUES="16")
+    if args.frames:
+        env["EMU_FRAMES"] = f"{args.frames}:{args.warmup}:{args.repeat}"
+    if args.fpc:
+        env["EMU_FPC"] = str(args.fpc)
+    if args.cfg:
+        env["EMU_CFG"] = ",".join(args.cfg)
     if world > 1:
         env["PGRT_EMULATE_RANK"] = f"{rank}/{world}"
     else:
@@ -97,22 +125,30 @@ def main():
     ap.add_argument("--configs", default="C2,C4")
     ap.add_argument("--worlds", default="2,4,8")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--frames", type=int, default=None, help="timed frames per run (driver-shaped: 20)")
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--repeat", type=int, default=5)
+    ap.add_argument("--fpc", type=int, default=None, help="frames per call (default: CFG's rule)")
+    ap.add_argument("--cfg", action="append", default=[], help="pgrt_config override key=int (repeatable)")
     args = ap.parse_args()
     lines = []
     for config in args.configs.split(","):
-        one = run_child(config, 1, 0)
-        rec = {"config": config, "world": 1, "ms_per_frame": round(one["ms_per_frame"], 4),
+        one = run_child(config, 1, 0, args)
+        shape = {"frames": args.frames, "warmup": args.warmup, "repeat": args.repeat} if args.frames else "steady"
+        if args.cfg or args.fpc:
+            shape = {"shape": shape, "cfg": args.cfg, "fpc": args.fpc}
+        rec = {"config": config, "world": 1, "ms_per_frame": round(one["ms_per_frame"], 4), "job": shape,
                "rays_per_frame": one["rays_per_frame"], "frames_per_call": one["frames_per_call"]}
         print(json.dumps(rec), flush=True)
         lines.append(rec)
         for n in [int(x) for x in args.worlds.split(",")]:
             ranks = []
             for r in range(n):  # one line per rank child (a long silent run looks hung to the box's guard)
-                ranks.append(run_child(config, n, r))
+                ranks.append(run_child(config, n, r, args))
                 print(f"# {config} world {n} rank {r}: {ranks[-1]['ms_per_frame']:.4f} ms/frame", flush=True)
             ms = [r["ms_per_frame"] for r in ranks]
             slow = max(ms)
-            rec = {"config": config, "world": n, "emulated": True,
+            rec = {"config": config, "world": n, "emulated": True, "job": shape,
                    "rank_ms_per_frame": [round(x, 4) for x in ms],
                    "rank_rays_per_frame": [int(r["rays_per_frame"]) for r in ranks],
                    "max_over_mean": round(slow / (sum(ms) / n), 3),
