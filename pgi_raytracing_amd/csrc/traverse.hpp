@@ -202,27 +202,8 @@ __device__ __forceinline__ void trace8_group(const SceneView& s, float4 o4, floa
     unsigned gbase = 0, gbits = (1u << (24 + oct)) | 1u;  // the root: slot 0 of a virtual parent
     if (!(tfar >= 0.0f)) gbits = 0;
     unsigned tbase = 0, tbits = 0;
-#if PGRT_COOP_WATCHDOG
-    unsigned wd_steps = 0;
-#endif
     for (;;) {
-#if PGRT_COOP_WATCHDOG
-        if (++wd_steps > 100000u) {  // diagnostics: a traversal that never ends
-            if (k == 0)
-                printf("trace8_group watchdog: o %f %f %f tn %f d %f %f %f tf %f sp %d gbits %x tbits %x\n", ox, oy, oz,
-                       tnear, dx, dy, dz, tfar, sp, gbits, tbits);
-            break;
-        }
-#endif
         while (tbits == 0u) {  // ---- node phase (group-uniform) ----
-#if PGRT_COOP_WATCHDOG
-            if (++wd_steps > 100000u) {
-                if (k == 0)
-                    printf("trace8_group node-loop watchdog: o %f %f %f tn %f d %f %f %f tf %f sp %d gbits %x gbase %u\n",
-                           ox, oy, oz, tnear, dx, dy, dz, tfar, sp, gbits, gbase);
-                break;
-            }
-#endif
             long long pc0 = 0;
             if constexpr (PGRT_STEP_PROFILE) pc0 = clock64();  // (prof NULL: callers without a record)
             if (gbits <= 0x00ffffffu) {
