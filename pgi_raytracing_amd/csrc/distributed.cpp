@@ -408,7 +408,7 @@ void group_finish_set(pgrt_ctx* head, int si) {
         on_device(R[i]);
         FrameSet* fs = frame_set(R[i], si);
         frame_stats(R[i], fs, retries);
-        PGRT_HIP(hipEventRecord(fs->ev_ready, R[i]->stream));
+        // (the set's ready event stays behind its own gather, gather_end: see finish_frame)
         fs->has_result = true;
         const pgrt_stats& s = fs->stats;
         sum.rays_primary += s.rays_primary;
