@@ -10,3 +10,4 @@ for r in 1 2; do
   timeout -k 10 120 build/pg1_pgrt bench assets/avenger/6887_allied_avenger_proxy.obj assets/spherical_map_windows.jpg 20 5 > gpurun_out/cpp_dropin_r6fin_$r.out 2> gpurun_out/cpp_dropin_r6fin.err || { tail -5 gpurun_out/cpp_dropin_r6fin.err; exit 1; }
   tail -1 gpurun_out/cpp_dropin_r6fin_$r.out
 done
+bash tools/profile.sh r6finpath C2 --mode path --roofline-only || exit 1
