@@ -70,7 +70,7 @@ CONFIGS = {
 # (tools/profile.sh + tools/traffic.py, committed under profiles/)
 TRAFFIC = {"C2": "profiles/r6/r6fin/traffic_C2.json", "C3": "profiles/r6/r6fin/traffic_C3.json",
            "C4": "profiles/r6/r6fin/traffic_C4.json", "C5": "profiles/r6/r6fin/traffic_C5.json",
-           "C2-path": "profiles/r4/traffic_C2-path_r4v.json"}
+           "C2-path": "profiles/r6/r6fin/traffic_C2-path.json"}
 
 
 def parse():
