@@ -108,8 +108,8 @@ def parse():
     ap.add_argument("--in-flight", type=int, default=None,
                     help="calls in flight (pgrt_set_frames_in_flight); default 8 for C2, 6 otherwise")
     ap.add_argument("--frames-per-call", type=int, default=None,
-                    help="frames per submission (pgrt_render_frames_*_async, 1..64); default 8 x world for C2, "
-                         "1 otherwise (r1e scans)")
+                    help="frames per submission (pgrt_render_frames_*_async, 1..64); default for C2 8 x world, "
+                         "32 x world (at most 64) for jobs of >= 256 frames per rank; 1 otherwise")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (multi-thread leg)")
     ap.add_argument("--packet-levels", type=int, default=None,
                     help="A/B only: pgrt_config.packet_levels (default AUTO: chosen per level by libpgrt)")
@@ -333,7 +333,15 @@ def main():
     # rank's 1/world share at N GPUs); r1e scans: N=1 F=8 0.255 ms/frame (F=16 with 6 in flight
     # 0.39), emulated N=8 rank F=64 0.040 ms/frame (F=16 0.045)
     # (C3/C4/C5 frames are 15-250x heavier than C2's and fill the GPU on their own: 1 per call)
-    F = max(1, min(64, args.frames_per_call or (8 * world if args.config == "C2" else 1)))
+    # A long C2 job (>= 256 frames per rank) goes in calls of 32 frames' worth of rays per rank:
+    # fewer, wider launches per frame (r6q, 600 frames: 0.1413 -> 0.1333 ms/frame; 64 per call with
+    # 8 in flight does not fit one GPU's memory); a short one keeps 8 so several calls overlap (r6m:
+    # the driver's 20 frames in one call 0.183-0.189 vs 0.166 ms/frame in 8 + 8 + 4)
+    per_rank = 32 if args.steps >= 256 * world else 8
+    F = max(1, min(64, args.frames_per_call or (per_rank * world if args.config == "C2" else 1)))
+    # the profiled roofline calls and the host-framebuffer calls keep the short-job size (the
+    # committed rocprofv3 traffic is per 8-frame launch; 8 calls of 32 host frames would pin 8.5 GB)
+    F_aux = min(F, max(1, min(64, args.frames_per_call or (8 * world if args.config == "C2" else 1))))
     # calls in flight: a step is one whole frame (every rank's tiles rendered, gathered and
     # unpacked on rank 0); up to `in_flight` calls overlap on the device, so one call's
     # latency-bound deep levels share the CUs with the next call's wide levels
@@ -443,9 +451,9 @@ def main():
         # launch (profile=1), and the instrumented traversal counts (profile=2, separate call)
         # (1 GPU: the timed configuration, F frames per launch sequence; N GPUs: one frame)
         def prof_call(p):
-            return ctx.render_frames_device(p, F, fb) if world == 1 else frame(p)
+            return ctx.render_frames_device(p, F_aux, fb) if world == 1 else frame(p)
 
-        frames_per_prof = F if world == 1 else 1
+        frames_per_prof = F_aux if world == 1 else 1
         # level 0 on packets generates its rays in registers (k_trace_pkt<GEN>): 16-B direction
         # write instead of a 32-B ray read.  Whether it did is read off the launch timeline of one
         # unprofiled call of the same configuration (packets can be off by --packet-levels, --cfg
@@ -628,7 +636,7 @@ def main():
         # host-framebuffer figures (PCIe-inclusive; never the headline value).  SURVEY §8(d)'s
         # ms/frame: pgrt_render from camera upload to the framebuffer on the host, median of >= 10
         # frames after 2 warm-ups (into page-locked memory, as a D3D upload heap would be);
-        # throughput: pgrt_render_frames_host_async, F frames per call, their D2H copy (W*H*16 B
+        # throughput: pgrt_render_frames_host_async, F_aux frames per call, their D2H copy (W*H*16 B
         # per frame) queued behind them and overlapped with the calls in flight
         fb_host = ctx.host_array((args.height, args.width, 4))
         try:
@@ -644,15 +652,15 @@ def main():
             ctx.set_frames_in_flight(in_flight)
             ctx.host_free(fb_host)
         ring = min(in_flight, 4)
-        bufs = [ctx.host_array((F, args.height, args.width, 4)) for _ in range(ring)]
+        bufs = [ctx.host_array((F_aux, args.height, args.width, 4)) for _ in range(ring)]
         try:
             ctx.set_frames_in_flight(ring)
-            calls = max(2 * ring, 96 // F)
+            calls = max(2 * ring, 96 // F_aux)
 
             def host_calls(n):
                 pend = deque()
                 for k in range(n):
-                    pend.append(ctx.render_frames_host_async(params, F, bufs[k % ring]))
+                    pend.append(ctx.render_frames_host_async(params, F_aux, bufs[k % ring]))
                     if len(pend) >= ring:
                         ctx.render_wait(pend.popleft())
                 while pend:
@@ -669,11 +677,11 @@ def main():
         fb_bytes = args.width * args.height * 16
         host = {
             "ms_per_frame_sync_median": round(sorted(lat_h)[len(lat_h) // 2] * 1e3, 4),
-            "ms_per_frame_async": round(dt / (calls * F) * 1e3, 4),
-            "async_frames": calls * F,
+            "ms_per_frame_async": round(dt / (calls * F_aux) * 1e3, 4),
+            "async_frames": calls * F_aux,
             "async_calls_in_flight": ring,
             "frame_bytes": fb_bytes,
-            "pcie_d2h_gbs": round(calls * F * fb_bytes / dt / 1e9, 2),
+            "pcie_d2h_gbs": round(calls * F_aux * fb_bytes / dt / 1e9, 2),
             "note": "sync: SURVEY 8(d) definition (pgrt_render into a page-locked host framebuffer, median of "
                     f"{len(lat_h)} after 2 warm-ups); async: pgrt_render_frames_host_async throughput, bound by "
                     "the device-to-host copy of W*H*16 B per frame",
