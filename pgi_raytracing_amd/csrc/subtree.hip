@@ -54,9 +54,6 @@ __device__ unsigned long long g_step_rec[kStepRecs][kStepWords];
 __device__ unsigned g_step_count;
 #endif
 
-#ifndef PGRT_SUBTREE_REVERSE
-#define PGRT_SUBTREE_REVERSE 0
-#endif
 template <int G, bool LDS_TABLES, bool COUNT>
 #ifndef PGRT_SUBTREE_WAVES
 #define PGRT_SUBTREE_WAVES 1
@@ -94,9 +91,7 @@ __global__ __launch_bounds__(kSubtreeBlock, PGRT_SUBTREE_WAVES) void k_subtree(S
     const int n = min(fc_count(*fc, level), q.cap);
     const float4 no_hit_h = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
     (void)no_hit_h;
-    for (int slot = blockIdx.x * kGroups + gib; slot < n; slot += gridDim.x * kGroups) {
-        // PGRT_SUBTREE_REVERSE (A/B): the first blocks take the queue's last trees
-        const int i = PGRT_SUBTREE_REVERSE ? n - 1 - slot : slot;
+    for (int i = blockIdx.x * kGroups + gib; i < n; i += gridDim.x * kGroups) {
         float4 o4 = ld_stream(q.ro + i), d4 = ld_stream(q.rd + i);
         float rtime = ld_stream_nt(q.time + i);
         int sp = 0;  // pending dielectric frames; the ray being evaluated is of level `level + sp`
