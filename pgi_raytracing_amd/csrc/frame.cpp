@@ -7,6 +7,12 @@
 
 using namespace pgrt;
 
+// ShadowFinal (A/B switch, compile time): 1 = level-0 opaque pixels of 1-spp batches with one light
+// are completed by the shadow trace
+#ifndef PGRT_SHADOW_FINAL
+#define PGRT_SHADOW_FINAL 1
+#endif
+
 namespace pgrt {
 
 void ensure_frame_buffers(FrameSlot* sl, int n0, int levels, int nlight, int batches) {
@@ -508,8 +514,11 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                                    trace_launches);
                 continue;
             }
+            // one light over the binary BVH: the level-0 opaque pixels are completed by the shadow
+            // trace (ShadowFinal), the finish keeps the dielectric ones
+            const bool shadow_final = PGRT_SHADOW_FINAL && l0final && compact_shadow && p->max_level > 0;
             const L0Final l0f{l0final ? sl->l0_hit.p : nullptr, l0final ? sl->l0_pending.p : nullptr, fo,
-                              sl->tiles.p};
+                              sl->tiles.p, shadow_final ? 1 : 0};
             const PrimaryGen gen{ctx->cam, fp, sl->tiles.p, dir_only ? nullptr : q[0].ro, q[0].rd,
                                  dir_only ? nullptr : q[0].time, &fcd->count0, l0f.hit};
             int id = ctx->timer.begin(s, CAT_RAYGEN);
@@ -595,6 +604,13 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 if (compact_shadow) {
                     tl.const_org = make_float4(ctx->light0[0], ctx->light0[1], ctx->light0[2], 0.01f);
                     tl.lit = sq.lit;
+                }
+                if (shadow_final) {
+                    tl.sfin.contrib = sq.contrib;
+                    tl.sfin.n0 = fc_shadow_counts(fcd);  // level 0's count: the first term
+                    tl.sfin.fp = fp;
+                    tl.sfin.tiles = sl->tiles.p;
+                    tl.sfin.fo = fo;
                 }
                 id = ctx->timer.begin_kernel(CAT_TRACE, CAT_SHADOW);
                 const bool launched = launch_trace(view, tl, s);

@@ -202,11 +202,18 @@ __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : PGRT_SHADE_WAVE
         if constexpr (l0final) {
             // a final colour (environment texel; padding; a hit at max_level) -> the pixel, now;
             // the others are completed by the finish (n is a multiple of 64: whole waves)
-            const bool fin = active && r.kind == 0;
-            const unsigned long long pend = __ballot(active && !fin);
+            // shadow_final (one light): an opaque pixel without a shadow ray has its final colour
+            // too (k_finish would read it back from its node: nodes.color = r.color), and one with
+            // a shadow ray is completed by the shadow trace -- the finish keeps the dielectric ones
+            const bool opaque = r.kind == 2 && l0f.shadow_final;
+            const bool fin = active && (r.kind == 0 || (opaque && r.nshadow == 0));
+            const bool by_shadow = active && opaque && r.nshadow > 0;
+            const unsigned long long pend = __ballot(active && !fin && !by_shadow);
             if (active && __lane_id() == 0) st_stream_nt(l0f.pending + (i >> 6), pend);
             if (fin) store_final_1spp(fp, l0f.tiles, l0f.fo, i, r.color);
-            if (active && !fin) shade_emit(s, mats, level, i, r, sl, next, nodes, sq, fc);
+            if (active && !fin)
+                shade_emit(s, mats, level, i, r, sl, next, nodes, sq, fc, false, make_float4(0, 0, 0, 0),
+                           by_shadow ? i : -1);
         } else if (active) {
             shade_emit(s, mats, level, i, r, sl, next, nodes, sq, fc);
         }
@@ -365,16 +372,40 @@ __global__ __launch_bounds__(kBlock) void k_finish(SceneView s, FrameParams fp, 
 }
 
 // 1-spp batch whose level-0 shade finished every final-colour pixel (L0Final): the pixels of the
-// pending masks only
+// pending masks only.  PGRT_FINISH_WORDS > 1 (A/B): a wave reads that many mask words at once and
+// completes the pixels of its non-empty words one word after another (lane = pixel of the word)
+#ifndef PGRT_FINISH_WORDS
+#define PGRT_FINISH_WORDS 1
+#endif
+constexpr int kFinishWords = PGRT_FINISH_WORDS;
+
 __global__ __launch_bounds__(kBlock) void k_finish_pending(SceneView s, FrameParams fp, const int4* __restrict__ tiles,
                                                            LevelNodes l0, const float4* __restrict__ child,
                                                            ShadowQueue sq, FrameOut fo,
                                                            const unsigned long long* __restrict__ pending, int npix) {
     PGRT_STAMP_BEGIN(s.stamps);
-    const int p = blockIdx.x * kBlock + threadIdx.x;
-    if (p < npix) {
-        const unsigned long long pm = pending[__builtin_amdgcn_readfirstlane(p >> 6)];
-        if (((pm >> (p & 63)) & 1ull) != 0ull) store_final_1spp(fp, tiles, fo, p, node_color(s, sq, l0, child, p));
+    if constexpr (kFinishWords == 1) {
+        const int p = blockIdx.x * kBlock + threadIdx.x;
+        if (p < npix) {
+            const unsigned long long pm = pending[__builtin_amdgcn_readfirstlane(p >> 6)];
+            if (((pm >> (p & 63)) & 1ull) != 0ull) store_final_1spp(fp, tiles, fo, p, node_color(s, sq, l0, child, p));
+        }
+    } else {
+        const int nw = (npix + 63) >> 6;
+        const int w0 = (int)(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * kFinishWords;
+        const int lane = __lane_id();
+        const unsigned long long mine = lane < kFinishWords && w0 + lane < nw ? pending[w0 + lane] : 0ull;
+        unsigned long long nz = __ballot(mine != 0ull);  // the words with pending pixels
+        while (nz != 0ull) {
+            const int j = __builtin_ctzll(nz);
+            nz &= nz - 1ull;
+            const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)mine, j);
+            const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(mine >> 32), j);
+            const unsigned long long pm = ((unsigned long long)hi << 32) | lo;
+            const int p = (w0 + j) * 64 + lane;
+            if (((pm >> lane) & 1ull) != 0ull && p < npix)
+                store_final_1spp(fp, tiles, fo, p, node_color(s, sq, l0, child, p));
+        }
     }
     PGRT_STAMP_END(s.stamps);
 }
@@ -384,12 +415,14 @@ void launch_finish(const SceneView& s_in, const FrameParams& fp, const int4* til
                    const unsigned long long* pending, hipStream_t stream) {
     if (npix <= 0) return;
     SceneView s = s_in;
-    s.stamps = stamp_next(kStampFinish, 0, ceil_div(npix, kBlock), kBlock);
     if (pending) {
-        hipLaunchKernelGGL(k_finish_pending, dim3(ceil_div(npix, kBlock)), dim3(kBlock), 0, stream, s, fp, tiles, l0,
-                           child, sq, fo, pending, npix);
+        const int grid = ceil_div(ceil_div(npix, 64), kBlock / 64 * kFinishWords);
+        s.stamps = stamp_next(kStampFinish, 0, grid, kBlock);
+        hipLaunchKernelGGL(k_finish_pending, dim3(grid), dim3(kBlock), 0, stream, s, fp, tiles, l0, child, sq, fo,
+                           pending, npix);
         return;
     }
+    s.stamps = stamp_next(kStampFinish, 0, ceil_div(npix, kBlock), kBlock);
     hipLaunchKernelGGL(k_finish, dim3(ceil_div(npix, kBlock)), dim3(kBlock), 0, stream, s, fp, tiles, l0, child, sq,
                        accum, fo, npix, first ? 1 : 0, last ? 1 : 0, resolved ? 1 : 0);
 }

@@ -371,10 +371,11 @@ __device__ __forceinline__ int4 emit_children(int level, const ShadeOut& r, cons
 // Phase 3b for an active ray i: the node record (attenuation of a dielectric; an opaque hit's
 // shadow rays with their Phong terms; a final colour).  link: emit_children's result for a
 // dielectric.  use_pre0: light 0's Phong term is pre0 (computed earlier by the caller).
+// owner >= 0: the node's pixel, carried in the shadow rays' Phong terms (contrib.w; ShadowFinal)
 __device__ __forceinline__ void emit_node(const SceneView& s, const DevMaterial* mats, int i, const ShadeOut& r,
                                           const ShadeSlots& sl, int4 link, LevelNodes nodes, ShadowQueue sq,
                                           FrameCounters* fc, bool use_pre0 = false,
-                                          float4 pre0 = make_float4(0, 0, 0, 0)) {
+                                          float4 pre0 = make_float4(0, 0, 0, 0), int owner = -1) {
     if (r.kind == 1) {
         st_stream(nodes.att + i, r.att);
     } else if (r.kind == 2 && r.nshadow > 0) {
@@ -393,7 +394,9 @@ __device__ __forceinline__ void emit_node(const SceneView& s, const DevMaterial*
                 st_stream(sq.rd + k,
                           make_float4(hitp.x, hitp.y, hitp.z, length(v3(lp.x - hitp.x, lp.y - hitp.y, lp.z - hitp.z))));
                 // Phong term for this light (raytracer.cpp:355-382)
-                st_stream(sq.contrib + k, (use_pre0 && li == 0) ? pre0 : phong_term(m, L, r));
+                float4 c = (use_pre0 && li == 0) ? pre0 : phong_term(m, L, r);
+                if (owner >= 0) c.w = __int_as_float(owner);
+                st_stream(sq.contrib + k, c);
                 ++k;
             }
             link.z = sl.shadow;
@@ -408,9 +411,9 @@ __device__ __forceinline__ void emit_node(const SceneView& s, const DevMaterial*
 __device__ __forceinline__ void shade_emit(const SceneView& s, const DevMaterial* mats, int level, int i,
                                            const ShadeOut& r, const ShadeSlots& sl, Queue next, LevelNodes nodes,
                                            ShadowQueue sq, FrameCounters* fc, bool use_pre0 = false,
-                                           float4 pre0 = make_float4(0, 0, 0, 0)) {
+                                           float4 pre0 = make_float4(0, 0, 0, 0), int owner = -1) {
     const int4 link = r.kind == 1 ? emit_children(level, r, sl, next, fc) : make_int4(-1, -1, -1, 0);
-    emit_node(s, mats, i, r, sl, link, nodes, sq, fc, use_pre0, pre0);
+    emit_node(s, mats, i, r, sl, link, nodes, sq, fc, use_pre0, pre0, owner);
 }
 
 }  // namespace pgrt

@@ -54,10 +54,12 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
                                                        const int* __restrict__ count_dev, int count_terms,
                                                        int count_host, int cap, int* __restrict__ gstack,
                                                        unsigned long long* __restrict__ counters,
-                                                       float4 const_org, unsigned char* __restrict__ lit) {
+                                                       float4 const_org, unsigned char* __restrict__ lit,
+                                                       ShadowFinal sf) {
     PGRT_STAMP_BEGIN(s.stamps);
     chain_priority();
     extern __shared__ int lstack[];  // [entries][kTraceBlock]
+    const int n0 = sf.contrib ? *sf.n0 : 0;  // level-0 shadow rays (ShadowFinal)
     const int tid = threadIdx.x;
     const int lane = __lane_id();
     const int n = ray_count(count_dev, count_terms, count_host, cap);
@@ -202,9 +204,17 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
             }
             if (COUNT) rcyc_leaf += (unsigned long long)(clock64() - tl0);
         }
-        if (lit)  // is_illuminated (raytracer.cpp:163-173): no hit, or the occluder is dielectric
-            st_stream_nt(lit + i, (unsigned char)((best_prim < 0 || *at_bytes(s.prim_glass, (unsigned)best_prim) != 0) ? 1 : 0));
-        else
+        if (lit) {  // is_illuminated (raytracer.cpp:163-173): no hit, or the occluder is dielectric
+            const bool lv = best_prim < 0 || *at_bytes(s.prim_glass, (unsigned)best_prim) != 0;
+            st_stream_nt(lit + i, (unsigned char)(lv ? 1 : 0));
+            if (i < n0) {  // a level-0 pixel's only shadow ray: the pixel is final (ShadowFinal)
+                const float4 c = ld_stream(sf.contrib + i);
+                // opaque_color's sum over the one light (from 0: 0 + x), then get_pixel's
+                const float4 v = lv ? make_float4(0.0f + c.x, 0.0f + c.y, 0.0f + c.z, 1.0f)
+                                    : make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+                store_final_1spp(sf.fp, sf.tiles, sf.fo, __float_as_int(c.w), v);
+            }
+        } else
             st_stream(hits + i, make_float4(best_t, best_u, best_v, __int_as_float(best_prim)));
         if (COUNT) {
             const unsigned long long dt = (unsigned long long)(wall_clock64() - t_start);
@@ -818,7 +828,7 @@ bool launch_trace(const SceneView& s_in, const TraceLaunch& t, hipStream_t strea
     s.stamps = stamp_next(t.lit || !t.allow_group ? kStampTraceShadow : kStampTrace, t.level, grid, kTraceBlock);
 #define PGRT_LAUNCH(C, S)                                                                                      \
     PGRT_TLAUNCH((k_trace<C, S>), dim3(grid), dim3(kTraceBlock), lds, stream, s, t.ro, t.rd, t.hits, t.count_dev, \
-                 t.count_terms, t.count_host, max_count, t.gstack, t.counters, t.const_org, t.lit)
+                 t.count_terms, t.count_host, max_count, t.gstack, t.counters, t.const_org, t.lit, t.sfin)
     if (t.count) {
         if (spill) PGRT_LAUNCH(true, true); else PGRT_LAUNCH(true, false);
     } else {

@@ -119,6 +119,23 @@ struct L0Final {
     unsigned long long* pending;
     FrameOut fo;
     const int4* tiles;
+    // one light, compact shadow queue (ShadowFinal): an opaque pixel with a shadow ray is completed
+    // by the shadow trace (its pixel travels in the ray's Phong term), not by the finish; an opaque
+    // pixel without one has its final colour already and is written here like a miss
+    int shadow_final = 0;
+};
+
+// Level 0 of such a batch (L0Final.shadow_final): the shadow queue's first fc_shadow(0) rays are
+// the level-0 pixels' only shadow rays, contrib.w = the pixel's slot index.  The shadow trace
+// completes each of those pixels -- opaque_color (lit: the Phong term, else 0) and get_pixel's
+// sum and gamma (raytracer.cpp:163-173, 344-386, 422-435) -- so k_finish_pending is left with the
+// dielectric pixels.  contrib NULL: off.
+struct ShadowFinal {
+    const float4* contrib = nullptr;
+    const int* n0 = nullptr;  // &fc_shadow(0) (FrameCounters::alloc's high word of level 0)
+    FrameParams fp{};
+    const int4* tiles = nullptr;
+    FrameOut fo{};
 };
 
 struct LevelNodes {  // per-level node records kept until the combine pass
@@ -178,6 +195,7 @@ struct TraceLaunch {
     int* defer_count = nullptr;
     int defer_expect = 0;
     bool resume = true;  // false: the deferred rays are not finished (a side launch that only samples)
+    ShadowFinal sfin;    // the compact shadow queue of a 1-spp batch: level-0 pixels completed here
 };
 // the packet traversal needs the binary layout and a tree that fits its wave-uniform stack
 bool trace_packets_available(const SceneView& s);
