@@ -12,6 +12,10 @@ using namespace pgrt;
 #ifndef PGRT_SHADOW_FINAL
 #define PGRT_SHADOW_FINAL 1
 #endif
+// ... and at every level below the subtree launch (the opaque nodes' colours; A/B switch)
+#ifndef PGRT_SHADOW_FINAL_ALL
+#define PGRT_SHADOW_FINAL_ALL 1
+#endif
 
 namespace pgrt {
 
@@ -517,6 +521,8 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
             // one light over the binary BVH: the level-0 opaque pixels are completed by the shadow
             // trace (ShadowFinal), the finish keeps the dielectric ones
             const bool shadow_final = PGRT_SHADOW_FINAL && l0final && compact_shadow && p->max_level > 0;
+            // ... and the opaque nodes of the deeper levels get their colour there (k_combine skips them)
+            const bool shadow_final_all = shadow_final && PGRT_SHADOW_FINAL_ALL;
             const L0Final l0f{l0final ? sl->l0_hit.p : nullptr, l0final ? sl->l0_pending.p : nullptr, fo,
                               sl->tiles.p, shadow_final ? 1 : 0};
             const PrimaryGen gen{ctx->cam, fp, sl->tiles.p, dir_only ? nullptr : q[0].ro, q[0].rd,
@@ -578,7 +584,7 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                 id = ctx->timer.begin(s, CAT_SHADE, CAT_LSHADE + L);
                 const PinholeOrigin l0{ctx->cam.from[0], ctx->cam.from[1], ctx->cam.from[2], L == 0 && dir_only ? 1 : 0};
                 launch_shade(view, fp, L, qc, qn, ln, sq, fcd, maxc, s, ex, l0,
-                             L == 0 ? l0f : L0Final{nullptr, nullptr, fo, nullptr});
+                             L == 0 ? l0f : L0Final{nullptr, nullptr, fo, nullptr, shadow_final_all ? 1 : 0});
                 debug_sync(s, "shade", L, bi);
                 ctx->timer.end(s, id);
                 if (ordered) {
@@ -611,6 +617,9 @@ void enqueue_frame(pgrt_ctx* ctx, FrameSet* fs) {
                     tl.sfin.fp = fp;
                     tl.sfin.tiles = sl->tiles.p;
                     tl.sfin.fo = fo;
+                    tl.sfin.levels = tl.count_terms;
+                    if (shadow_final_all)
+                        for (int L = 1; L < tl.count_terms && L < kMaxLevels; ++L) tl.sfin.colors[L] = sl->n_color[L]->p;
                 }
                 id = ctx->timer.begin_kernel(CAT_TRACE, CAT_SHADOW);
                 const bool launched = launch_trace(view, tl, s);

@@ -215,7 +215,9 @@ __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : PGRT_SHADE_WAVE
                 shade_emit(s, mats, level, i, r, sl, next, nodes, sq, fc, false, make_float4(0, 0, 0, 0),
                            by_shadow ? i : -1);
         } else if (active) {
-            shade_emit(s, mats, level, i, r, sl, next, nodes, sq, fc);
+            // ShadowFinal at every level: an opaque node's one shadow ray carries the node
+            shade_emit(s, mats, level, i, r, sl, next, nodes, sq, fc, false, make_float4(0, 0, 0, 0),
+                       l0f.shadow_final && r.kind == 2 && r.nshadow > 0 ? i : -1);
         }
 #if PGRT_STEP_PROFILE
         {

@@ -399,12 +399,14 @@ __device__ __forceinline__ void emit_node(const SceneView& s, const DevMaterial*
                 st_stream(sq.contrib + k, c);
                 ++k;
             }
-            link.z = sl.shadow;
-            link.w = r.nshadow;
+            if (owner < 0) {  // (owner >= 0: the shadow trace writes the colour, k_combine skips the node)
+                link.z = sl.shadow;
+                link.w = r.nshadow;
+            }
         }
     }
     st_stream(nodes.link + i, link);
-    if (link.x < 0 && link.z < 0) st_stream(nodes.color + i, r.color);  // else derived by k_finish
+    if (link.x < 0 && link.z < 0 && owner < 0) st_stream(nodes.color + i, r.color);  // else derived later
 }
 
 // Phase 3 for an active ray i.

@@ -207,12 +207,25 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
         if (lit) {  // is_illuminated (raytracer.cpp:163-173): no hit, or the occluder is dielectric
             const bool lv = best_prim < 0 || *at_bytes(s.prim_glass, (unsigned)best_prim) != 0;
             st_stream_nt(lit + i, (unsigned char)(lv ? 1 : 0));
-            if (i < n0) {  // a level-0 pixel's only shadow ray: the pixel is final (ShadowFinal)
+            if (sf.contrib) {  // ShadowFinal: the ray's owner is complete with this verdict
                 const float4 c = ld_stream(sf.contrib + i);
-                // opaque_color's sum over the one light (from 0: 0 + x), then get_pixel's
+                // opaque_color's sum over the one light (from 0: 0 + x)
                 const float4 v = lv ? make_float4(0.0f + c.x, 0.0f + c.y, 0.0f + c.z, 1.0f)
                                     : make_float4(0.0f, 0.0f, 0.0f, 1.0f);
-                store_final_1spp(sf.fp, sf.tiles, sf.fo, __float_as_int(c.w), v);
+                const int owner = __float_as_int(c.w);
+                if (i < n0) {  // a level-0 pixel: get_pixel's sum and gamma, to the framebuffer
+                    store_final_1spp(sf.fp, sf.tiles, sf.fo, owner, v);
+                } else if (sf.colors[1]) {  // a deeper node: its colour (the queue is level-major)
+                    int base = n0;
+                    float4* dst = nullptr;
+                    for (int L = 1; L < kMaxLevels; ++L) {
+                        if (L >= sf.levels) break;
+                        const int cnt = sf.n0[2 * L];
+                        if (!dst && i < base + cnt) dst = sf.colors[L];
+                        base += cnt;
+                    }
+                    if (dst) st_stream(dst + owner, v);
+                }
             }
         } else
             st_stream(hits + i, make_float4(best_t, best_u, best_v, __int_as_float(best_prim)));

@@ -130,12 +130,16 @@ struct L0Final {
 // completes each of those pixels -- opaque_color (lit: the Phong term, else 0) and get_pixel's
 // sum and gamma (raytracer.cpp:163-173, 344-386, 422-435) -- so k_finish_pending is left with the
 // dielectric pixels.  contrib NULL: off.
+// Levels 1 .. levels-1 likewise (colors[L] non-NULL): an opaque node's only shadow ray carries its
+// node index, and the shadow trace writes the node's colour (opaque_color), so k_combine skips it.
 struct ShadowFinal {
     const float4* contrib = nullptr;
-    const int* n0 = nullptr;  // &fc_shadow(0) (FrameCounters::alloc's high word of level 0)
+    const int* n0 = nullptr;  // &fc_shadow(0) (FrameCounters::alloc's high word of level 0), stride 2
     FrameParams fp{};
     const int4* tiles = nullptr;
     FrameOut fo{};
+    int levels = 0;                       // levels whose shadow rays are in the queue (count terms)
+    float4* colors[kMaxLevels] = {};      // colors[L]: level L's node colours (L >= 1), NULL: off
 };
 
 struct LevelNodes {  // per-level node records kept until the combine pass
