@@ -1,0 +1,12 @@
+#!/bin/bash
+# r6fin2 (part a): after ShadowFinal -- the C2 and C5 roofline profiles again (their closest-hit
+# launches changed: the shadow trace completes opaque pixels / nodes), the device timelines
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for c in C2 C5; do
+  bash tools/profile.sh r6fin2 $c || exit 1
+done
+timeout -k 10 300 python3 tools/frame_timeline.py --out gpurun_out/timeline_r6fin2.json > gpurun_out/timeline_r6fin2.txt 2>&1 || { tail -5 gpurun_out/timeline_r6fin2.txt; exit 1; }
+bash tools/steady_profile.sh r6fin2 || exit 1
