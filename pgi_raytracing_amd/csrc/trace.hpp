@@ -152,7 +152,8 @@ struct ShadowQueue {  // one per batch: the shadow rays of every level, level-ma
     float4* ro;       // NULL in the compact form (one light: every shadow ray starts at it)
     float4* rd;
     float4* hit;      // closest hits (full form); NULL in the compact form
-    float4* contrib;  // (blue, green, red, -) Phong term of the owning node for this light
+    float4* contrib;  // (blue, green, red, owner) Phong term of the owning node for this light; w = the
+                      // owner node as int bits when the shadow trace completes it (ShadowFinal), else unused
     int cap;
     // compact form (one light, binary BVH): the shadow trace writes is_illuminated's verdict
     // (raytracer.cpp:163-173: no hit, or a hit on a dielectric) as one byte per ray instead of a
