@@ -100,6 +100,8 @@ def parse():
                          "(no jitter, one framebuffer shared by every call) -- A/B only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the synchronous-frame latency after the timed region (profiles of the timed calls only)")
     ap.add_argument("--hw-queues", type=int, default=None,
                     help="A/B only: GPU_MAX_HW_QUEUES for this process (default: 16, as the C++ drop-in sets it; "
                          "HIP reads it at its first call, after this)")
@@ -428,7 +430,7 @@ def main():
     # (pgrt_config.tile_order), which needs one earlier frame of the same size (2 warm-ups)
     lat = []
     ctx.set_frames_in_flight(1)
-    for k in range(min(args.steps, 30) + 2):
+    for k in range(0 if args.no_latency else min(args.steps, 30) + 2):
         t1 = time.perf_counter()
         frame(params)
         if k >= 2:

@@ -1,6 +1,7 @@
 #!/bin/bash
 # rocprofv3 passes over the THROUGHPUT run of bench.py (frames in flight; not the synchronous
-# roofline calls): kernel trace, FETCH_SIZE, WRITE_SIZE -- then tools/throughput_breakdown.py.
+# roofline calls, and without the synchronous latency frames after the timed region: their
+# per-slot k_export_counters would count as calls in the breakdown's window -- fixed in r6): kernel trace, FETCH_SIZE, WRITE_SIZE -- then tools/throughput_breakdown.py.
 # usage: tools/steady_profile.sh <tag> [bench args...]   (default: C2, 400 frames)
 set -u
 cd "$(dirname "$0")/.."
@@ -18,7 +19,7 @@ for pass in trace fetch write sq sq2; do
     sq2) P="--kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC";;
   esac
   timeout -k 10 300 rocprofv3 $P -d "$OUT/$pass" -o $pass --output-format csv -- \
-      python3 bench.py --no-cpu-baseline --no-roofline $ARGS > "$OUT/$pass.log" 2>&1
+      python3 bench.py --no-cpu-baseline --no-roofline --no-latency $ARGS > "$OUT/$pass.log" 2>&1
   rc=$?
   echo "=== $pass rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$OUT/$pass.log"; exit $rc; fi
