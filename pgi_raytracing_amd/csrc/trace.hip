@@ -47,7 +47,9 @@ __device__ __forceinline__ int ray_count(const int* count_dev, int count_terms, 
 __device__ __noinline__ void spill_store(int* p, int v) { *p = v; }
 __device__ __noinline__ int spill_load(const int* p) { return *p; }
 
-template <bool COUNT, bool SPILL>
+// SFIN: the shadow queue of a ShadowFinal batch (its own instance: the completion code's registers
+// stay out of the deep levels' traversal kernel)
+template <bool COUNT, bool SPILL, bool SFIN>
 __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4* __restrict__ ro,
                                                        const float4* __restrict__ rd,
                                                        float4* __restrict__ hits,
@@ -59,7 +61,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
     PGRT_STAMP_BEGIN(s.stamps);
     chain_priority();
     extern __shared__ int lstack[];  // [entries][kTraceBlock]
-    const int n0 = sf.contrib ? *sf.n0 : 0;  // level-0 shadow rays (ShadowFinal)
+    const int n0 = SFIN ? *sf.n0 : 0;  // level-0 shadow rays (ShadowFinal)
     const int tid = threadIdx.x;
     const int lane = __lane_id();
     const int n = ray_count(count_dev, count_terms, count_host, cap);
@@ -207,7 +209,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
         if (lit) {  // is_illuminated (raytracer.cpp:163-173): no hit, or the occluder is dielectric
             const bool lv = best_prim < 0 || *at_bytes(s.prim_glass, (unsigned)best_prim) != 0;
             st_stream_nt(lit + i, (unsigned char)(lv ? 1 : 0));
-            if (sf.contrib) {  // ShadowFinal: the ray's owner is complete with this verdict
+            if constexpr (SFIN) {  // ShadowFinal: the ray's owner is complete with this verdict
                 const float4 c = ld_stream(sf.contrib + i);
                 // opaque_color's sum over the one light (from 0: 0 + x)
                 const float4 v = lv ? make_float4(0.0f + c.x, 0.0f + c.y, 0.0f + c.z, 1.0f)
@@ -839,13 +841,19 @@ bool launch_trace(const SceneView& s_in, const TraceLaunch& t, hipStream_t strea
     const bool spill = entries * kTraceBlock * 4 > 65536;
     const size_t lds = (size_t)(spill ? kLdsStack : entries) * kTraceBlock * sizeof(int);
     s.stamps = stamp_next(t.lit || !t.allow_group ? kStampTraceShadow : kStampTrace, t.level, grid, kTraceBlock);
-#define PGRT_LAUNCH(C, S)                                                                                      \
-    PGRT_TLAUNCH((k_trace<C, S>), dim3(grid), dim3(kTraceBlock), lds, stream, s, t.ro, t.rd, t.hits, t.count_dev, \
+#define PGRT_LAUNCH(C, S, F)                                                                                      \
+    PGRT_TLAUNCH((k_trace<C, S, F>), dim3(grid), dim3(kTraceBlock), lds, stream, s, t.ro, t.rd, t.hits, t.count_dev, \
                  t.count_terms, t.count_host, max_count, t.gstack, t.counters, t.const_org, t.lit, t.sfin)
-    if (t.count) {
-        if (spill) PGRT_LAUNCH(true, true); else PGRT_LAUNCH(true, false);
+    if (t.sfin.contrib && t.lit) {  // ShadowFinal: the compact shadow queue's own instance
+        if (t.count) {
+            if (spill) PGRT_LAUNCH(true, true, true); else PGRT_LAUNCH(true, false, true);
+        } else {
+            if (spill) PGRT_LAUNCH(false, true, true); else PGRT_LAUNCH(false, false, true);
+        }
+    } else if (t.count) {
+        if (spill) PGRT_LAUNCH(true, true, false); else PGRT_LAUNCH(true, false, false);
     } else {
-        if (spill) PGRT_LAUNCH(false, true); else PGRT_LAUNCH(false, false);
+        if (spill) PGRT_LAUNCH(false, true, false); else PGRT_LAUNCH(false, false, false);
     }
 #undef PGRT_LAUNCH
     return true;
