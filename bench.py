@@ -68,8 +68,8 @@ CONFIGS = {
 }
 # PMC-measured HBM traffic per closest-hit launch of the bench's profiled configuration
 # (tools/profile.sh + tools/traffic.py, committed under profiles/)
-TRAFFIC = {"C2": "profiles/r6/r6fin2/traffic_C2.json", "C3": "profiles/r6/r6fin/traffic_C3.json",
-           "C4": "profiles/r6/r6fin/traffic_C4.json", "C5": "profiles/r6/r6fin2/traffic_C5.json",
+TRAFFIC = {"C2": "profiles/r6/r6fin3/traffic_C2.json", "C3": "profiles/r6/r6fin/traffic_C3.json",
+           "C4": "profiles/r6/r6fin/traffic_C4.json", "C5": "profiles/r6/r6fin3/traffic_C5.json",
            "C2-path": "profiles/r6/r6fin/traffic_C2-path.json"}
 
 
