@@ -69,17 +69,6 @@ struct DevBuf {
     }
 };
 
-// Wave issue priority of the frame's critical chain (A/B switch): the bounce-level traces, the
-// ray-tree launch and the bounce-level shades raise their waves' priority with s_setprio, so a SIMD
-// that also holds bulk waves of another call (level-0 packet traces and shades) issues the chain's
-// dependent instructions first.  0 = off.
-#ifndef PGRT_CHAIN_PRIO
-#define PGRT_CHAIN_PRIO 0
-#endif
-__device__ __forceinline__ void chain_priority() {
-    if constexpr (PGRT_CHAIN_PRIO > 0) __builtin_amdgcn_s_setprio(PGRT_CHAIN_PRIO);
-}
-
 // ---- device-side scene layout (HBM) -------------------------------------------------------
 
 struct DevMaterial {  // 48 B, read through the scalar/vector cache

@@ -100,7 +100,6 @@ __global__ __launch_bounds__(kShadeBlock, L0F ? kShadeL0fWaves : PGRT_SHADE_WAVE
                                                        LevelNodes nodes, ShadowQueue sq, FrameCounters* fc,
                                                        PinholeOrigin l0, L0Final l0f) {
     PGRT_STAMP_BEGIN(s.stamps);
-    if (!L0F && level > 0) chain_priority();
     __shared__ float lut255[256];
     __shared__ DevMaterial smat[LDS_TABLES ? kLdsMats : 1];
     __shared__ DevTexture stex[LDS_TABLES ? kLdsTex : 1];
@@ -374,40 +373,16 @@ __global__ __launch_bounds__(kBlock) void k_finish(SceneView s, FrameParams fp, 
 }
 
 // 1-spp batch whose level-0 shade finished every final-colour pixel (L0Final): the pixels of the
-// pending masks only.  PGRT_FINISH_WORDS > 1 (A/B): a wave reads that many mask words at once and
-// completes the pixels of its non-empty words one word after another (lane = pixel of the word)
-#ifndef PGRT_FINISH_WORDS
-#define PGRT_FINISH_WORDS 1
-#endif
-constexpr int kFinishWords = PGRT_FINISH_WORDS;
-
+// pending masks only (with ShadowFinal: the dielectric ones)
 __global__ __launch_bounds__(kBlock) void k_finish_pending(SceneView s, FrameParams fp, const int4* __restrict__ tiles,
                                                            LevelNodes l0, const float4* __restrict__ child,
                                                            ShadowQueue sq, FrameOut fo,
                                                            const unsigned long long* __restrict__ pending, int npix) {
     PGRT_STAMP_BEGIN(s.stamps);
-    if constexpr (kFinishWords == 1) {
-        const int p = blockIdx.x * kBlock + threadIdx.x;
-        if (p < npix) {
-            const unsigned long long pm = pending[__builtin_amdgcn_readfirstlane(p >> 6)];
-            if (((pm >> (p & 63)) & 1ull) != 0ull) store_final_1spp(fp, tiles, fo, p, node_color(s, sq, l0, child, p));
-        }
-    } else {
-        const int nw = (npix + 63) >> 6;
-        const int w0 = (int)(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * kFinishWords;
-        const int lane = __lane_id();
-        const unsigned long long mine = lane < kFinishWords && w0 + lane < nw ? pending[w0 + lane] : 0ull;
-        unsigned long long nz = __ballot(mine != 0ull);  // the words with pending pixels
-        while (nz != 0ull) {
-            const int j = __builtin_ctzll(nz);
-            nz &= nz - 1ull;
-            const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)mine, j);
-            const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(mine >> 32), j);
-            const unsigned long long pm = ((unsigned long long)hi << 32) | lo;
-            const int p = (w0 + j) * 64 + lane;
-            if (((pm >> lane) & 1ull) != 0ull && p < npix)
-                store_final_1spp(fp, tiles, fo, p, node_color(s, sq, l0, child, p));
-        }
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p < npix) {
+        const unsigned long long pm = pending[__builtin_amdgcn_readfirstlane(p >> 6)];
+        if (((pm >> (p & 63)) & 1ull) != 0ull) store_final_1spp(fp, tiles, fo, p, node_color(s, sq, l0, child, p));
     }
     PGRT_STAMP_END(s.stamps);
 }
@@ -417,14 +392,12 @@ void launch_finish(const SceneView& s_in, const FrameParams& fp, const int4* til
                    const unsigned long long* pending, hipStream_t stream) {
     if (npix <= 0) return;
     SceneView s = s_in;
+    s.stamps = stamp_next(kStampFinish, 0, ceil_div(npix, kBlock), kBlock);
     if (pending) {
-        const int grid = ceil_div(ceil_div(npix, 64), kBlock / 64 * kFinishWords);
-        s.stamps = stamp_next(kStampFinish, 0, grid, kBlock);
-        hipLaunchKernelGGL(k_finish_pending, dim3(grid), dim3(kBlock), 0, stream, s, fp, tiles, l0, child, sq, fo,
-                           pending, npix);
+        hipLaunchKernelGGL(k_finish_pending, dim3(ceil_div(npix, kBlock)), dim3(kBlock), 0, stream, s, fp, tiles, l0,
+                           child, sq, fo, pending, npix);
         return;
     }
-    s.stamps = stamp_next(kStampFinish, 0, ceil_div(npix, kBlock), kBlock);
     hipLaunchKernelGGL(k_finish, dim3(ceil_div(npix, kBlock)), dim3(kBlock), 0, stream, s, fp, tiles, l0, child, sq,
                        accum, fo, npix, first ? 1 : 0, last ? 1 : 0, resolved ? 1 : 0);
 }

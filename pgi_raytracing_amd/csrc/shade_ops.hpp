@@ -77,18 +77,6 @@ struct TexTap {
     unsigned w1[3], w2[3];  // the two rows' aligned 12-byte windows (mode 1)
     unsigned k1, k2;        // byte shift of each window
 };
-// texel window loads: plain (default) or nontemporal (PGRT_TEXEL_NT, A/B: the env map's 24 MB then
-// streams through each XCD's L2 at low retention instead of evicting the traversal data)
-#ifndef PGRT_TEXEL_NT
-#define PGRT_TEXEL_NT 0
-#endif
-__device__ __forceinline__ unsigned ld_texel(const unsigned* p) {
-#if PGRT_TEXEL_NT
-    return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
-}
 __device__ __forceinline__ TexTap tex_fetch(const DevTexture& t, const unsigned char* pool, float u, float v) {
     TexTap q;
     q.x = u * (float)t.width;
@@ -116,12 +104,12 @@ __device__ __forceinline__ TexTap tex_fetch(const DevTexture& t, const unsigned 
         q.k2 = f2 & 3u;
         const unsigned* a = at_bytes(reinterpret_cast<const unsigned*>(pool), f1 & ~3u);
         const unsigned* b = at_bytes(reinterpret_cast<const unsigned*>(pool), f2 & ~3u);
-        q.w1[0] = ld_texel(a);
-        q.w1[1] = ld_texel(a + 1);
-        q.w1[2] = ld_texel(a + 2);
-        q.w2[0] = ld_texel(b);
-        q.w2[1] = ld_texel(b + 1);
-        q.w2[2] = ld_texel(b + 2);
+        q.w1[0] = a[0];
+        q.w1[1] = a[1];
+        q.w1[2] = a[2];
+        q.w2[0] = b[0];
+        q.w2[1] = b[1];
+        q.w2[2] = b[2];
         q.mode = 1;
     } else {
         q.mode = 2;

@@ -61,7 +61,6 @@ template <int G, bool LDS_TABLES, bool COUNT>
 __global__ __launch_bounds__(kSubtreeBlock, PGRT_SUBTREE_WAVES) void k_subtree(SceneView s, FrameParams fp, int level, Queue q,
                                                            LevelNodes nodes, FrameCounters* fc, int frames) {
     PGRT_STAMP_BEGIN(s.stamps);
-    chain_priority();
     constexpr int kGroups = kSubtreeBlock / G;
     __shared__ uint2 gstk[kGroupStack][kGroups];
     __shared__ float lut255[256];

@@ -59,7 +59,6 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(SceneView s, const float4
                                                        float4 const_org, unsigned char* __restrict__ lit,
                                                        ShadowFinal sf) {
     PGRT_STAMP_BEGIN(s.stamps);
-    chain_priority();
     extern __shared__ int lstack[];  // [entries][kTraceBlock]
     const int n0 = SFIN ? *sf.n0 : 0;  // level-0 shadow rays (ShadowFinal)
     const int tid = threadIdx.x;
@@ -423,7 +422,6 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace8g(SceneView s, const floa
                                                          const int* __restrict__ perm) {
     static_assert(G == 4 || G == 8, "lanes per ray");
     PGRT_STAMP_BEGIN(s.stamps);
-    chain_priority();
     constexpr int kGroups = kTraceBlock / G;
     __shared__ uint2 gstk[kGroupStack][kGroups];
     const int tid = threadIdx.x;
@@ -715,7 +713,6 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void k_trace_pkt(SceneView s, co
                                                            unsigned long long* __restrict__ util, int budget,
                                                            int* __restrict__ defer_list, int* __restrict__ defer_count) {
     PGRT_STAMP_BEGIN(s.stamps);
-    if constexpr (!GEN) chain_priority();
     __shared__ int wstack[kTraceBlock / 64][kPktStack];
     const int n = ray_count(count_dev, count_terms, count_host, cap);
     if constexpr (GEN) {
